@@ -1,0 +1,117 @@
+// zr_internal.h — data layout shared by the host runtime and the HIP kernels.
+// DESIGN.md §4 describes each buffer's HBM layout and the per-unit byte counts.
+#pragma once
+#include <stdint.h>
+
+namespace zr {
+
+constexpr int kTile = 32;          // screen-tile edge in pixels (one workgroup per tile)
+constexpr int kTileShift = 5;
+constexpr int kTilePixels = kTile * kTile;
+constexpr int kTileThreads = 256;  // 4 waves of 64
+constexpr int kSetupThreads = 256;
+
+enum Program : int32_t { kProgTriangle = 0, kProgFlat = 1, kProgBlinn = 2, kProgCount = 3 };
+
+// Visibility-key schemes: the per-pixel 64-bit atomicMin key
+// reproduces in-order Vulkan depth-test semantics independent of fragment order.
+enum DepthMode : int32_t {
+    kDepthLastWins = 0,     // no depth write (or ALWAYS/EQUAL): pre-test vs initial depth, last primitive wins
+    kDepthMinStrict = 1,    // LESS + write: min z, ties -> first
+    kDepthMinNonStrict = 2, // LESS_OR_EQUAL + write: min z, ties -> last
+    kDepthMaxStrict = 3,    // GREATER + write: max z, ties -> first
+    kDepthMaxNonStrict = 4, // GREATER_OR_EQUAL + write: max z, ties -> last
+    kDepthModeCount = 5,
+};
+
+// Per-primitive setup record, 64 B (4 x 16 B), written once by k_setup.
+// Vertices are oriented so that A2 > 0 (v1/v2 swapped when needed; flag bit 0).
+struct alignas(16) TriRecord {
+    int32_t X0, Y0, X1, Y1;   // 24.8 fixed-point framebuffer coordinates
+    int32_t X2, Y2;
+    float z0, dz1;            // z0, z1 - z0
+    float dz2, invA2;         // z2 - z0, 1 / (float)A2
+    float invw0, invw1;       // 1 / w_clip (perspective correction)
+    float invw2;
+    uint32_t bb0;             // px0 | py0 << 16  (inclusive pixel bbox, clipped)
+    uint32_t bb1;             // px1 | py1 << 16
+    uint32_t flags;           // bit0 swapped v1<->v2, bits1..3 edge bias (0 = top-left edge)
+};
+static_assert(sizeof(TriRecord) == 64, "TriRecord must be 64 B");
+
+enum : uint32_t { kFlagSwapped = 1u, kFlagBias0 = 2u, kFlagBias1 = 4u, kFlagBias2 = 8u };
+
+// Status words in host-mapped pinned memory (read by the runtime at sync points).
+enum StatusWord : uint32_t {
+    kStTotalPairs = 0,
+    kStOverflow = 1,
+    kStMaxPairs = 2,
+    kStTrianglesSetup = 3,
+    kStDroppedClip = 4,
+    kStWords = 16,
+};
+// Device-side counters (zeroed with the tile counts before each draw).
+enum CounterWord : uint32_t { kCtSetup = 0, kCtDropped = 1, kCtWords = 4 };
+
+struct DrawParams {
+    // vertex input (binding 0) and index buffer
+    const uint8_t* vb;
+    uint64_t vb_bytes;
+    const uint8_t* ib;
+    uint64_t ib_bytes;
+    uint32_t stride;
+    uint32_t nattr;
+    uint32_t attr_offset[4];
+    uint32_t index_size;      // 0 = non-indexed draw, 2 or 4
+    uint32_t first;           // first_index / first_vertex
+    int32_t vertex_offset;
+    uint32_t tris_per_instance;
+    uint32_t prims;           // tris_per_instance * instance_count
+    // viewport transform (Vulkan 1.3 §Controlling the Viewport)
+    float hw, hh, cx, cy, dr, dmin, dlo, dhi;
+    // fragment rectangle = scissor ∩ render area ∩ attachment (inclusive)
+    int32_t clip_x0, clip_y0, clip_x1, clip_y1;
+    uint32_t cull_mode;
+    int32_t front_face;
+    // attachments
+    uint32_t fb_w, fb_h;
+    int32_t color_format;
+    uint32_t color_bpp;       // 0 = no colour attachment
+    uint8_t* color;
+    float* depth;             // nullptr = no depth attachment
+    uint32_t write_mask;
+    int32_t ra_x0, ra_y0, ra_x1, ra_y1;  // render area ∩ attachment (inclusive)
+    uint32_t clear_color_enable;
+    uint32_t clear_color_packed;         // pre-encoded for 8-bit formats
+    float clear_color[4];
+    uint32_t clear_depth_enable;
+    float clear_depth;
+    uint32_t load_depth;      // initial depth from the attachment (LOAD)
+    // depth test
+    int32_t depth_mode;
+    int32_t depth_op;         // VkCompareOp for the LastWins pre-test
+    uint32_t depth_write_out; // write the winner's depth
+    // shading
+    int32_t program;
+    const float* time_ptr;    // Time.time uniform (device) or nullptr
+    // tiling / sharding
+    uint32_t tiles_x, tiles_y, shard_rank, shard_count, owned_rows, ntiles;
+    // scratch
+    TriRecord* records;
+    uint32_t* tri_ntiles;
+    uint32_t* tile_counts;    // [ntiles] followed by kCtWords counters
+    uint32_t* tile_offsets;   // exclusive scan; ends after k_bin
+    uint32_t* bins;
+    uint32_t bin_capacity;
+    uint32_t* status;         // host-mapped
+};
+
+// Launchers (zr_kernels.hip).  All enqueue on `stream`; no host synchronisation.
+struct KernelTimer;
+void launch_setup(const DrawParams& p, void* stream);
+void launch_scan(const DrawParams& p, void* stream);
+void launch_bin(const DrawParams& p, void* stream);
+void launch_tile(const DrawParams& p, void* stream);
+void launch_clear(const DrawParams& p, void* stream);
+
+}  // namespace zr

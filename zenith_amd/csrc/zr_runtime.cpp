@@ -1,0 +1,1204 @@
+// zr_runtime.cpp — host side of libzenith_raster: the C ABI in include/zenith_raster.h.
+//
+// Objects mirror zenith-rhi's (RenderDevice, Buffer, Texture, Shader, pipeline,
+// CommandEncoder, Fence); command buffers record like vkCmd* and are executed at
+// zr_submit by walking the recorded state machine and launching the HIP passes
+// of zr_kernels.hip on the device's stream.  No CPU fallback:
+// every draw runs the HIP kernels or returns an error.
+#include <hip/hip_runtime.h>
+
+#include <algorithm>
+#include <cstdio>
+#include <cstring>
+#include <map>
+#include <string>
+#include <vector>
+
+#include "zenith_raster.h"
+#include "zr_internal.h"
+#include "zr_shading.h"
+
+using namespace zr;
+
+namespace {
+
+thread_local std::string g_last_error = "";
+
+zr_result fail(zr_result code, const std::string& msg) {
+    g_last_error = msg;
+    return code;
+}
+
+#define ZR_HIP(expr)                                                                              \
+    do {                                                                                          \
+        hipError_t _e = (expr);                                                                   \
+        if (_e != hipSuccess) {                                                                   \
+            return fail(_e == hipErrorOutOfMemory ? ZR_ERROR_OUT_OF_DEVICE_MEMORY : ZR_ERROR_DEVICE_LOST, \
+                        std::string(#expr) + ": " + hipGetErrorString(_e));                       \
+        }                                                                                         \
+    } while (0)
+
+// ------------------------------------------------------------ shader registry
+
+struct ShaderEntry {
+    const char* file;
+    const char* entry;
+    uint32_t stage;
+    int32_t program;
+    int nbind;
+    zr_shader_binding bind[1];
+    int ninputs;
+    zr_vertex_input_attr inputs[4];
+};
+
+// Built-in stage variants.  triangle.slang is the reference's
+// (content/shaders/triangle.slang:3-8 inputs, :27-32 "Time" at set 0 / binding 0);
+// flat_color / blinn_phong are this repo's (content/shaders/).
+const ShaderEntry kShaders[] = {
+    {"triangle.slang", "vsmain", ZR_SHADER_STAGE_VERTEX, kProgTriangle, 0, {},
+     2, {{0, ZR_FORMAT_R32G32B32_SFLOAT}, {1, ZR_FORMAT_R32G32B32_SFLOAT}}},
+    {"triangle.slang", "psmain", ZR_SHADER_STAGE_FRAGMENT, kProgTriangle, 1,
+     {{"Time", 0, 0, ZR_DESCRIPTOR_TYPE_UNIFORM_BUFFER, 1, ZR_SHADER_STAGE_FRAGMENT}}, 0, {}},
+    {"flat_color.slang", "vsmain", ZR_SHADER_STAGE_VERTEX, kProgFlat, 0, {},
+     2, {{0, ZR_FORMAT_R32G32B32_SFLOAT}, {1, ZR_FORMAT_R32G32B32_SFLOAT}}},
+    {"flat_color.slang", "psmain", ZR_SHADER_STAGE_FRAGMENT, kProgFlat, 0, {}, 0, {}},
+    {"blinn_phong.slang", "vsmain", ZR_SHADER_STAGE_VERTEX, kProgBlinn, 0, {},
+     3, {{0, ZR_FORMAT_R32G32B32_SFLOAT}, {1, ZR_FORMAT_R32G32B32_SFLOAT}, {2, ZR_FORMAT_R32G32B32_SFLOAT}}},
+    {"blinn_phong.slang", "psmain", ZR_SHADER_STAGE_FRAGMENT, kProgBlinn, 0, {}, 0, {}},
+};
+
+std::string basename_of(const char* path) {
+    std::string p(path ? path : "");
+    const size_t s = p.find_last_of("/\\");
+    return s == std::string::npos ? p : p.substr(s + 1);
+}
+
+}  // namespace
+
+// ------------------------------------------------------------------ objects
+
+struct zr_shader_t {
+    int32_t program;
+    uint32_t stage;
+    std::string file, entry;
+    std::vector<zr_shader_binding> bindings;
+    std::vector<zr_vertex_input_attr> inputs;
+};
+
+struct zr_buffer_t {
+    zr_device* dev;
+    void* ptr;
+    uint64_t size;
+    bool external;
+    std::string name;
+};
+
+struct zr_texture_t {
+    zr_device* dev;
+    void* ptr;
+    uint32_t width, height;
+    int32_t format;
+    uint32_t bpp;
+    bool external;
+    std::string name;
+};
+
+struct zr_pipeline_t {
+    int32_t program;
+    bool has_fs;
+    uint32_t stride;
+    uint32_t nattr;
+    uint32_t attr_offset[4];
+    std::vector<zr_shader_binding> bindings;  // merged reflection
+    uint32_t cull_mode;
+    int32_t front_face;
+    bool has_depth_state;
+    zr_depth_stencil_desc ds;
+    uint32_t color_count;
+    zr_color_attachment_desc color;
+    int32_t color_format;
+    int32_t depth_format;
+};
+
+enum CmdType { C_BEGIN_RENDERING, C_END_RENDERING, C_BIND_PIPELINE, C_BIND_UNIFORM, C_SET_VIEWPORT, C_SET_SCISSOR,
+               C_BIND_VB, C_BIND_IB, C_DRAW, C_SET_SHARD };
+
+struct RenderingState {
+    zr_rect2d area;
+    bool has_color = false, has_depth = false;
+    zr_rendering_attachment color{}, depth{};
+};
+
+struct Cmd {
+    CmdType type;
+    RenderingState rendering;
+    const zr_pipeline* pipeline = nullptr;
+    const zr_buffer* buffer = nullptr;
+    uint64_t offset = 0, range = 0;
+    uint32_t a = 0, b = 0, c = 0, d = 0;
+    int32_t e = 0;
+    zr_viewport vp{};
+    zr_rect2d rect{};
+};
+
+struct zr_cmd_t {
+    zr_device* dev;
+    std::vector<Cmd> cmds;
+    zr_result err = ZR_SUCCESS;
+    std::string err_msg;
+    bool in_rendering = false;
+};
+
+struct zr_fence_t {
+    zr_device* dev;
+    hipEvent_t ev;
+    bool submitted = false;
+};
+
+struct TimedLaunch {
+    const char* name;
+    hipEvent_t start, stop;
+};
+
+struct zr_device_t {
+    int hip_device = 0;
+    hipStream_t stream = nullptr;
+    // scratch (grow-only)
+    TriRecord* records = nullptr;
+    uint64_t records_cap = 0;  // primitives
+    uint32_t* tri_ntiles = nullptr;
+    uint32_t* tile_counts = nullptr;
+    uint32_t* tile_offsets = nullptr;
+    uint64_t tiles_cap = 0;
+    uint32_t* bins = nullptr;
+    uint64_t bins_cap = 0;
+    uint32_t* status_host = nullptr;
+    uint32_t* status_dev = nullptr;
+    // replay + stats
+    std::vector<zr_cmd*> pending;
+    uint64_t replays = 0;
+    zr_draw_stats last{};
+    uint64_t last_prims = 0;
+    // profiling
+    bool profiling = false;
+    std::vector<TimedLaunch> timed;
+    std::vector<hipEvent_t> event_pool;
+    std::map<std::string, std::pair<double, uint64_t>> times;
+};
+
+// ------------------------------------------------------------ device helpers
+
+namespace {
+
+zr_result set_device(zr_device* d) {
+    ZR_HIP(hipSetDevice(d->hip_device));
+    return ZR_SUCCESS;
+}
+
+hipEvent_t take_event(zr_device* d) {
+    if (!d->event_pool.empty()) {
+        hipEvent_t e = d->event_pool.back();
+        d->event_pool.pop_back();
+        return e;
+    }
+    hipEvent_t e = nullptr;
+    if (hipEventCreate(&e) != hipSuccess) return nullptr;
+    return e;
+}
+
+void collect_timings(zr_device* d) {
+    for (auto& t : d->timed) {
+        float ms = 0.f;
+        if (hipEventElapsedTime(&ms, t.start, t.stop) == hipSuccess) {
+            auto& slot = d->times[t.name];
+            slot.first += ms;
+            slot.second += 1;
+        }
+        d->event_pool.push_back(t.start);
+        d->event_pool.push_back(t.stop);
+    }
+    d->timed.clear();
+}
+
+template <typename F>
+void timed_launch(zr_device* d, const char* name, F&& fn) {
+    if (!d->profiling) {
+        fn();
+        return;
+    }
+    TimedLaunch t{name, take_event(d), take_event(d)};
+    (void)hipEventRecord(t.start, d->stream);
+    fn();
+    (void)hipEventRecord(t.stop, d->stream);
+    d->timed.push_back(t);
+}
+
+template <typename T>
+zr_result grow(zr_device* d, T*& ptr, uint64_t& cap, uint64_t need, uint64_t elem_bytes) {
+    if (need <= cap && ptr) return ZR_SUCCESS;
+    ZR_HIP(hipStreamSynchronize(d->stream));
+    if (ptr) (void)hipFree(ptr);
+    ptr = nullptr;
+    uint64_t n = std::max<uint64_t>(need, 1024);
+    void* p = nullptr;
+    ZR_HIP(hipMalloc(&p, n * elem_bytes));
+    ptr = (T*)p;
+    cap = n;
+    return ZR_SUCCESS;
+}
+
+zr_result execute(zr_device* d, zr_cmd* cmd);
+
+zr_result device_sync(zr_device* d) {
+    zr_result rc = set_device(d);
+    if (rc) return rc;
+    for (int attempt = 0; attempt < 8; ++attempt) {
+        ZR_HIP(hipStreamSynchronize(d->stream));
+        collect_timings(d);
+        volatile uint32_t* st = d->status_host;
+        d->last.bin_pairs = st[kStTotalPairs];
+        d->last.triangles_setup = st[kStTrianglesSetup];
+        d->last.triangles_dropped_clip = st[kStDroppedClip];
+        d->last.bin_capacity = d->bins_cap;
+        d->last.replays = d->replays;
+        if (!st[kStOverflow]) {
+            d->pending.clear();
+            return ZR_SUCCESS;
+        }
+        // A draw produced more (tile, primitive) pairs than the bin buffer holds:
+        // grow it and replay every submission since the last sync, in order.
+        const uint64_t need = (uint64_t)st[kStMaxPairs] * 5 / 4 + 4096;
+        st[kStOverflow] = 0;
+        ZR_HIP(hipFree(d->bins));
+        d->bins = nullptr;
+        void* p = nullptr;
+        ZR_HIP(hipMalloc(&p, need * 4));
+        d->bins = (uint32_t*)p;
+        d->bins_cap = need;
+        d->replays++;
+        std::vector<zr_cmd*> again;
+        again.swap(d->pending);
+        for (zr_cmd* c : again) {
+            rc = execute(d, c);
+            if (rc) return rc;
+            d->pending.push_back(c);
+        }
+    }
+    return fail(ZR_ERROR_OUT_OF_DEVICE_MEMORY, "bin buffer overflow persisted after replays");
+}
+
+// ------------------------------------------------------------ draw execution
+
+struct VertexBinding {
+    const zr_buffer* buf = nullptr;
+    uint64_t offset = 0;
+};
+
+struct ExecState {
+    const zr_pipeline* pipe = nullptr;
+    bool vp_set = false, sc_set = false;
+    zr_viewport vp{};
+    zr_rect2d sc{};
+    VertexBinding vb[8];
+    const zr_buffer* ib = nullptr;
+    uint64_t ib_offset = 0;
+    int32_t index_type = 0;
+    std::map<std::pair<uint32_t, uint32_t>, std::pair<const zr_buffer*, uint64_t>> ubos;
+    bool rendering = false;
+    RenderingState rs;
+    bool color_clear_pending = false, depth_clear_pending = false;
+    uint32_t shard_rank = 0, shard_count = 1;
+};
+
+int32_t choose_depth_mode(bool test, bool write, int32_t op) {
+    if (!test) return kDepthLastWins;
+    if (write) {
+        switch (op) {
+        case 1: return kDepthMinStrict;
+        case 3: return kDepthMinNonStrict;
+        case 4: return kDepthMaxStrict;
+        case 6: return kDepthMaxNonStrict;
+        default: break;
+        }
+    }
+    return kDepthLastWins;
+}
+
+zr_result fill_target(const ExecState& s, DrawParams& P) {
+    const zr_texture* ct = s.rs.has_color ? s.rs.color.texture : nullptr;
+    const zr_texture* dt = s.rs.has_depth ? s.rs.depth.texture : nullptr;
+    if (!ct && !dt) return fail(ZR_ERROR_VALIDATION_FAILED, "render pass without attachments");
+    const zr_texture* ref = ct ? ct : dt;
+    if (ct && dt && (ct->width != dt->width || ct->height != dt->height))
+        return fail(ZR_ERROR_VALIDATION_FAILED, "colour and depth attachment extents differ");
+    if (dt && dt->format != ZR_FORMAT_D32_SFLOAT) return fail(ZR_ERROR_FORMAT_NOT_SUPPORTED, "depth format");
+    if (ct && format_bpp(ct->format) == 0) return fail(ZR_ERROR_FORMAT_NOT_SUPPORTED, "colour format");
+    P.fb_w = ref->width;
+    P.fb_h = ref->height;
+    P.color = ct ? (uint8_t*)ct->ptr : nullptr;
+    P.color_format = ct ? ct->format : 0;
+    P.color_bpp = ct ? ct->bpp : 0;
+    P.depth = dt ? (float*)dt->ptr : nullptr;
+    const int32_t ax0 = std::max(0, s.rs.area.x), ay0 = std::max(0, s.rs.area.y);
+    const int64_t ax1 = std::min<int64_t>((int64_t)s.rs.area.x + s.rs.area.width, P.fb_w) - 1;
+    const int64_t ay1 = std::min<int64_t>((int64_t)s.rs.area.y + s.rs.area.height, P.fb_h) - 1;
+    P.ra_x0 = ax0;
+    P.ra_y0 = ay0;
+    P.ra_x1 = (int32_t)ax1;
+    P.ra_y1 = (int32_t)ay1;
+    P.tiles_x = (P.fb_w + kTile - 1) / kTile;
+    P.tiles_y = (P.fb_h + kTile - 1) / kTile;
+    P.shard_rank = s.shard_rank;
+    P.shard_count = s.shard_count;
+    P.owned_rows = P.tiles_y > s.shard_rank ? (P.tiles_y - s.shard_rank + s.shard_count - 1) / s.shard_count : 0;
+    P.ntiles = P.owned_rows * P.tiles_x;
+    // clears (fused into the first draw of the pass, else k_clear at end_rendering)
+    P.clear_color_enable = (ct && s.color_clear_pending) ? 1u : 0u;
+    if (ct) {
+        for (int i = 0; i < 4; ++i) P.clear_color[i] = s.rs.color.clear_value[i];
+        P.clear_color_packed = pack_rgba8(P.clear_color, ct->format, kSrgbThresholds);
+    }
+    P.clear_depth_enable = (dt && s.depth_clear_pending) ? 1u : 0u;
+    P.clear_depth = dt ? s.rs.depth.clear_value[0] : 1.0f;
+    P.load_depth = (dt && !s.depth_clear_pending) ? 1u : 0u;
+    return ZR_SUCCESS;
+}
+
+zr_result ensure_scratch(zr_device* d, uint64_t prims, uint64_t ntiles) {
+    zr_result rc;
+    if (prims > d->records_cap || !d->records) {
+        uint64_t cap = d->records_cap, cap2 = d->records_cap;
+        if ((rc = grow(d, d->records, cap, prims, sizeof(TriRecord)))) return rc;
+        if ((rc = grow(d, d->tri_ntiles, cap2, prims, 4))) return rc;
+        d->records_cap = std::min(cap, cap2);
+    }
+    if (ntiles + kCtWords > d->tiles_cap || !d->tile_counts) {
+        uint64_t cap = d->tiles_cap, cap2 = d->tiles_cap;
+        if ((rc = grow(d, d->tile_counts, cap, ntiles + kCtWords, 4))) return rc;
+        if ((rc = grow(d, d->tile_offsets, cap2, ntiles + kCtWords, 4))) return rc;
+        d->tiles_cap = std::min(cap, cap2);
+    }
+    if (!d->bins) {
+        uint64_t cap = 0;
+        if ((rc = grow(d, d->bins, cap, std::max<uint64_t>(1u << 20, prims * 3), 4))) return rc;
+        d->bins_cap = cap;
+    }
+    return ZR_SUCCESS;
+}
+
+zr_result exec_draw(zr_device* d, ExecState& s, const Cmd& c, bool indexed) {
+    if (!s.rendering) return fail(ZR_ERROR_VALIDATION_FAILED, "draw outside begin_rendering/end_rendering");
+    const zr_pipeline* pp = s.pipe;
+    if (!pp) return fail(ZR_ERROR_VALIDATION_FAILED, "draw without a bound pipeline");
+    if (!s.vp_set || !s.sc_set)
+        return fail(ZR_ERROR_VALIDATION_FAILED, "dynamic viewport/scissor not set (pipeline.rs:734)");
+    if (pp->color_count != (s.rs.has_color ? 1u : 0u))
+        return fail(ZR_ERROR_VALIDATION_FAILED, "node colour targets do not match pipeline colour attachments");
+    if (!s.vb[0].buf) return fail(ZR_ERROR_VALIDATION_FAILED, "vertex buffer binding 0 not bound");
+    if (indexed && !s.ib) return fail(ZR_ERROR_VALIDATION_FAILED, "draw_indexed without an index buffer");
+
+    DrawParams P;
+    memset(&P, 0, sizeof P);
+    zr_result rc = fill_target(s, P);
+    if (rc) return rc;
+    if (!pp->has_fs) {
+        P.color = nullptr;
+        P.color_bpp = 0;
+    }
+    const uint64_t count = c.a, instances = c.b;
+    const uint64_t tpi = count / 3u;
+    const uint64_t prims = tpi * instances;
+    if (prims >= 0xFFFFFFFFull) return fail(ZR_ERROR_FEATURE_NOT_PRESENT, "more than 2^32-2 primitives in one draw");
+    if (P.fb_w > 16384 || P.fb_h > 16384) return fail(ZR_ERROR_FEATURE_NOT_PRESENT, "attachment larger than 16384");
+
+    const zr_buffer* vb = s.vb[0].buf;
+    P.vb = (const uint8_t*)vb->ptr + s.vb[0].offset;
+    P.vb_bytes = vb->size > s.vb[0].offset ? vb->size - s.vb[0].offset : 0;
+    P.stride = pp->stride;
+    P.nattr = pp->nattr;
+    for (int i = 0; i < 4; ++i) P.attr_offset[i] = pp->attr_offset[i];
+    if (indexed) {
+        P.ib = (const uint8_t*)s.ib->ptr + s.ib_offset;
+        P.ib_bytes = s.ib->size > s.ib_offset ? s.ib->size - s.ib_offset : 0;
+        P.index_size = s.index_type == ZR_INDEX_TYPE_UINT16 ? 2u : 4u;
+        P.first = c.c;
+        P.vertex_offset = c.e;
+    } else {
+        P.index_size = 0;
+        P.first = c.c;
+        P.vertex_offset = 0;
+    }
+    P.tris_per_instance = (uint32_t)tpi;
+    P.prims = (uint32_t)prims;
+    // viewport transform constants (Vulkan 1.3 §Controlling the Viewport)
+    P.hw = s.vp.width * 0.5f;
+    P.hh = s.vp.height * 0.5f;
+    P.cx = s.vp.x + P.hw;
+    P.cy = s.vp.y + P.hh;
+    P.dr = s.vp.max_depth - s.vp.min_depth;
+    P.dmin = s.vp.min_depth;
+    P.dlo = std::min(s.vp.min_depth, s.vp.max_depth);
+    P.dhi = std::max(s.vp.min_depth, s.vp.max_depth);
+    P.clip_x0 = std::max<int32_t>(s.sc.x, P.ra_x0);
+    P.clip_y0 = std::max<int32_t>(s.sc.y, P.ra_y0);
+    P.clip_x1 = (int32_t)std::min<int64_t>((int64_t)s.sc.x + s.sc.width - 1, P.ra_x1);
+    P.clip_y1 = (int32_t)std::min<int64_t>((int64_t)s.sc.y + s.sc.height - 1, P.ra_y1);
+    P.cull_mode = pp->cull_mode;
+    P.front_face = pp->front_face;
+    P.write_mask = pp->color.write_mask;
+    // depth
+    const bool has_depth = P.depth != nullptr;
+    const bool test = has_depth && pp->has_depth_state && pp->ds.depth_test_enable;
+    const bool write = test && pp->ds.depth_write_enable;
+    const int32_t op = test ? pp->ds.depth_compare_op : 7;
+    if (write && op == 5) return fail(ZR_ERROR_FEATURE_NOT_PRESENT, "NOT_EQUAL with depth writes");
+    P.depth_mode = choose_depth_mode(test, write, op);
+    P.depth_op = op;
+    P.depth_write_out = write ? 1u : 0u;
+    // shading
+    P.program = pp->program;
+    P.time_ptr = nullptr;
+    for (const auto& b : pp->bindings) {
+        auto it = s.ubos.find({b.set, b.binding});
+        if (it == s.ubos.end())
+            return fail(ZR_ERROR_VALIDATION_FAILED, std::string("descriptor '") + b.name + "' not bound");
+        if (pp->program == kProgTriangle && !strcmp(b.name, "Time")) {
+            if (it->second.second + 4 > it->second.first->size)
+                return fail(ZR_ERROR_VALIDATION_FAILED, "Time uniform range out of bounds");
+            P.time_ptr = (const float*)((const uint8_t*)it->second.first->ptr + it->second.second);
+        }
+    }
+    // scratch
+    if ((rc = ensure_scratch(d, prims, P.ntiles))) return rc;
+    P.records = d->records;
+    P.tri_ntiles = d->tri_ntiles;
+    P.tile_counts = d->tile_counts;
+    P.tile_offsets = d->tile_offsets;
+    P.bins = d->bins;
+    P.bin_capacity = (uint32_t)std::min<uint64_t>(d->bins_cap, 0xFFFFFFFFull);
+    P.status = d->status_dev;
+    d->last_prims = prims;
+    d->last.triangles_in = prims;
+
+    ZR_HIP(hipMemsetAsync(P.tile_counts, 0, (P.ntiles + kCtWords) * 4, d->stream));
+    timed_launch(d, "setup", [&] { launch_setup(P, d->stream); });
+    timed_launch(d, "scan", [&] { launch_scan(P, d->stream); });
+    timed_launch(d, "bin", [&] { launch_bin(P, d->stream); });
+    timed_launch(d, "tile", [&] { launch_tile(P, d->stream); });
+    ZR_HIP(hipGetLastError());
+    s.color_clear_pending = false;
+    s.depth_clear_pending = false;
+    return ZR_SUCCESS;
+}
+
+zr_result exec_end_rendering(zr_device* d, ExecState& s) {
+    if (s.color_clear_pending || s.depth_clear_pending) {
+        DrawParams P;
+        memset(&P, 0, sizeof P);
+        zr_result rc = fill_target(s, P);
+        if (rc) return rc;
+        timed_launch(d, "clear", [&] { launch_clear(P, d->stream); });
+        ZR_HIP(hipGetLastError());
+    }
+    s.rendering = false;
+    s.color_clear_pending = s.depth_clear_pending = false;
+    return ZR_SUCCESS;
+}
+
+zr_result execute(zr_device* d, zr_cmd* cmd) {
+    ExecState s;
+    for (const Cmd& c : cmd->cmds) {
+        zr_result rc = ZR_SUCCESS;
+        switch (c.type) {
+        case C_BEGIN_RENDERING:
+            s.rendering = true;
+            s.rs = c.rendering;
+            s.color_clear_pending = s.rs.has_color && s.rs.color.load_op == ZR_ATTACHMENT_LOAD_OP_CLEAR;
+            s.depth_clear_pending = s.rs.has_depth && s.rs.depth.load_op == ZR_ATTACHMENT_LOAD_OP_CLEAR;
+            break;
+        case C_END_RENDERING: rc = exec_end_rendering(d, s); break;
+        case C_BIND_PIPELINE: s.pipe = c.pipeline; break;
+        case C_BIND_UNIFORM: s.ubos[{c.a, c.b}] = {c.buffer, c.offset}; break;
+        case C_SET_VIEWPORT: s.vp = c.vp; s.vp_set = true; break;
+        case C_SET_SCISSOR: s.sc = c.rect; s.sc_set = true; break;
+        case C_BIND_VB:
+            if (c.a < 8) s.vb[c.a] = {c.buffer, c.offset};
+            break;
+        case C_BIND_IB: s.ib = c.buffer; s.ib_offset = c.offset; s.index_type = c.e; break;
+        case C_DRAW: rc = exec_draw(d, s, c, c.d != 0); break;
+        case C_SET_SHARD: s.shard_rank = c.a; s.shard_count = c.b; break;
+        }
+        if (rc) return rc;
+    }
+    if (s.rendering) return exec_end_rendering(d, s);
+    return ZR_SUCCESS;
+}
+
+void latch(zr_cmd* cmd, zr_result rc, const std::string& msg) {
+    if (cmd->err == ZR_SUCCESS) {
+        cmd->err = rc;
+        cmd->err_msg = msg;
+    }
+}
+
+}  // namespace
+
+// ======================================================================= ABI
+
+extern "C" {
+
+ZR_API const char* zr_last_error_message(void) { return g_last_error.c_str(); }
+
+ZR_API const char* zr_build_info(void) {
+    return "libzenith_raster (HIP, gfx950): setup/scan/bin/tile passes, tile=32x32, 64-bit LDS visibility keys";
+}
+
+ZR_API zr_result zr_device_create(int32_t hip_device, zr_device** out) {
+    if (!out) return fail(ZR_ERROR_VALIDATION_FAILED, "out is NULL");
+    *out = nullptr;
+    int n = 0;
+    if (hipGetDeviceCount(&n) != hipSuccess || n <= 0)
+        return fail(ZR_ERROR_INITIALIZATION_FAILED, "no HIP device available");
+    if (hip_device < 0 || hip_device >= n) return fail(ZR_ERROR_INITIALIZATION_FAILED, "bad device index");
+    zr_device* d = new (std::nothrow) zr_device_t();
+    if (!d) return fail(ZR_ERROR_OUT_OF_HOST_MEMORY, "device alloc");
+    d->hip_device = hip_device;
+    ZR_HIP(hipSetDevice(hip_device));
+    ZR_HIP(hipStreamCreateWithFlags(&d->stream, hipStreamNonBlocking));
+    void* st = nullptr;
+    ZR_HIP(hipHostMalloc(&st, kStWords * 4, hipHostMallocMapped));
+    memset(st, 0, kStWords * 4);
+    d->status_host = (uint32_t*)st;
+    void* sd = nullptr;
+    ZR_HIP(hipHostGetDevicePointer(&sd, st, 0));
+    d->status_dev = (uint32_t*)sd;
+    *out = d;
+    return ZR_SUCCESS;
+}
+
+ZR_API void zr_device_destroy(zr_device* d) {
+    if (!d) return;
+    (void)hipSetDevice(d->hip_device);
+    (void)hipStreamSynchronize(d->stream);
+    collect_timings(d);
+    for (hipEvent_t e : d->event_pool) (void)hipEventDestroy(e);
+    (void)hipFree(d->records);
+    (void)hipFree(d->tri_ntiles);
+    (void)hipFree(d->tile_counts);
+    (void)hipFree(d->tile_offsets);
+    (void)hipFree(d->bins);
+    (void)hipHostFree(d->status_host);
+    (void)hipStreamDestroy(d->stream);
+    delete d;
+}
+
+ZR_API zr_result zr_device_wait_idle(zr_device* d) {
+    if (!d) return fail(ZR_ERROR_VALIDATION_FAILED, "device is NULL");
+    return device_sync(d);
+}
+
+ZR_API zr_result zr_device_set_profiling(zr_device* d, int32_t enable) {
+    if (!d) return fail(ZR_ERROR_VALIDATION_FAILED, "device is NULL");
+    d->profiling = enable != 0;
+    return ZR_SUCCESS;
+}
+
+ZR_API int32_t zr_device_kernel_times(zr_device* d, zr_kernel_time* out, int32_t capacity, int32_t reset) {
+    if (!d) return 0;
+    int32_t n = 0;
+    for (const auto& kv : d->times) {
+        if (out && n < capacity) {
+            memset(&out[n], 0, sizeof(zr_kernel_time));
+            snprintf(out[n].name, sizeof(out[n].name), "%s", kv.first.c_str());
+            out[n].total_ms = kv.second.first;
+            out[n].launches = kv.second.second;
+        }
+        ++n;
+    }
+    if (reset) d->times.clear();
+    return std::min(n, capacity);
+}
+
+ZR_API zr_result zr_device_last_draw_stats(zr_device* d, zr_draw_stats* out) {
+    if (!d || !out) return fail(ZR_ERROR_VALIDATION_FAILED, "NULL argument");
+    *out = d->last;
+    return ZR_SUCCESS;
+}
+
+// ------------------------------------------------------------------ buffers
+
+static zr_result buffer_make(zr_device* d, const zr_buffer_desc* desc, void* ext, zr_buffer** out) {
+    if (!d || !desc || !out) return fail(ZR_ERROR_VALIDATION_FAILED, "NULL argument");
+    *out = nullptr;
+    zr_result rc = set_device(d);
+    if (rc) return rc;
+    zr_buffer* b = new (std::nothrow) zr_buffer_t();
+    if (!b) return fail(ZR_ERROR_OUT_OF_HOST_MEMORY, "buffer alloc");
+    b->dev = d;
+    b->size = desc->size;
+    b->name = desc->name ? desc->name : "";
+    b->external = ext != nullptr;
+    if (ext) {
+        b->ptr = ext;
+    } else {
+        void* p = nullptr;
+        hipError_t e = hipMalloc(&p, std::max<uint64_t>(desc->size, 16));
+        if (e != hipSuccess) {
+            delete b;
+            return fail(ZR_ERROR_OUT_OF_DEVICE_MEMORY, "hipMalloc failed for buffer " + std::string(desc->name ? desc->name : ""));
+        }
+        b->ptr = p;
+    }
+    *out = b;
+    return ZR_SUCCESS;
+}
+
+ZR_API zr_result zr_buffer_create(zr_device* d, const zr_buffer_desc* desc, zr_buffer** out) {
+    return buffer_make(d, desc, nullptr, out);
+}
+
+ZR_API zr_result zr_buffer_create_external(zr_device* d, const zr_buffer_desc* desc, void* ptr, zr_buffer** out) {
+    if (!ptr) return fail(ZR_ERROR_VALIDATION_FAILED, "external pointer is NULL");
+    return buffer_make(d, desc, ptr, out);
+}
+
+ZR_API void zr_buffer_destroy(zr_buffer* b) {
+    if (!b) return;
+    device_sync(b->dev);
+    if (!b->external) (void)hipFree(b->ptr);
+    delete b;
+}
+
+ZR_API zr_result zr_buffer_write(zr_buffer* b, uint64_t offset, const void* src, uint64_t size) {
+    if (!b) return fail(ZR_ERROR_VALIDATION_FAILED, "buffer is NULL");
+    if (size == 0) return ZR_SUCCESS;  // buffer.rs:301-303
+    if (offset > b->size || size > b->size - offset)
+        return fail(ZR_ERROR_OUT_OF_DEVICE_MEMORY, "write past the end of buffer '" + b->name + "'");
+    zr_result rc = device_sync(b->dev);
+    if (rc) return rc;
+    ZR_HIP(hipMemcpyAsync((uint8_t*)b->ptr + offset, src, size, hipMemcpyHostToDevice, b->dev->stream));
+    ZR_HIP(hipStreamSynchronize(b->dev->stream));
+    return ZR_SUCCESS;
+}
+
+ZR_API zr_result zr_buffer_read(zr_buffer* b, uint64_t offset, void* dst, uint64_t size) {
+    if (!b) return fail(ZR_ERROR_VALIDATION_FAILED, "buffer is NULL");
+    if (offset > b->size || size > b->size - offset) return fail(ZR_ERROR_VALIDATION_FAILED, "read out of range");
+    zr_result rc = device_sync(b->dev);
+    if (rc) return rc;
+    ZR_HIP(hipMemcpyAsync(dst, (const uint8_t*)b->ptr + offset, size, hipMemcpyDeviceToHost, b->dev->stream));
+    ZR_HIP(hipStreamSynchronize(b->dev->stream));
+    return ZR_SUCCESS;
+}
+
+ZR_API uint64_t zr_buffer_size(const zr_buffer* b) { return b ? b->size : 0; }
+ZR_API void* zr_buffer_device_address(const zr_buffer* b) { return b ? b->ptr : nullptr; }
+
+// ----------------------------------------------------------------- textures
+
+static zr_result texture_make(zr_device* d, const zr_texture_desc* desc, void* ext, zr_texture** out) {
+    if (!d || !desc || !out) return fail(ZR_ERROR_VALIDATION_FAILED, "NULL argument");
+    *out = nullptr;
+    uint32_t bpp = desc->format == ZR_FORMAT_D32_SFLOAT ? 4u : format_bpp(desc->format);
+    if (!bpp) return fail(ZR_ERROR_FORMAT_NOT_SUPPORTED, "unsupported texture format");
+    if (desc->width == 0 || desc->height == 0) return fail(ZR_ERROR_VALIDATION_FAILED, "zero extent");
+    zr_result rc = set_device(d);
+    if (rc) return rc;
+    zr_texture* t = new (std::nothrow) zr_texture_t();
+    if (!t) return fail(ZR_ERROR_OUT_OF_HOST_MEMORY, "texture alloc");
+    t->dev = d;
+    t->width = desc->width;
+    t->height = desc->height;
+    t->format = desc->format;
+    t->bpp = bpp;
+    t->external = ext != nullptr;
+    t->name = desc->name ? desc->name : "";
+    if (ext) {
+        t->ptr = ext;
+    } else {
+        void* p = nullptr;
+        if (hipMalloc(&p, (size_t)desc->width * desc->height * bpp) != hipSuccess) {
+            delete t;
+            return fail(ZR_ERROR_OUT_OF_DEVICE_MEMORY, "hipMalloc failed for texture");
+        }
+        t->ptr = p;
+    }
+    *out = t;
+    return ZR_SUCCESS;
+}
+
+ZR_API zr_result zr_texture_create(zr_device* d, const zr_texture_desc* desc, zr_texture** out) {
+    return texture_make(d, desc, nullptr, out);
+}
+
+ZR_API zr_result zr_texture_create_external(zr_device* d, const zr_texture_desc* desc, void* ptr, zr_texture** out) {
+    if (!ptr) return fail(ZR_ERROR_VALIDATION_FAILED, "external pointer is NULL");
+    return texture_make(d, desc, ptr, out);
+}
+
+ZR_API void zr_texture_destroy(zr_texture* t) {
+    if (!t) return;
+    device_sync(t->dev);
+    if (!t->external) (void)hipFree(t->ptr);
+    delete t;
+}
+
+ZR_API zr_result zr_texture_read(zr_texture* t, void* dst, uint64_t size) {
+    if (!t || !dst) return fail(ZR_ERROR_VALIDATION_FAILED, "NULL argument");
+    const uint64_t bytes = (uint64_t)t->width * t->height * t->bpp;
+    if (size < bytes) return fail(ZR_ERROR_VALIDATION_FAILED, "destination too small");
+    zr_result rc = device_sync(t->dev);
+    if (rc) return rc;
+    ZR_HIP(hipMemcpyAsync(dst, t->ptr, bytes, hipMemcpyDeviceToHost, t->dev->stream));
+    ZR_HIP(hipStreamSynchronize(t->dev->stream));
+    return ZR_SUCCESS;
+}
+
+ZR_API zr_result zr_texture_write(zr_texture* t, const void* src, uint64_t size) {
+    if (!t || !src) return fail(ZR_ERROR_VALIDATION_FAILED, "NULL argument");
+    const uint64_t bytes = (uint64_t)t->width * t->height * t->bpp;
+    if (size < bytes) return fail(ZR_ERROR_VALIDATION_FAILED, "source too small");
+    zr_result rc = device_sync(t->dev);
+    if (rc) return rc;
+    ZR_HIP(hipMemcpyAsync(t->ptr, src, bytes, hipMemcpyHostToDevice, t->dev->stream));
+    ZR_HIP(hipStreamSynchronize(t->dev->stream));
+    return ZR_SUCCESS;
+}
+
+ZR_API void* zr_texture_device_address(const zr_texture* t) { return t ? t->ptr : nullptr; }
+
+// ------------------------------------------------------------------ shaders
+
+ZR_API zr_result zr_shader_lookup(zr_device* d, const char* path, const char* entry, uint32_t stage, zr_shader** out) {
+    (void)d;
+    if (!out || !path || !entry) return fail(ZR_ERROR_VALIDATION_FAILED, "NULL argument");
+    *out = nullptr;
+    const std::string base = basename_of(path);
+    for (const auto& s : kShaders) {
+        if (base == s.file && !strcmp(entry, s.entry) && stage == s.stage) {
+            zr_shader* sh = new (std::nothrow) zr_shader_t();
+            if (!sh) return fail(ZR_ERROR_OUT_OF_HOST_MEMORY, "shader alloc");
+            sh->program = s.program;
+            sh->stage = s.stage;
+            sh->file = s.file;
+            sh->entry = s.entry;
+            sh->bindings.assign(s.bind, s.bind + s.nbind);
+            sh->inputs.assign(s.inputs, s.inputs + s.ninputs);
+            *out = sh;
+            return ZR_SUCCESS;
+        }
+    }
+    return fail(ZR_ERROR_SHADER_NOT_FOUND, "no built-in stage for " + base + ":" + entry);
+}
+
+ZR_API void zr_shader_destroy(zr_shader* sh) { delete sh; }
+
+ZR_API int32_t zr_shader_bindings(const zr_shader* sh, zr_shader_binding* out, int32_t capacity) {
+    if (!sh) return 0;
+    const int32_t n = (int32_t)sh->bindings.size();
+    for (int32_t i = 0; out && i < std::min(n, capacity); ++i) out[i] = sh->bindings[i];
+    return n;
+}
+
+ZR_API int32_t zr_shader_vertex_inputs(const zr_shader* sh, zr_vertex_input_attr* out, int32_t capacity) {
+    if (!sh) return 0;
+    const int32_t n = (int32_t)sh->inputs.size();
+    for (int32_t i = 0; out && i < std::min(n, capacity); ++i) out[i] = sh->inputs[i];
+    return n;
+}
+
+// ---------------------------------------------------------------- pipelines
+
+// validate_vertex_inputs, zenith-rhi/src/pipeline.rs:228-287 (strict match).
+static zr_result validate_vertex_inputs(const zr_shader* vs, const zr_vertex_attribute* attrs, uint32_t n,
+                                        zr_pipeline_error* err) {
+    if (vs->inputs.empty()) {
+        if (n == 0) return ZR_SUCCESS;
+        return fail(ZR_ERROR_VERTEX_INPUT_REFLECTION_MISSING,
+                    "vertex shader reflection contains no vertex_inputs, but vertex_attributes were provided");
+    }
+    std::map<uint32_t, int32_t> expected, provided;
+    for (const auto& vi : vs->inputs) expected[vi.location] = vi.format;
+    for (uint32_t i = 0; i < n; ++i) {
+        auto it = provided.find(attrs[i].location);
+        if (it != provided.end()) {
+            if (it->second != attrs[i].format) {
+                if (err) *err = {attrs[i].location, it->second, attrs[i].format};
+                return fail(ZR_ERROR_DUPLICATE_VERTEX_ATTRIBUTE_LOCATION,
+                            "duplicate vertex attribute location: " + std::to_string(attrs[i].location));
+            }
+        } else {
+            provided[attrs[i].location] = attrs[i].format;
+        }
+    }
+    for (const auto& kv : expected) {
+        auto it = provided.find(kv.first);
+        if (it == provided.end()) {
+            if (err) *err = {kv.first, kv.second, 0};
+            return fail(ZR_ERROR_MISSING_VERTEX_ATTRIBUTE,
+                        "missing vertex attribute for location " + std::to_string(kv.first));
+        }
+        if (it->second != kv.second) {
+            if (err) *err = {kv.first, kv.second, it->second};
+            return fail(ZR_ERROR_VERTEX_ATTRIBUTE_FORMAT_MISMATCH,
+                        "vertex attribute format mismatch at location " + std::to_string(kv.first));
+        }
+    }
+    for (const auto& kv : provided) {
+        if (!expected.count(kv.first)) {
+            if (err) *err = {kv.first, 0, kv.second};
+            return fail(ZR_ERROR_UNEXPECTED_VERTEX_ATTRIBUTE,
+                        "unexpected vertex attribute at location " + std::to_string(kv.first));
+        }
+    }
+    return ZR_SUCCESS;
+}
+
+ZR_API zr_result zr_pipeline_create(zr_device* d, const zr_graphic_pipeline_desc* desc, zr_pipeline** out,
+                                    zr_pipeline_error* err) {
+    (void)d;
+    if (!desc || !out) return fail(ZR_ERROR_VALIDATION_FAILED, "NULL argument");
+    *out = nullptr;
+    if (err) *err = {0, 0, 0};
+    const zr_shader* vs = desc->vertex_shader;
+    const zr_shader* fs = desc->fragment_shader;
+    if (!vs) return fail(ZR_ERROR_MISSING_VERTEX_SHADER, "missing vertex shader");
+    if (vs->stage != ZR_SHADER_STAGE_VERTEX || (fs && fs->stage != ZR_SHADER_STAGE_FRAGMENT))
+        return fail(ZR_ERROR_VALIDATION_FAILED, "shader stage mismatch");
+    zr_result rc = validate_vertex_inputs(vs, desc->vertex_attributes, desc->vertex_attribute_count, err);
+    if (rc) return rc;
+    if (fs && fs->program != vs->program)
+        return fail(ZR_ERROR_FEATURE_NOT_PRESENT, "vertex and fragment stages come from different programs");
+    if (desc->topology != 3) return fail(ZR_ERROR_FEATURE_NOT_PRESENT, "only TRIANGLE_LIST is supported");
+    if (desc->rasterization.polygon_mode != 0) return fail(ZR_ERROR_FEATURE_NOT_PRESENT, "only FILL polygon mode");
+    if (desc->rasterization.depth_clamp || desc->rasterization.depth_bias_enable)
+        return fail(ZR_ERROR_FEATURE_NOT_PRESENT, "depth clamp / depth bias not supported");
+    if (desc->samples > 1) return fail(ZR_ERROR_FEATURE_NOT_PRESENT, "only 1x multisampling");
+    if (desc->color_attachment_count > 1) return fail(ZR_ERROR_FEATURE_NOT_PRESENT, "at most one colour attachment");
+    zr_pipeline* p = new (std::nothrow) zr_pipeline_t();
+    if (!p) return fail(ZR_ERROR_OUT_OF_HOST_MEMORY, "pipeline alloc");
+    p->program = vs->program;
+    p->has_fs = fs != nullptr;
+    p->color_count = desc->color_attachment_count;
+    p->color = zr_color_attachment_desc{};
+    p->color.write_mask = 0xF;
+    p->color_format = 0;
+    if (p->color_count) {
+        p->color = desc->color_attachments[0];
+        p->color_format = desc->color_formats ? desc->color_formats[0] : 0;
+        if (p->color.blend_enable) {
+            delete p;
+            return fail(ZR_ERROR_FEATURE_NOT_PRESENT, "colour blending is not supported on this path");
+        }
+        if (p->color_format && format_bpp(p->color_format) == 0) {
+            delete p;
+            return fail(ZR_ERROR_FORMAT_NOT_SUPPORTED, "colour attachment format");
+        }
+    }
+    p->depth_format = desc->depth_format;
+    p->has_depth_state = desc->depth_stencil != nullptr;
+    if (p->has_depth_state) {
+        p->ds = *desc->depth_stencil;
+        if (p->ds.stencil_test_enable || p->ds.depth_bounds_test_enable) {
+            delete p;
+            return fail(ZR_ERROR_FEATURE_NOT_PRESENT, "stencil / depth-bounds tests are not supported");
+        }
+        if (p->ds.depth_write_enable && p->ds.depth_test_enable && p->ds.depth_compare_op == 5) {
+            delete p;
+            return fail(ZR_ERROR_FEATURE_NOT_PRESENT, "NOT_EQUAL with depth writes is order dependent");
+        }
+    }
+    p->cull_mode = desc->rasterization.cull_mode;
+    p->front_face = desc->rasterization.front_face;
+    // vertex layout: binding 0, per-vertex rate (VertexLayout derive, rhi-derive/src/lib.rs:126-131)
+    p->stride = 0;
+    for (uint32_t i = 0; i < desc->vertex_binding_count; ++i) {
+        if (desc->vertex_bindings[i].binding == 0) {
+            p->stride = desc->vertex_bindings[i].stride;
+            if (desc->vertex_bindings[i].input_rate != 0) {
+                delete p;
+                return fail(ZR_ERROR_FEATURE_NOT_PRESENT, "per-instance vertex input rate");
+            }
+        }
+    }
+    p->nattr = (uint32_t)vs->inputs.size();
+    memset(p->attr_offset, 0, sizeof p->attr_offset);
+    for (uint32_t i = 0; i < desc->vertex_attribute_count; ++i) {
+        const auto& a = desc->vertex_attributes[i];
+        if (a.binding != 0 || a.location >= 4 || (a.offset & 3u)) {
+            delete p;
+            return fail(ZR_ERROR_FEATURE_NOT_PRESENT, "vertex attributes must live in binding 0, 4-byte aligned");
+        }
+        p->attr_offset[a.location] = a.offset;
+    }
+    if (p->nattr && (p->stride == 0 || (p->stride & 3u))) {
+        delete p;
+        return fail(ZR_ERROR_FEATURE_NOT_PRESENT, "vertex binding 0 missing or stride not 4-byte aligned");
+    }
+    // ShaderReflection::merge (shader.rs:222-259): union by (set, binding), stage flags OR-ed
+    std::map<std::pair<uint32_t, uint32_t>, zr_shader_binding> merged;
+    for (const zr_shader* sh : {vs, fs}) {
+        if (!sh) continue;
+        for (const auto& b : sh->bindings) {
+            auto key = std::make_pair(b.set, b.binding);
+            auto it = merged.find(key);
+            if (it == merged.end()) merged[key] = b;
+            else it->second.stage_flags |= b.stage_flags;
+        }
+    }
+    for (const auto& kv : merged) p->bindings.push_back(kv.second);
+    *out = p;
+    return ZR_SUCCESS;
+}
+
+ZR_API void zr_pipeline_destroy(zr_pipeline* p) { delete p; }
+
+// ----------------------------------------------------------------- commands
+
+ZR_API zr_result zr_cmd_create(zr_device* d, zr_cmd** out) {
+    if (!d || !out) return fail(ZR_ERROR_VALIDATION_FAILED, "NULL argument");
+    zr_cmd* c = new (std::nothrow) zr_cmd_t();
+    if (!c) return fail(ZR_ERROR_OUT_OF_HOST_MEMORY, "cmd alloc");
+    c->dev = d;
+    *out = c;
+    return ZR_SUCCESS;
+}
+
+ZR_API void zr_cmd_destroy(zr_cmd* c) {
+    if (!c) return;
+    auto& pend = c->dev->pending;
+    if (std::find(pend.begin(), pend.end(), c) != pend.end()) device_sync(c->dev);
+    delete c;
+}
+
+ZR_API zr_result zr_cmd_begin(zr_cmd* c) {
+    if (!c) return fail(ZR_ERROR_VALIDATION_FAILED, "cmd is NULL");
+    auto& pend = c->dev->pending;
+    if (std::find(pend.begin(), pend.end(), c) != pend.end()) {
+        zr_result rc = device_sync(c->dev);
+        if (rc) return rc;
+    }
+    c->cmds.clear();
+    c->err = ZR_SUCCESS;
+    c->err_msg.clear();
+    c->in_rendering = false;
+    return ZR_SUCCESS;
+}
+
+ZR_API zr_result zr_cmd_end(zr_cmd* c) {
+    if (!c) return fail(ZR_ERROR_VALIDATION_FAILED, "cmd is NULL");
+    if (c->in_rendering) latch(c, ZR_ERROR_VALIDATION_FAILED, "command buffer ended inside a render pass");
+    if (c->err) return fail(c->err, c->err_msg);
+    return ZR_SUCCESS;
+}
+
+ZR_API void zr_cmd_begin_rendering(zr_cmd* c, const zr_rendering_info* info) {
+    if (!c) return;
+    if (!info) return latch(c, ZR_ERROR_VALIDATION_FAILED, "rendering info is NULL");
+    if (c->in_rendering) return latch(c, ZR_ERROR_VALIDATION_FAILED, "nested begin_rendering");
+    if (info->color_attachment_count > 1)
+        return latch(c, ZR_ERROR_FEATURE_NOT_PRESENT, "at most one colour attachment");
+    Cmd k;
+    k.type = C_BEGIN_RENDERING;
+    k.rendering.area = info->render_area;
+    if (info->color_attachment_count == 1) {
+        k.rendering.has_color = info->color_attachments[0].texture != nullptr;
+        k.rendering.color = info->color_attachments[0];
+    }
+    if (info->depth_attachment && info->depth_attachment->texture) {
+        k.rendering.has_depth = true;
+        k.rendering.depth = *info->depth_attachment;
+    }
+    c->cmds.push_back(k);
+    c->in_rendering = true;
+}
+
+ZR_API void zr_cmd_end_rendering(zr_cmd* c) {
+    if (!c) return;
+    if (!c->in_rendering) return latch(c, ZR_ERROR_VALIDATION_FAILED, "end_rendering without begin_rendering");
+    Cmd k;
+    k.type = C_END_RENDERING;
+    c->cmds.push_back(k);
+    c->in_rendering = false;
+}
+
+ZR_API void zr_cmd_bind_pipeline(zr_cmd* c, const zr_pipeline* p) {
+    if (!c) return;
+    if (!p) return latch(c, ZR_ERROR_VALIDATION_FAILED, "pipeline is NULL");
+    Cmd k;
+    k.type = C_BIND_PIPELINE;
+    k.pipeline = p;
+    c->cmds.push_back(k);
+}
+
+ZR_API void zr_cmd_bind_uniform_buffer(zr_cmd* c, uint32_t set, uint32_t binding, const zr_buffer* buf,
+                                       uint64_t offset, uint64_t range) {
+    if (!c) return;
+    if (!buf) return latch(c, ZR_ERROR_VALIDATION_FAILED, "uniform buffer is NULL");
+    Cmd k;
+    k.type = C_BIND_UNIFORM;
+    k.a = set;
+    k.b = binding;
+    k.buffer = buf;
+    k.offset = offset;
+    k.range = range;
+    c->cmds.push_back(k);
+}
+
+ZR_API zr_result zr_cmd_bind_uniform_by_name(zr_cmd* c, const zr_pipeline* p, const char* name, const zr_buffer* buf,
+                                             uint64_t offset, uint64_t range) {
+    if (!c || !p || !name || !buf) return fail(ZR_ERROR_VALIDATION_FAILED, "NULL argument");
+    for (const auto& b : p->bindings) {
+        if (!strcmp(b.name, name)) {
+            if (b.descriptor_type != ZR_DESCRIPTOR_TYPE_UNIFORM_BUFFER && b.descriptor_type != ZR_DESCRIPTOR_TYPE_STORAGE_BUFFER)
+                return fail(ZR_ERROR_BINDING_TYPE_MISMATCH, std::string("binding '") + name + "' is not a buffer");
+            zr_cmd_bind_uniform_buffer(c, b.set, b.binding, buf, offset, range);
+            return ZR_SUCCESS;
+        }
+    }
+    return fail(ZR_ERROR_BINDING_NOT_FOUND, std::string("binding '") + name + "' not found");
+}
+
+ZR_API void zr_cmd_set_viewport(zr_cmd* c, uint32_t first, uint32_t count, const zr_viewport* vps) {
+    if (!c) return;
+    if (!vps || count == 0) return;
+    if (first != 0 || count != 1) return latch(c, ZR_ERROR_FEATURE_NOT_PRESENT, "only viewport 0");
+    Cmd k;
+    k.type = C_SET_VIEWPORT;
+    k.vp = vps[0];
+    c->cmds.push_back(k);
+}
+
+ZR_API void zr_cmd_set_scissor(zr_cmd* c, uint32_t first, uint32_t count, const zr_rect2d* rects) {
+    if (!c) return;
+    if (!rects || count == 0) return;
+    if (first != 0 || count != 1) return latch(c, ZR_ERROR_FEATURE_NOT_PRESENT, "only scissor 0");
+    Cmd k;
+    k.type = C_SET_SCISSOR;
+    k.rect = rects[0];
+    c->cmds.push_back(k);
+}
+
+ZR_API void zr_cmd_bind_vertex_buffers(zr_cmd* c, uint32_t first_binding, uint32_t count, const zr_buffer* const* bufs,
+                                       const uint64_t* offsets) {
+    if (!c) return;
+    for (uint32_t i = 0; i < count; ++i) {
+        if (!bufs || !bufs[i]) return latch(c, ZR_ERROR_VALIDATION_FAILED, "vertex buffer is NULL");
+        Cmd k;
+        k.type = C_BIND_VB;
+        k.a = first_binding + i;
+        k.buffer = bufs[i];
+        k.offset = offsets ? offsets[i] : 0;
+        c->cmds.push_back(k);
+    }
+}
+
+ZR_API void zr_cmd_bind_index_buffer(zr_cmd* c, const zr_buffer* buf, uint64_t offset, int32_t index_type) {
+    if (!c) return;
+    if (!buf) return latch(c, ZR_ERROR_VALIDATION_FAILED, "index buffer is NULL");
+    if (index_type != ZR_INDEX_TYPE_UINT16 && index_type != ZR_INDEX_TYPE_UINT32)
+        return latch(c, ZR_ERROR_FEATURE_NOT_PRESENT, "index type");
+    Cmd k;
+    k.type = C_BIND_IB;
+    k.buffer = buf;
+    k.offset = offset;
+    k.e = index_type;
+    c->cmds.push_back(k);
+}
+
+ZR_API void zr_cmd_draw(zr_cmd* c, uint32_t vertex_count, uint32_t instance_count, uint32_t first_vertex,
+                        uint32_t first_instance) {
+    if (!c) return;
+    Cmd k;
+    k.type = C_DRAW;
+    k.a = vertex_count;
+    k.b = instance_count;
+    k.c = first_vertex;
+    k.d = 0;
+    k.e = 0;
+    (void)first_instance;
+    c->cmds.push_back(k);
+}
+
+ZR_API void zr_cmd_draw_indexed(zr_cmd* c, uint32_t index_count, uint32_t instance_count, uint32_t first_index,
+                                int32_t vertex_offset, uint32_t first_instance) {
+    if (!c) return;
+    Cmd k;
+    k.type = C_DRAW;
+    k.a = index_count;
+    k.b = instance_count;
+    k.c = first_index;
+    k.d = 1;
+    k.e = vertex_offset;
+    (void)first_instance;
+    c->cmds.push_back(k);
+}
+
+ZR_API void zr_cmd_set_tile_shard(zr_cmd* c, uint32_t rank, uint32_t count) {
+    if (!c) return;
+    if (count == 0 || rank >= count) return latch(c, ZR_ERROR_VALIDATION_FAILED, "bad tile shard");
+    Cmd k;
+    k.type = C_SET_SHARD;
+    k.a = rank;
+    k.b = count;
+    c->cmds.push_back(k);
+}
+
+// --------------------------------------------------------------- submission
+
+ZR_API zr_result zr_fence_create(zr_device* d, zr_fence** out) {
+    if (!d || !out) return fail(ZR_ERROR_VALIDATION_FAILED, "NULL argument");
+    zr_result rc = set_device(d);
+    if (rc) return rc;
+    zr_fence* f = new (std::nothrow) zr_fence_t();
+    if (!f) return fail(ZR_ERROR_OUT_OF_HOST_MEMORY, "fence alloc");
+    f->dev = d;
+    if (hipEventCreateWithFlags(&f->ev, hipEventDisableTiming) != hipSuccess) {
+        delete f;
+        return fail(ZR_ERROR_DEVICE_LOST, "hipEventCreate failed");
+    }
+    *out = f;
+    return ZR_SUCCESS;
+}
+
+ZR_API void zr_fence_destroy(zr_fence* f) {
+    if (!f) return;
+    (void)hipEventSynchronize(f->ev);
+    (void)hipEventDestroy(f->ev);
+    delete f;
+}
+
+ZR_API zr_result zr_submit(zr_device* d, zr_cmd* c, zr_fence* f) {
+    if (!d || !c) return fail(ZR_ERROR_VALIDATION_FAILED, "NULL argument");
+    if (c->err) return fail(c->err, c->err_msg);
+    if (c->in_rendering) return fail(ZR_ERROR_VALIDATION_FAILED, "submitted inside a render pass");
+    zr_result rc = set_device(d);
+    if (rc) return rc;
+    rc = execute(d, c);
+    if (rc) return rc;
+    d->pending.push_back(c);
+    if (f) {
+        ZR_HIP(hipEventRecord(f->ev, d->stream));
+        f->submitted = true;
+    }
+    return ZR_SUCCESS;
+}
+
+ZR_API zr_result zr_fence_wait(zr_fence* f, uint64_t timeout_ns) {
+    if (!f) return fail(ZR_ERROR_VALIDATION_FAILED, "fence is NULL");
+    if (!f->submitted) return ZR_SUCCESS;
+    if (timeout_ns == 0) {
+        hipError_t e = hipEventQuery(f->ev);
+        if (e == hipErrorNotReady) return ZR_TIMEOUT;
+        if (e != hipSuccess) return fail(ZR_ERROR_DEVICE_LOST, hipGetErrorString(e));
+    }
+    return device_sync(f->dev);
+}
+
+ZR_API zr_result zr_submit_and_wait(zr_device* d, zr_cmd* c) {
+    zr_result rc = zr_submit(d, c, nullptr);
+    if (rc) return rc;
+    return device_sync(d);
+}
+
+}  // extern "C"

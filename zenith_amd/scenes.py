@@ -1,0 +1,229 @@
+"""Synthetic scenes for the draw path (BASELINE.json ``configs``).
+
+Everything here is host-side workload generation (numpy), shared by the tests, the
+bench and the goldens.  Scenes are plain data: interleaved vertex bytes, index
+bytes and the pipeline/render-pass parameters that ``triangle.rs`` (or the config
+table) would set.  Nothing here rasterizes.
+
+Random soups follow SURVEY.md §8d exactly: a counter-based SplitMix64 stream,
+``float = (u >> 40) * 2^-24``, 32 draws per triangle at fixed offsets (so any
+triangle can be generated independently and in parallel).
+"""
+from __future__ import annotations
+
+import dataclasses
+import math
+
+import numpy as np
+
+# VkFormat / Vk enums used in scene descriptions (numeric Vulkan values).
+FMT_R8G8B8A8_UNORM = 37
+FMT_R8G8B8A8_SRGB = 43
+FMT_B8G8R8A8_UNORM = 44
+FMT_B8G8R8A8_SRGB = 50
+FMT_R32G32B32A32_SFLOAT = 109
+FMT_D32_SFLOAT = 126
+FMT_R32G32B32_SFLOAT = 106
+
+CULL_NONE, CULL_FRONT, CULL_BACK = 0, 1, 2
+FRONT_CCW, FRONT_CW = 0, 1
+OP_NEVER, OP_LESS, OP_EQUAL, OP_LEQUAL, OP_GREATER, OP_NOTEQUAL, OP_GEQUAL, OP_ALWAYS = range(8)
+INDEX_U16, INDEX_U32 = 0, 1
+LOAD_LOAD, LOAD_CLEAR, LOAD_DONT_CARE = 0, 1, 2
+
+PROGRAM_TRIANGLE, PROGRAM_FLAT_COLOR, PROGRAM_BLINN_PHONG = 0, 1, 2
+PROGRAM_FILES = {
+    PROGRAM_TRIANGLE: "content/shaders/triangle.slang",
+    PROGRAM_FLAT_COLOR: "content/shaders/flat_color.slang",
+    PROGRAM_BLINN_PHONG: "content/shaders/blinn_phong.slang",
+}
+PROGRAM_ATTRS = {PROGRAM_TRIANGLE: 2, PROGRAM_FLAT_COLOR: 2, PROGRAM_BLINN_PHONG: 3}
+
+
+@dataclasses.dataclass
+class Scene:
+    """One render pass with one draw, as ``TriangleRenderer::render_to`` records it."""
+
+    name: str
+    width: int
+    height: int
+    program: int
+    vertices: np.ndarray          # float32 [V, 3*attrs] interleaved, location order
+    indices: np.ndarray | None    # uint16/uint32 [I] or None for a non-indexed draw
+    color_format: int = FMT_B8G8R8A8_SRGB
+    clear_color: tuple = (0.1, 0.1, 0.1, 1.0)       # triangle.rs:110-113
+    cull_mode: int = CULL_NONE                       # triangle.rs:116
+    front_face: int = FRONT_CCW                      # pipeline.rs:520-533 default
+    depth: bool = False                              # DepthStencilDesc present?
+    depth_test: bool = True
+    depth_write: bool = True
+    depth_op: int = OP_LESS                          # pipeline.rs:435-453 default
+    depth_clear: float = 1.0
+    time: float = 0.0                                # Time.time, pinned for goldens
+    write_mask: int = 0xF
+
+    @property
+    def stride(self) -> int:
+        return 12 * PROGRAM_ATTRS[self.program]
+
+    @property
+    def index_type(self) -> int:
+        if self.indices is None:
+            return -1
+        return INDEX_U16 if self.indices.dtype == np.uint16 else INDEX_U32
+
+    @property
+    def draw_count(self) -> int:
+        return int(self.indices.size if self.indices is not None else self.vertices.shape[0])
+
+    @property
+    def triangles(self) -> int:
+        return self.draw_count // 3
+
+    def vertex_bytes(self) -> bytes:
+        return np.ascontiguousarray(self.vertices, dtype=np.float32).tobytes()
+
+    def index_bytes(self) -> bytes:
+        return b"" if self.indices is None else np.ascontiguousarray(self.indices).tobytes()
+
+
+# ---------------------------------------------------------------- C0 scenes
+
+def triangle_scene(width: int = 640, height: int = 480, time: float = 0.0) -> Scene:
+    """The reference's only scene: zenith-renderer/src/triangle.rs:28-33 (3 verts,
+    u16 indices [0,1,2]), clear [.1,.1,.1,1], cull NONE, no depth attachment."""
+    verts = np.array(
+        [[0.0, 0.5, 0.0, 1.0, 0.0, 0.0],
+         [-0.5, -0.5, 0.0, 0.0, 1.0, 0.0],
+         [0.5, -0.5, 0.0, 0.0, 0.0, 1.0]], dtype=np.float32)
+    idx = np.array([0, 1, 2], dtype=np.uint16)
+    return Scene("triangle", width, height, PROGRAM_TRIANGLE, verts, idx, time=time)
+
+
+def cube_scene(width: int = 640, height: int = 480, angle_deg: float = 30.0) -> Scene:
+    """Synthetic 12-triangle cube (content/mesh has no cube).
+
+    The vertex stage is pass-through, so the cube is rotated and projected on the
+    host (orthographic, z mapped into [0.2, 0.8]); faces are wound CCW in Vulkan's
+    sense and drawn with cull BACK + depth LESS, one flat colour per face."""
+    a = math.radians(angle_deg)
+    b = math.radians(angle_deg * 0.7)
+    ry = np.array([[math.cos(a), 0, math.sin(a)], [0, 1, 0], [-math.sin(a), 0, math.cos(a)]])
+    rx = np.array([[1, 0, 0], [0, math.cos(b), -math.sin(b)], [0, math.sin(b), math.cos(b)]])
+    corners = np.array([[x, y, z] for x in (-1, 1) for y in (-1, 1) for z in (-1, 1)], dtype=np.float64)
+    p = corners @ (rx @ ry).T * 0.45
+    aspect = width / height
+    ndc = np.stack([p[:, 0] / aspect, p[:, 1], 0.5 + p[:, 2] * 0.35], axis=1)
+    # faces as corner quads (outward normals), split into two triangles each
+    faces = [(0, 1, 3, 2), (4, 6, 7, 5), (0, 4, 5, 1), (2, 3, 7, 6), (0, 2, 6, 4), (1, 5, 7, 3)]
+    colors = [(1, 0.2, 0.2), (0.2, 1, 0.2), (0.2, 0.2, 1), (1, 1, 0.2), (1, 0.2, 1), (0.2, 1, 1)]
+    verts, idx = [], []
+    for f, col in zip(faces, colors):
+        quad = [f[0], f[1], f[2], f[3]]
+        for tri in ((0, 1, 2), (0, 2, 3)):
+            for k in tri:
+                idx.append(len(verts))
+                verts.append([*ndc[quad[k]], *col])
+    v = np.array(verts, dtype=np.float32)
+    i = np.array(idx, dtype=np.uint16)
+    s = Scene("cube", width, height, PROGRAM_FLAT_COLOR, v, i, cull_mode=CULL_BACK, depth=True)
+    # pick the winding that leaves the camera-facing faces (|z| smaller = nearer) CCW
+    s.front_face = _front_face_for_nearer(v, i, width, height)
+    return s
+
+
+def _front_face_for_nearer(v, i, w, h):
+    tri = v[i.astype(np.int64)].reshape(-1, 3, 6)
+    xf = (tri[:, :, 0] * 0.5 + 0.5) * w
+    yf = (tri[:, :, 1] * 0.5 + 0.5) * h
+    a2 = (xf[:, 1] - xf[:, 0]) * (yf[:, 2] - yf[:, 0]) - (xf[:, 2] - xf[:, 0]) * (yf[:, 1] - yf[:, 0])
+    zc = tri[:, :, 2].mean(axis=1)
+    near = zc < np.median(zc)
+    ccw = a2 < 0  # Vulkan: a = -A2/2 > 0 is counter-clockwise
+    return FRONT_CCW if (ccw[near].mean() >= 0.5) else FRONT_CW
+
+
+# ------------------------------------------------------------- random soups
+
+_GOLD = np.uint64(0x9E3779B97F4A7C15)
+
+
+def splitmix64(seed: int, counters: np.ndarray) -> np.ndarray:
+    """Counter-based SplitMix64: value i = mix(seed + (i+1)*golden)."""
+    with np.errstate(over="ignore"):
+        z = np.uint64(seed) + (counters.astype(np.uint64) + np.uint64(1)) * _GOLD
+        z = (z ^ (z >> np.uint64(30))) * np.uint64(0xBF58476D1CE4E5B9)
+        z = (z ^ (z >> np.uint64(27))) * np.uint64(0x94D049BB133111EB)
+        return z ^ (z >> np.uint64(31))
+
+
+def _uniform(seed: int, counters: np.ndarray) -> np.ndarray:
+    u = splitmix64(seed, counters)
+    return (u >> np.uint64(40)).astype(np.float64) * (2.0 ** -24)
+
+
+def soup_arrays(seed: int, n: int, width: int, height: int, L: float, normals: bool,
+                first: int = 0) -> np.ndarray:
+    """Per-vertex interleaved float32 rows for triangles [first, first+n)."""
+    t = np.arange(first, first + n, dtype=np.uint64)
+    base = t * np.uint64(32)
+
+    def U(off):
+        return _uniform(seed, base + np.uint64(off))
+
+    cx = U(0) * 2.0 - 1.0
+    cy = U(1) * 2.0 - 1.0
+    ex, ey = 2.0 * L / width, 2.0 * L / height
+    cols = 9 if normals else 6
+    out = np.empty((n, 3, cols), dtype=np.float32)
+    for k in range(3):
+        o = 2 + 10 * k
+        out[:, k, 0] = cx + (U(o) * 2.0 - 1.0) * ex
+        out[:, k, 1] = cy + (U(o + 1) * 2.0 - 1.0) * ey
+        out[:, k, 2] = 0.05 + U(o + 2) * 0.9
+        ccol = 6 if normals else 3
+        out[:, k, ccol] = U(o + 3)
+        out[:, k, ccol + 1] = U(o + 4)
+        out[:, k, ccol + 2] = U(o + 5)
+        if normals:
+            u1 = np.maximum(U(o + 6), 2.0 ** -24)
+            u2 = U(o + 7)
+            u3 = np.maximum(U(o + 8), 2.0 ** -24)
+            u4 = U(o + 9)
+            r1 = np.sqrt(-2.0 * np.log(u1))
+            r2 = np.sqrt(-2.0 * np.log(u3))
+            g = np.stack([r1 * np.cos(2 * np.pi * u2), r1 * np.sin(2 * np.pi * u2),
+                          r2 * np.cos(2 * np.pi * u4)], axis=1)
+            g /= np.maximum(np.linalg.norm(g, axis=1, keepdims=True), 1e-30)
+            out[:, k, 3:6] = g
+    return out.reshape(n * 3, cols)
+
+
+CONFIGS = {
+    # id: (seed, triangles, width, height, L px, program)   SURVEY.md §8d table
+    "c1": (1, 100_000, 1920, 1080, 12.0, PROGRAM_FLAT_COLOR),
+    "c2": (2, 1_000_000, 1920, 1080, 6.0, PROGRAM_BLINN_PHONG),
+    "c3": (3, 1_000_000, 3840, 2160, 12.0, PROGRAM_BLINN_PHONG),
+    "c4": (4, 10_000_000, 1920, 1080, 0.5, PROGRAM_FLAT_COLOR),
+}
+
+
+def soup_scene(seed: int, n: int, width: int, height: int, L: float, program: int,
+               name: str | None = None) -> Scene:
+    normals = program == PROGRAM_BLINN_PHONG
+    verts = soup_arrays(seed, n, width, height, L, normals)
+    idx = np.arange(3 * n, dtype=np.uint32)
+    return Scene(name or f"soup_s{seed}_n{n}", width, height, program, verts, idx,
+                 depth=True, cull_mode=CULL_NONE)
+
+
+def config_scene(cfg: str, n: int | None = None, width: int | None = None,
+                 height: int | None = None) -> Scene:
+    seed, tris, w, h, L, prog = CONFIGS[cfg]
+    return soup_scene(seed, n or tris, width or w, height or h, L, prog, name=cfg)
+
+
+def config_bytes_per_triangle(cfg: str) -> int:
+    """B_in of SURVEY.md §8d: 3 vertices at the stride + 3 u32 indices."""
+    prog = CONFIGS[cfg][5]
+    return 3 * 12 * PROGRAM_ATTRS[prog] + 3 * 4
