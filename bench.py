@@ -1,0 +1,188 @@
+#!/usr/bin/env python3
+"""Draw-path benchmark (BASELINE.json metric): Mtri/s + frames/s at 1080p on the
+1M-triangle scene (config C2), 1..N GPUs of one node.
+
+A step is one frame of the hot path: vertex/setup -> bin -> tile raster+resolve
+(-> tile-row gather to rank 0 when N > 1).  Inputs (vertex/index buffers) are
+uploaded once and resident in HBM before timing; the attachment CLEAR is fused
+into the tile pass.  `value` is whole-job throughput: triangles of all frames /
+max-over-ranks wall time.
+
+  python bench.py [--gpus N] [--steps K] [--warmup W] [--config c2]
+  torchrun --nproc-per-node N bench.py --gpus N ...      (N > 1, RCCL gather)
+"""
+import argparse
+import json
+import os
+import sys
+import time
+
+import torch  # first: libzenith_raster then binds to the same HIP runtime
+import torch.distributed as dist
+
+ROOT = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, ROOT)
+
+from zenith_amd import renderer, rhi, scenes, shard, zr  # noqa: E402
+
+HBM_PEAK_GBPS = 8000.0           # MI355X_MICROARCH.md: HBM3E 8.0 TB/s spec
+HBM_MEASURED_GBPS = 6290.0       # same table: float4 copy achievable
+METRIC = BASELINE_METRIC = "Mtriangles/s + frames/s at 1080p (1M-tri scene), 1/2/4/8 GPU; HBM GB/s vs roofline"
+RECORD_BYTES = 64                # TriRecord (zr_internal.h)
+BIN_ENTRY_BYTES = 4
+
+
+def parse():
+    p = argparse.ArgumentParser()
+    p.add_argument("--gpus", type=int, default=1)
+    p.add_argument("--steps", type=int, default=100)
+    p.add_argument("--warmup", type=int, default=10)
+    p.add_argument("--config", default="c2", choices=sorted(scenes.CONFIGS))
+    p.add_argument("--cpu-frames", type=int, default=5)
+    p.add_argument("--no-cpu-baseline", action="store_true")
+    p.add_argument("--pmc", default=os.path.join(ROOT, "profiles", "r01_pmc_tile.json"),
+                   help="rocprofv3 PMC summary for roofline.traffic (tools/pmc_summary.py)")
+    return p.parse_args()
+
+
+def algorithmic_bytes(kernel, n_tris, b_in, pairs, pixels):
+    """Per-launch algorithmic bytes of each pass (SURVEY.md §8d per-pass accounting)."""
+    if kernel == "setup":
+        return n_tris * b_in + n_tris * RECORD_BYTES
+    if kernel == "bin":
+        return pairs * BIN_ENTRY_BYTES + n_tris * RECORD_BYTES
+    if kernel == "tile":
+        return pairs * (BIN_ENTRY_BYTES + RECORD_BYTES) + pixels * 8
+    if kernel == "scan":
+        return 0
+    return 0
+
+
+def cpu_baseline(scene, frames):
+    """The CPU oracle (oracle/, OpenMP over tile-row bands) on the same scene."""
+    from oracle import oracle
+    threads = min(16, os.cpu_count() or 1)
+    oracle.render(scene, nthreads=threads)  # warm-up
+    t0 = time.perf_counter()
+    for _ in range(frames):
+        oracle.render(scene, nthreads=threads)
+    dt = time.perf_counter() - t0
+    return {"value": round(scene.triangles * frames / dt / 1e6, 3), "unit": "Mtri/s", "cores": threads,
+            "kind": "port",
+            "sample": f"{frames} full frames of {scene.name} ({scene.triangles} tris, {scene.width}x{scene.height}) "
+                      f"after 1 warm-up; {dt:.2f} s wall on {threads} threads"}
+
+
+def main():
+    a = parse()
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    if world != a.gpus:
+        raise SystemExit(f"--gpus {a.gpus} but WORLD_SIZE={world}: launch N>1 with torch.distributed.run")
+    torch.cuda.set_device(local)
+    cuda = torch.device("cuda", local)
+    if world > 1:
+        dist.init_process_group("nccl", device_id=cuda)
+
+    scene = scenes.config_scene(a.config)
+    W, H, N = scene.width, scene.height, scene.triangles
+    dev = rhi.RenderDevice(local)
+    color_t = torch.zeros((H, W * 4), dtype=torch.uint8, device=cuda)
+    depth_t = torch.zeros((H, W), dtype=torch.float32, device=cuda)
+    torch.cuda.synchronize()
+    color = rhi.Texture(dev, rhi.TextureDesc.new_color("frame.color", W, H, scene.color_format), color_t.data_ptr())
+    depth = rhi.Texture(dev, rhi.TextureDesc.new_depth("frame.depth", W, H), depth_t.data_ptr())
+    r = renderer.SceneRenderer(dev, scene)
+    enc = r.record(color, depth, shard=(rank, world) if world > 1 else None)
+    gather = shard.TileRowGather(H, W * 4, rank, world, cuda) if world > 1 else None
+
+    def step():
+        dev.submit(enc)
+        if gather is not None:
+            dev.wait_idle()          # frame done on the raster stream before RCCL reads it
+            gather.gather(color_t)
+
+    for _ in range(a.warmup):
+        step()
+    dev.wait_idle()
+    torch.cuda.synchronize()
+    dev.kernel_times(reset=True)
+    dev.set_profiling(True)
+    if world > 1:
+        dist.barrier()
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    for _ in range(a.steps):
+        step()
+    dev.wait_idle()
+    torch.cuda.synchronize()
+    if world > 1:
+        dist.barrier()
+    t1 = time.perf_counter()
+    dev.set_profiling(False)
+    elapsed = torch.tensor([t1 - t0], dtype=torch.float64, device=cuda)
+    if world > 1:
+        dist.all_reduce(elapsed, op=dist.ReduceOp.MAX)
+    elapsed = float(elapsed.item())
+
+    kt = dev.kernel_times()
+    stats = dev.last_draw_stats()
+    pairs = stats["bin_pairs"]
+    pixels = int(shard.owned_rows(H, rank, world).numel()) * W
+    b_in = scenes.config_bytes_per_triangle(a.config)
+    kernels = {}
+    for name, (ms, n) in kt.items():
+        avg_us = ms * 1e3 / max(n, 1)
+        by = algorithmic_bytes(name, N, b_in, pairs, pixels)
+        kernels[name] = {"avg_us": round(avg_us, 2), "launches": n, "alg_bytes": by,
+                         "gbps": round(by / (avg_us * 1e-6) / 1e9, 1) if by and avg_us > 0 else None}
+    dom = max(kt, key=lambda k: kt[k][0]) if kt else "tile"
+    dk = kernels.get(dom, {})
+    traffic = None
+    if os.path.exists(a.pmc):
+        with open(a.pmc) as fh:
+            pmc = json.load(fh)
+        if pmc.get("kernel") == dom and pmc.get("config") == a.config:
+            traffic = pmc.get("hbm_bytes_per_launch")
+    achieved = dk.get("gbps") or 0.0
+
+    ms_per_step = elapsed / a.steps * 1e3
+    value = N * a.steps / elapsed / 1e6
+    frame_bytes = N * b_in + W * H * 8
+    out = {
+        "metric": METRIC, "value": round(value, 2), "unit": "Mtri/s", "n_gpus": world, "steps": a.steps,
+        "warmup": a.warmup, "ms_per_step": round(ms_per_step, 4), "higher_is_better": True,
+        "scaling": "strong", "vs_baseline": None, "dtype": "f32",
+        "data": "synthetic (SplitMix64 triangle soup, SURVEY.md §8d)",
+        "config": {"workload": f"{a.config}: {N} tris soup, {W}x{H}, "
+                               f"{'Blinn-Phong' if scene.program == scenes.PROGRAM_BLINN_PHONG else 'flat'} "
+                               f"+ D32 LESS, B8G8R8A8_SRGB",
+                   "triangles": N, "width": W, "height": H, "tile": shard.TILE,
+                   "parallelism": f"tile-rows x{world}" + (" + RCCL row gather" if world > 1 else "")},
+        "fps": round(1e3 / ms_per_step, 2),
+        "frame_alg_bytes": frame_bytes,
+        "frame_gbps": round(frame_bytes / (ms_per_step * 1e-3) / 1e9, 1),
+        "roofline": {"bound": "hbm", "kernel": dom, "achieved": achieved, "peak": HBM_PEAK_GBPS, "unit": "GB/s",
+                     "frac": round(achieved / HBM_PEAK_GBPS, 4), "traffic": traffic,
+                     "peak_measured_copy": HBM_MEASURED_GBPS},
+        "kernels": kernels,
+        "bin_pairs": pairs,
+        "triangles_setup": stats["triangles_setup"],
+    }
+    if rank == 0 and world == 1 and not a.no_cpu_baseline:
+        out["cpu_baseline"] = cpu_baseline(scene, a.cpu_frames)
+    elif rank == 0:
+        out["cpu_baseline"] = None
+    if rank == 0:
+        print(json.dumps(out), flush=True)
+    enc.destroy()
+    color.destroy()
+    depth.destroy()
+    dev.close()
+    if world > 1:
+        dist.destroy_process_group()
+
+
+if __name__ == "__main__":
+    main()
