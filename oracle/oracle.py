@@ -143,7 +143,8 @@ def render(scene, tile_size: int = 32, shard=(0, 1), nthreads: int = 1, with_sta
                     scene.cull_mode, scene.front_face, 1 if scene.depth_test else 0,
                     1 if scene.depth_write else 0, scene.depth_op, scene.write_mask, tile_size,
                     shard[0], shard[1])
-    cmd = _DrawCmd(scene.draw_count, 1, 0, 0, 0, 1 if ib is not None else 0)
+    cmd = _DrawCmd(scene.draw_count, scene.instance_count, scene.first, scene.vertex_offset, 0,
+                   1 if ib is not None else 0)
     stats = Stats()
     rc = L.zro_draw(C.byref(tgt), C.byref(st), C.byref(vi), C.byref(cmd), nthreads, C.byref(stats))
     if rc != 0:

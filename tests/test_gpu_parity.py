@@ -92,3 +92,133 @@ def test_depth_modes(device, op, write):
 def test_c1_scaled(device):
     s = scenes.config_scene("c1", n=20000, width=640, height=360)
     assert_parity(device, s)
+
+
+# ---------------------------------------------------------- coverage of paths
+def test_large_triangles_wave_path(device):
+    """Primitives beyond the 64-px "small" bound take the wave-cooperative path."""
+    s = scenes.soup_scene(13, 400, 512, 384, 150.0, scenes.PROGRAM_BLINN_PHONG)
+    assert_parity(device, s)
+
+
+def test_mixed_sizes(device):
+    a = scenes.soup_scene(14, 1500, 300, 200, 6.0, scenes.PROGRAM_FLAT_COLOR)
+    b = scenes.soup_scene(15, 60, 300, 200, 120.0, scenes.PROGRAM_FLAT_COLOR)
+    v = np.concatenate([a.vertices[:1500], b.vertices[:60], a.vertices[1500:]])
+    s = scenes.Scene("mixed", 300, 200, scenes.PROGRAM_FLAT_COLOR, v, np.arange(v.shape[0], dtype=np.uint32),
+                     depth=True)
+    assert_parity(device, s)
+
+
+def test_bin_overflow_replay(monkeypatch):
+    """A bin buffer too small for the draw's (tile, primitive) pairs is detected,
+    grown and the submission replayed; the image is still exact."""
+    monkeypatch.setenv("ZR_BIN_CAPACITY", "1024")
+    dev = rhi.RenderDevice(0)
+    try:
+        s = scenes.soup_scene(16, 3000, 640, 480, 40.0, scenes.PROGRAM_FLAT_COLOR)
+        assert_parity(dev, s)
+        st = dev.last_draw_stats()
+        assert st["replays"] >= 1 and st["bin_pairs"] > 1024 and st["bin_capacity"] >= st["bin_pairs"]
+    finally:
+        dev.close()
+
+
+@pytest.mark.parametrize("fmt", [zr.FORMAT_R8G8B8A8_UNORM, zr.FORMAT_B8G8R8A8_UNORM, zr.FORMAT_R8G8B8A8_SRGB,
+                                 zr.FORMAT_R32G32B32A32_SFLOAT])
+def test_color_formats(device, fmt):
+    s = scenes.soup_scene(17, 800, 160, 120, 12.0, scenes.PROGRAM_BLINN_PHONG)
+    s.color_format = fmt
+    assert_parity(device, s)
+
+
+@pytest.mark.parametrize("mask", [0x1, 0x6, 0x8, 0xB])
+def test_write_masks(device, mask):
+    s = scenes.soup_scene(18, 600, 128, 96, 10.0, scenes.PROGRAM_FLAT_COLOR)
+    s.write_mask = mask
+    assert_parity(device, s)
+
+
+@pytest.mark.parametrize("cull,front", [(scenes.CULL_BACK, scenes.FRONT_CCW), (scenes.CULL_BACK, scenes.FRONT_CW),
+                                        (scenes.CULL_FRONT, scenes.FRONT_CCW), (3, scenes.FRONT_CCW)])
+def test_cull_modes(device, cull, front):
+    s = scenes.soup_scene(19, 1000, 160, 120, 12.0, scenes.PROGRAM_FLAT_COLOR)
+    s.cull_mode, s.front_face = cull, front
+    assert_parity(device, s)
+
+
+@pytest.mark.parametrize("vp,sc", [((20.0, 10.0, 200.0, 150.0, 0.0, 1.0), (30, 20, 150, 100)),
+                                   ((0.0, 180.0, 256.0, -180.0, 0.0, 1.0), (0, 0, 256, 180)),
+                                   ((-40.0, -30.0, 320.0, 240.0, 0.25, 0.75), (5, 7, 240, 160))])
+def test_viewport_scissor(device, vp, sc):
+    s = scenes.soup_scene(20, 1200, 256, 180, 14.0, scenes.PROGRAM_FLAT_COLOR)
+    assert_parity(device, s, viewport=vp, scissor=sc)
+
+
+def test_draw_arguments(device):
+    """u16 indices with first_index / vertex_offset, instancing, non-indexed draws."""
+    base = scenes.soup_scene(23, 300, 128, 128, 12.0, scenes.PROGRAM_FLAT_COLOR)
+    s = scenes.Scene("args", 128, 128, scenes.PROGRAM_FLAT_COLOR, base.vertices,
+                     np.arange(base.vertices.shape[0] - 30, dtype=np.uint16), depth=True,
+                     first=12, vertex_offset=30, count=600, instance_count=2)
+    assert_parity(device, s)
+    s2 = scenes.Scene("nonindexed", 128, 128, scenes.PROGRAM_FLAT_COLOR, base.vertices, None, depth=True,
+                      first=9, count=450)
+    assert_parity(device, s2)
+
+
+def test_out_of_range_indices_dropped(device):
+    base = scenes.soup_scene(24, 200, 128, 128, 12.0, scenes.PROGRAM_FLAT_COLOR)
+    idx = np.arange(600, dtype=np.uint32)
+    idx[::7] = 10_000_000  # beyond the vertex buffer: those primitives are discarded
+    s = scenes.Scene("oob", 128, 128, scenes.PROGRAM_FLAT_COLOR, base.vertices, idx, depth=True)
+    assert_parity(device, s)
+
+
+@pytest.mark.parametrize("world", [2, 3, 8])
+def test_tile_row_shards(device, world):
+    s = scenes.soup_scene(25, 3000, 320, 240, 10.0, scenes.PROGRAM_BLINN_PHONG)
+    for r in range(world):
+        assert_parity(device, s, shard=(r, world))
+
+
+# ------------------------------------------------------- full benchmark sizes
+@pytest.mark.parametrize("cfg", ["c1", "c2"])
+def test_full_config_parity(device, cfg):
+    """C1 (100k tris) and C2 (1M tris) at 1920x1080, bit-exact vs the oracle."""
+    s = scenes.config_scene(cfg)
+    gc, gd = renderer.render_scene(device, s)
+    st = device.last_draw_stats()
+    oc, od, ost = oracle.render(s, nthreads=16, with_stats=True)
+    assert np.array_equal(gc, oc)
+    assert np.array_equal(gd.view(np.uint32), od.view(np.uint32))
+    assert st["triangles_setup"] == ost.triangles_setup
+
+
+def test_c3_4k_shards_union(device):
+    """C3 geometry (1M tris, 3840x2160): the union of 8 tile-row shards rendered
+    separately equals the oracle frame (the multi-GPU partition, on one GPU)."""
+    s = scenes.config_scene("c3")
+    oc, od = oracle.render(s, nthreads=16)
+    acc = np.zeros_like(oc)
+    for r in range(8):
+        gc, _ = renderer.render_scene(device, s, shard=(r, 8))
+        rows = owned_rows(s.height, 32, (r, 8))
+        acc[rows] = gc[rows]
+    assert np.array_equal(acc, oc)
+
+
+def test_c4_micro_triangles(device):
+    """C4: 10M sub-pixel triangles at 1080p; exact vs the oracle."""
+    s = scenes.config_scene("c4")
+    gc, gd = renderer.render_scene(device, s)
+    oc, od = oracle.render(s, nthreads=16)
+    assert np.array_equal(gc, oc)
+    assert np.array_equal(gd.view(np.uint32), od.view(np.uint32))
+
+
+def test_determinism_repeat(device):
+    s = scenes.config_scene("c2", n=200_000)
+    a = renderer.render_scene(device, s)
+    b = renderer.render_scene(device, s)
+    assert np.array_equal(a[0], b[0]) and np.array_equal(a[1].view(np.uint32), b[1].view(np.uint32))

@@ -9,7 +9,9 @@ constexpr int kTile = 32;          // screen-tile edge in pixels (one workgroup 
 constexpr int kTileShift = 5;
 constexpr int kTilePixels = kTile * kTile;
 constexpr int kTileThreads = 256;  // 4 waves of 64
-constexpr int kSetupThreads = 256;
+constexpr uint32_t kSortCap = 1024;     // tile-list segment sorted by area in LDS
+constexpr uint32_t kSortBuckets = 64;   // 4-pixel-wide area buckets (last: > 252 px)
+constexpr int kSetupThreads = 1024;  // setup / bin workgroups (one LDS histogram each)
 
 enum Program : int32_t { kProgTriangle = 0, kProgFlat = 1, kProgBlinn = 2, kProgCount = 3 };
 
@@ -31,15 +33,32 @@ struct alignas(16) TriRecord {
     int32_t X2, Y2;
     float z0, dz1;            // z0, z1 - z0
     float dz2, invA2;         // z2 - z0, 1 / (float)A2
-    float invw0, invw1;       // 1 / w_clip (perspective correction)
-    float invw2;
+    uint32_t v0, v1;          // vertex ids in record order (after the v1/v2 swap).  The built-in
+    uint32_t v2;              // vertex stages emit w = 1 (triangle.slang:22), so 1/w = 1 and the
+                              // perspective weights equal the barycentrics
     uint32_t bb0;             // px0 | py0 << 16  (inclusive pixel bbox, clipped)
     uint32_t bb1;             // px1 | py1 << 16
-    uint32_t flags;           // bit0 swapped v1<->v2, bits1..3 edge bias (0 = top-left edge)
+    uint32_t flags;           // bit0 swapped v1<->v2, bits1..3 edge bias (0 = top-left edge), bit4 small
 };
 static_assert(sizeof(TriRecord) == 64, "TriRecord must be 64 B");
 
-enum : uint32_t { kFlagSwapped = 1u, kFlagBias0 = 2u, kFlagBias1 = 4u, kFlagBias2 = 8u };
+enum : uint32_t { kFlagSwapped = 1u, kFlagBias0 = 2u, kFlagBias1 = 4u, kFlagBias2 = 8u, kFlagSmall = 16u };
+// A primitive is "small" when its fixed-point bbox spans <= 64 px in x and y: every
+// edge function inside it then fits int32 (|w| <= 2^29), so the lane-parallel
+// raster path steps edges incrementally in 32-bit integers.
+constexpr int32_t kSmallExtent = 64 * 256;
+constexpr uint32_t kEmptyBox = 0xFFFFFFFFu;
+// Bin entry = primitive id | (area bucket of its bbox ∩ tile) << kBinPrimBits
+constexpr uint32_t kBinPrimBits = 26;
+constexpr uint32_t kBinPrimMask = (1u << kBinPrimBits) - 1u;
+struct alignas(8) BBox {
+    uint32_t bb0, bb1;  // as TriRecord::bb0/bb1
+};
+constexpr uint32_t kMaxTilesPerPass = 16384;  // LDS histogram of the setup pass (64 KB)
+
+// Timing-experiment switches (ZR_DEBUG env var); never set in production runs.
+enum : uint32_t { kDebugSkipRaster = 1u, kDebugSkipShade = 2u, kDebugNoAtomic = 8u, kDebugLoadOnly = 16u,
+                  kDebugPhase1Only = 32u, kDebugStopAfterScan = 64u, kDebugStamps = 128u };
 
 // Status words in host-mapped pinned memory (read by the runtime at sync points).
 enum StatusWord : uint32_t {
@@ -48,10 +67,11 @@ enum StatusWord : uint32_t {
     kStMaxPairs = 2,
     kStTrianglesSetup = 3,
     kStDroppedClip = 4,
+    kStBarrierTimeout = 5,
     kStWords = 16,
 };
 // Device-side counters (zeroed with the tile counts before each draw).
-enum CounterWord : uint32_t { kCtSetup = 0, kCtDropped = 1, kCtWords = 4 };
+enum CounterWord : uint32_t { kCtSetup = 0, kCtDropped = 1, kCtBarrier = 2, kCtWords = 4 };
 
 struct DrawParams {
     // vertex input (binding 0) and index buffer
@@ -96,21 +116,26 @@ struct DrawParams {
     const float* time_ptr;    // Time.time uniform (device) or nullptr
     // tiling / sharding
     uint32_t tiles_x, tiles_y, shard_rank, shard_count, owned_rows, ntiles;
-    // scratch
-    TriRecord* records;
-    uint32_t* tri_ntiles;
-    uint32_t* tile_counts;    // [ntiles] followed by kCtWords counters
-    uint32_t* tile_offsets;   // exclusive scan; ends after k_bin
-    uint32_t* bins;
+    // scratch (binning without contended global atomics)
+    TriRecord* records;       // [prims]
+    BBox* bboxes;             // [prims]; bb0 == kEmptyBox when culled / no owned tile
+    uint32_t* counts;         // M[setup_wgs][ntiles]: per-workgroup tile histograms, then offsets
+    uint32_t* tile_counts;    // [ntiles]
+    uint32_t* tile_offsets;   // [ntiles] exclusive scan (list starts)
+    uint32_t* counters;       // [kCtWords]
+    uint32_t* bins;           // [bin_capacity] primitive ids grouped by tile
     uint32_t bin_capacity;
+    uint32_t setup_wgs;       // workgroups of k_setup_bin (<= CUs: all resident)
+    uint32_t tris_per_thread; // primitives per setup thread (chunk = kSetupThreads * this)
+    uint32_t debug;           // kDebug* bits (timing experiments only)
+    unsigned long long* dbg_ts; // [setup_wgs][8] s_memrealtime stamps (kDebugStamps only)
     uint32_t* status;         // host-mapped
 };
 
 // Launchers (zr_kernels.hip).  All enqueue on `stream`; no host synchronisation.
-struct KernelTimer;
-void launch_setup(const DrawParams& p, void* stream);
-void launch_scan(const DrawParams& p, void* stream);
-void launch_bin(const DrawParams& p, void* stream);
+void launch_setup_bin(const DrawParams& p, void* stream);  // persistent: setup + scan + scatter
+size_t setup_bin_lds_bytes(uint32_t ntiles);
+const void* setup_bin_kernel();
 void launch_tile(const DrawParams& p, void* stream);
 void launch_clear(const DrawParams& p, void* stream);
 

@@ -1,12 +1,15 @@
 // zr_kernels.hip — the MI355X (gfx950) draw path: setup -> scan -> bin -> tile.
 //
 // Pass structure:
-//   k_setup  one thread per primitive: index + vertex fetch, vertex stage
+//   k_setup  chunks of primitives per workgroup: index + vertex fetch, vertex stage
 //            (triangle.slang:19-25: SV_Position = float4(position, 1)), viewport
 //            transform, 8-bit sub-pixel snap, facing/cull, orientation, top-left
-//            biases, clipped pixel bbox -> 64-B TriRecord; per-tile overlap counts.
-//   k_scan   one workgroup: exclusive scan of the per-tile counts.
-//   k_bin    one thread per primitive: scatter primitive ids into per-tile lists.
+//            biases, clipped pixel bbox -> 64-B TriRecord; per-workgroup LDS
+//            histogram of tile overlaps -> counts[wg][tile].
+//   k_colsum/k_scan_tiles/k_apply  column scan of counts -> per-(wg, tile)
+//            list offsets, per-tile list starts and lengths.
+//   k_bin    same chunks: scatter primitive ids into per-tile lists through LDS
+//            cursors (no global atomics anywhere in binning).
 //   k_tile   one 256-thread workgroup per 32x32 screen tile: LDS-resident 64-bit
 //            visibility keys (depth | primitive sequence) updated with ds_min_u64
 //            by a wave per primitive (lanes over the primitive's bbox ∩ tile),
@@ -40,21 +43,6 @@ __device__ __forceinline__ bool fetch_index(const DrawParams& P, uint64_t e, int
 
 __device__ __forceinline__ const float* attr_ptr(const DrawParams& P, uint32_t vid, uint32_t loc) {
     return (const float*)(P.vb + (uint64_t)vid * P.stride + P.attr_offset[loc]);
-}
-
-__device__ __forceinline__ void prim_vids(const DrawParams& P, uint32_t prim, uint32_t flags, uint32_t vid[3]) {
-    const uint32_t tri = (P.tris_per_instance == P.prims) ? prim : prim % P.tris_per_instance;
-#pragma unroll
-    for (int k = 0; k < 3; ++k) {
-        int64_t v;
-        fetch_index(P, (uint64_t)P.first + (uint64_t)tri * 3u + (uint64_t)k, v);
-        vid[k] = (uint32_t)v;
-    }
-    if (flags & kFlagSwapped) {
-        const uint32_t t = vid[1];
-        vid[1] = vid[2];
-        vid[2] = t;
-    }
 }
 
 __device__ __forceinline__ bool depth_pass(int op, float z, float d) {
@@ -135,119 +123,202 @@ __device__ __forceinline__ float interp_depth(const TriRecord& r, long long w1, 
 }
 
 // ------------------------------------------------------------------ k_setup
+//
+// One workgroup per chunk of 256 * tris_per_thread primitives (coalesced: step k
+// of every thread covers 256 consecutive primitives).  Tile overlaps are counted
+// in an LDS histogram (no global atomics); the histogram row is written to
+// counts[wg][*] for the column scan.
 
-__global__ __launch_bounds__(kSetupThreads) void k_setup(DrawParams P) {
-    const uint32_t prim = blockIdx.x * kSetupThreads + threadIdx.x;
-    uint32_t ntiles = 0;
-    int valid = 0, dropped = 0;
-    if (prim < P.prims) {
-        const uint32_t tri = (P.tris_per_instance == P.prims) ? prim : prim % P.tris_per_instance;
-        uint32_t vid[3];
-        bool ok = true;
+// Primitive assembly, split in stages so that a thread's loads for several
+// primitives are in flight together (index loads, then position loads, then math).
+struct PrimIn {
+    uint32_t vid[3];
+    float3 p[3];
+    bool ok;
+};
+
+__device__ __forceinline__ void fetch_indices(const DrawParams& P, uint32_t prim, PrimIn& in) {
+    in.ok = prim < P.prims;
+    if (!in.ok) return;
+    const uint32_t tri = (P.tris_per_instance == P.prims) ? prim : prim % P.tris_per_instance;
+    const uint64_t e0 = (uint64_t)P.first + (uint64_t)tri * 3u;
+    bool ok = true;
+    if (P.index_size == 4 && (e0 + 3) * 4 <= P.ib_bytes) {
+        const uint3 ix = *reinterpret_cast<const uint3*>(P.ib + e0 * 4);  // one 12-B load
+        const int64_t v0 = (int64_t)ix.x + P.vertex_offset, v1 = (int64_t)ix.y + P.vertex_offset,
+                      v2 = (int64_t)ix.z + P.vertex_offset;
+        ok = v0 >= 0 && v0 <= 0xFFFFFFFFll && v1 >= 0 && v1 <= 0xFFFFFFFFll && v2 >= 0 && v2 <= 0xFFFFFFFFll;
+        in.vid[0] = (uint32_t)v0; in.vid[1] = (uint32_t)v1; in.vid[2] = (uint32_t)v2;
+    } else {
 #pragma unroll
         for (int k = 0; k < 3; ++k) {
             int64_t v = 0;
-            ok = ok && fetch_index(P, (uint64_t)P.first + (uint64_t)tri * 3u + (uint64_t)k, v);
+            ok = ok && fetch_index(P, e0 + (uint64_t)k, v);
             ok = ok && v >= 0 && v <= 0xFFFFFFFFll;
-            vid[k] = (uint32_t)v;
-            for (uint32_t a = 0; a < P.nattr; ++a)
-                ok = ok && ((uint64_t)vid[k] * P.stride + P.attr_offset[a] + 12 <= P.vb_bytes);
+            in.vid[k] = (uint32_t)v;
         }
-        int32_t X[3], Y[3];
-        float z[3], invw[3];
-        if (ok) {
-#pragma unroll
-            for (int k = 0; k < 3; ++k) {
-                const float* pos = attr_ptr(P, vid[k], 0);
-                const float x = pos[0], y = pos[1], zc = pos[2], w = 1.0f;  // vsmain
-                if (!(w > 0.0f)) { dropped = 1; ok = false; break; }
-                const float xd = x / w, yd = y / w, zd = zc / w;
-                const float xf = fmaf(xd, P.hw, P.cx), yf = fmaf(yd, P.hh, P.cy);
-                if (!(fabsf(xf) < 4194304.0f && fabsf(yf) < 4194304.0f)) { dropped = 1; ok = false; break; }
-                X[k] = (int32_t)rintf(xf * 256.0f);
-                Y[k] = (int32_t)rintf(yf * 256.0f);
-                z[k] = fmaf(zd, P.dr, P.dmin);
-                invw[k] = 1.0f / w;
-            }
-        }
-        if (ok) {
-            long long A2 = (long long)(X[1] - X[0]) * (Y[2] - Y[0]) - (long long)(X[2] - X[0]) * (Y[1] - Y[0]);
-            const bool ccw = A2 < 0;  // Vulkan: a = -A2/2 > 0 is counter-clockwise
-            const bool front = (P.front_face == 0) ? ccw : !ccw;
-            ok = A2 != 0 && !((P.cull_mode & 1u) && front) && !((P.cull_mode & 2u) && !front);
-            uint32_t flags = 0;
-            if (ok && A2 < 0) {
-                int32_t t = X[1]; X[1] = X[2]; X[2] = t;
-                t = Y[1]; Y[1] = Y[2]; Y[2] = t;
-                float f = z[1]; z[1] = z[2]; z[2] = f;
-                f = invw[1]; invw[1] = invw[2]; invw[2] = f;
-                A2 = -A2;
-                flags |= kFlagSwapped;
-            }
-            int32_t px0 = 0, py0 = 0, px1 = -1, py1 = -1;
-            if (ok) {
-                // top-left rule (y-down): edge i is opposite vertex i
-#pragma unroll
-                for (int i = 0; i < 3; ++i) {
-                    const int a = (i + 1) % 3, b = (i + 2) % 3;
-                    const int32_t dx = X[b] - X[a], dy = Y[b] - Y[a];
-                    const bool tl = (dy < 0) || (dy == 0 && dx > 0);
-                    if (!tl) flags |= (kFlagBias0 << i);
-                }
-                const int32_t minX = min(X[0], min(X[1], X[2])), maxX = max(X[0], max(X[1], X[2]));
-                const int32_t minY = min(Y[0], min(Y[1], Y[2])), maxY = max(Y[0], max(Y[1], Y[2]));
-                px0 = max((minX - 128 + 255) >> 8, P.clip_x0);
-                px1 = min((maxX - 128) >> 8, P.clip_x1);
-                py0 = max((minY - 128 + 255) >> 8, P.clip_y0);
-                py1 = min((maxY - 128) >> 8, P.clip_y1);
-                ok = px0 <= px1 && py0 <= py1;
-            }
-            if (ok) {
-                valid = 1;
-                const int tx0 = px0 >> kTileShift, tx1 = px1 >> kTileShift;
-                const int ty0 = py0 >> kTileShift, ty1 = py1 >> kTileShift;
-                for (int ty = ty0; ty <= ty1; ++ty) {
-                    if ((uint32_t)ty % P.shard_count != P.shard_rank) continue;
-                    const uint32_t row = ((uint32_t)ty / P.shard_count) * P.tiles_x;
-                    for (int tx = tx0; tx <= tx1; ++tx) atomicAdd(&P.tile_counts[row + tx], 1u);
-                    ntiles += (uint32_t)(tx1 - tx0 + 1);
-                }
-                if (ntiles) {
-                    TriRecord r;
-                    r.X0 = X[0]; r.Y0 = Y[0]; r.X1 = X[1]; r.Y1 = Y[1]; r.X2 = X[2]; r.Y2 = Y[2];
-                    r.z0 = z[0];
-                    r.dz1 = z[1] - z[0];
-                    r.dz2 = z[2] - z[0];
-                    r.invA2 = 1.0f / (float)A2;
-                    r.invw0 = invw[0]; r.invw1 = invw[1]; r.invw2 = invw[2];
-                    r.bb0 = (uint32_t)px0 | ((uint32_t)py0 << 16);
-                    r.bb1 = (uint32_t)px1 | ((uint32_t)py1 << 16);
-                    r.flags = flags;
-                    P.records[prim] = r;
-                }
-            }
-        }
-        P.tri_ntiles[prim] = ntiles;
     }
-    const int nvalid = __syncthreads_count(valid);
-    const int ndropped = __syncthreads_count(dropped);
-    if (threadIdx.x == 0) {
-        uint32_t* ct = P.tile_counts + P.ntiles;
-        if (nvalid) atomicAdd(&ct[kCtSetup], (uint32_t)nvalid);
-        if (ndropped) atomicAdd(&ct[kCtDropped], (uint32_t)ndropped);
-    }
+    in.ok = ok;
 }
 
-// ------------------------------------------------------------------- k_scan
+__device__ __forceinline__ void fetch_positions(const DrawParams& P, PrimIn& in) {
+    if (!in.ok) return;
+    bool ok = true;
+#pragma unroll
+    for (int k = 0; k < 3; ++k)
+        for (uint32_t a = 0; a < P.nattr; ++a)
+            ok = ok && ((uint64_t)in.vid[k] * P.stride + P.attr_offset[a] + 12 <= P.vb_bytes);
+    in.ok = ok;
+    if (!ok) return;
+#pragma unroll
+    for (int k = 0; k < 3; ++k) in.p[k] = *reinterpret_cast<const float3*>(attr_ptr(P, in.vid[k], 0));  // 12-B loads
+}
 
-__global__ __launch_bounds__(1024) void k_scan(DrawParams P) {
-    __shared__ uint32_t s_wave[16];
-    const uint32_t n = P.ntiles, tid = threadIdx.x;
+__device__ __forceinline__ void setup_finish(const DrawParams& P, uint32_t prim, const PrimIn& in, uint32_t* s_hist,
+                                             int& nvalid, int& ndropped) {
+    if (prim >= P.prims) return;
+    bool ok = in.ok;
+    int32_t X[3], Y[3];
+    float z[3];
+    uint32_t rv[3] = {in.vid[0], in.vid[1], in.vid[2]};
+    BBox box{kEmptyBox, 0u};
+    if (ok) {
+#pragma unroll
+        for (int k = 0; k < 3; ++k) {
+            const float x = in.p[k].x, y = in.p[k].y, zc = in.p[k].z, w = 1.0f;  // vsmain (triangle.slang:22)
+            if (!(w > 0.0f)) { ++ndropped; ok = false; break; }
+            const float xd = x / w, yd = y / w, zd = zc / w;
+            const float xf = fmaf(xd, P.hw, P.cx), yf = fmaf(yd, P.hh, P.cy);
+            if (!(fabsf(xf) < 4194304.0f && fabsf(yf) < 4194304.0f)) { ++ndropped; ok = false; break; }
+            X[k] = (int32_t)rintf(xf * 256.0f);
+            Y[k] = (int32_t)rintf(yf * 256.0f);
+            z[k] = fmaf(zd, P.dr, P.dmin);
+        }
+    }
+    if (ok) {
+        long long A2 = (long long)(X[1] - X[0]) * (Y[2] - Y[0]) - (long long)(X[2] - X[0]) * (Y[1] - Y[0]);
+        const bool ccw = A2 < 0;  // Vulkan: a = -A2/2 > 0 is counter-clockwise
+        const bool front = (P.front_face == 0) ? ccw : !ccw;
+        ok = A2 != 0 && !((P.cull_mode & 1u) && front) && !((P.cull_mode & 2u) && !front);
+        uint32_t flags = 0;
+        if (ok && A2 < 0) {
+            int32_t t = X[1]; X[1] = X[2]; X[2] = t;
+            t = Y[1]; Y[1] = Y[2]; Y[2] = t;
+            float f = z[1]; z[1] = z[2]; z[2] = f;
+            const uint32_t u = rv[1]; rv[1] = rv[2]; rv[2] = u;
+            A2 = -A2;
+            flags |= kFlagSwapped;
+        }
+        int32_t px0 = 0, py0 = 0, px1 = -1, py1 = -1;
+        if (ok) {
+#pragma unroll
+            for (int i = 0; i < 3; ++i) {  // top-left rule (y-down), edge i opposite vertex i
+                const int a = (i + 1) % 3, b = (i + 2) % 3;
+                const int32_t dx = X[b] - X[a], dy = Y[b] - Y[a];
+                const bool tl = (dy < 0) || (dy == 0 && dx > 0);
+                if (!tl) flags |= (kFlagBias0 << i);
+            }
+            const int32_t minX = min(X[0], min(X[1], X[2])), maxX = max(X[0], max(X[1], X[2]));
+            const int32_t minY = min(Y[0], min(Y[1], Y[2])), maxY = max(Y[0], max(Y[1], Y[2]));
+            if (maxX - minX <= kSmallExtent && maxY - minY <= kSmallExtent) flags |= kFlagSmall;
+            px0 = max((minX - 128 + 255) >> 8, P.clip_x0);
+            px1 = min((maxX - 128) >> 8, P.clip_x1);
+            py0 = max((minY - 128 + 255) >> 8, P.clip_y0);
+            py1 = min((maxY - 128) >> 8, P.clip_y1);
+            ok = px0 <= px1 && py0 <= py1;
+        }
+        if (ok) {
+            ++nvalid;
+            const int tx0 = px0 >> kTileShift, tx1 = px1 >> kTileShift;
+            const int ty0 = py0 >> kTileShift, ty1 = py1 >> kTileShift;
+            uint32_t owned = 0;
+            for (int ty = ty0; ty <= ty1; ++ty) {
+                if ((uint32_t)ty % P.shard_count != P.shard_rank) continue;
+                const uint32_t row = ((uint32_t)ty / P.shard_count) * P.tiles_x;
+                for (int tx = tx0; tx <= tx1; ++tx) atomicAdd(&s_hist[row + tx], 1u);
+                owned += (uint32_t)(tx1 - tx0 + 1);
+            }
+            if (owned) {
+                TriRecord r;
+                r.X0 = X[0]; r.Y0 = Y[0]; r.X1 = X[1]; r.Y1 = Y[1]; r.X2 = X[2]; r.Y2 = Y[2];
+                r.z0 = z[0];
+                r.dz1 = z[1] - z[0];
+                r.dz2 = z[2] - z[0];
+                r.invA2 = 1.0f / (float)A2;
+                r.v0 = rv[0]; r.v1 = rv[1]; r.v2 = rv[2];
+                r.bb0 = (uint32_t)px0 | ((uint32_t)py0 << 16);
+                r.bb1 = (uint32_t)px1 | ((uint32_t)py1 << 16);
+                r.flags = flags;
+                P.records[prim] = r;
+                box.bb0 = r.bb0;
+                box.bb1 = r.bb1;
+            }
+        }
+    }
+    P.bboxes[prim] = box;
+}
+
+// ------------------------------------------------------------ grid barrier
+//
+// Monotonic-counter barrier for the persistent binning kernel (one workgroup per
+// CU, so every workgroup is resident).  Protocol per cdna_hip_programming.md §6
+// G16 / MI355X_MICROARCH.md "Valid forms": every storing wave drains its stores,
+// the workgroup meets, lane 0 releases at agent scope, arrives with a relaxed
+// agent atomic, polls relaxed with s_sleep (bounded), then acquires at agent
+// scope before the workgroup reads other workgroups' data.
+__device__ __forceinline__ void grid_barrier(uint32_t* counter, uint32_t target, uint32_t* status) {
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // every storing wave drains its (sc1) stores
+    __syncthreads();
+    if (threadIdx.x == 0) {
+        __hip_atomic_fetch_add(counter, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        uint32_t spins = 0;
+        while (__hip_atomic_load(counter, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) < target) {
+            __builtin_amdgcn_s_sleep(1);
+            if (++spins > (1u << 24)) {  // never expected: report instead of hanging
+                ((volatile uint32_t*)status)[kStBarrierTimeout] = 1u;
+                break;
+            }
+        }
+        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");  // compiler-only: keep loads below the poll
+    }
+    __syncthreads();
+}
+
+// Hand-off words between workgroups of k_setup_bin are written and read with
+// sc1 (agent-scope relaxed atomics): write-through stores, L1-bypassing loads.
+// That is "Valid forms" row 1 of MI355X_MICROARCH.md §Workgroup dispatch, which
+// needs no release/acquire fence -- a release would also write back the XCD
+// L2's freshly written records (hundreds of KB per workgroup).
+__device__ __forceinline__ void st_sc1(uint32_t* p, uint32_t v) {
+    __hip_atomic_store(p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+__device__ __forceinline__ uint32_t ld_sc1(const uint32_t* p) {
+    return __hip_atomic_load(const_cast<uint32_t*>(p), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+
+template <int R>
+__device__ __forceinline__ uint32_t load_rows(const uint32_t* counts, uint32_t nt, uint32_t cc, uint32_t r0, uint32_t r1,
+                                              uint32_t G, bool col_ok, uint32_t (&v)[16]) {
+    uint32_t sum = 0;
+#pragma unroll
+    for (int i = 0; i < R; ++i) v[i] = ld_sc1(&counts[(size_t)min(r0 + (uint32_t)i, G - 1u) * nt + cc]);
+#pragma unroll
+    for (int i = 0; i < R; ++i) {
+        v[i] = (col_ok && r0 + (uint32_t)i < r1) ? v[i] : 0u;
+        sum += v[i];
+    }
+#pragma unroll
+    for (int i = R; i < 16; ++i) v[i] = 0u;
+    return sum;
+}
+
+// Exclusive scan of a[0..n) in LDS by a 1024-thread workgroup; returns the total.
+__device__ __forceinline__ uint32_t block_exclusive_scan(uint32_t* a, uint32_t n, uint32_t* s_wave) {
+    const uint32_t tid = threadIdx.x;
     const uint32_t per = (n + 1023u) / 1024u;
     const uint32_t beg = min(tid * per, n), end = min(beg + per, n);
     uint32_t sum = 0;
-    for (uint32_t i = beg; i < end; ++i) sum += P.tile_counts[i];
-    // wave-level inclusive scan
+    for (uint32_t i = beg; i < end; ++i) sum += a[i];
     const int lane = tid & 63, wave = tid >> 6;
     uint32_t incl = sum;
 #pragma unroll
@@ -258,68 +329,217 @@ __global__ __launch_bounds__(1024) void k_scan(DrawParams P) {
     if (lane == 63) s_wave[wave] = incl;
     __syncthreads();
     if (tid < 16) {
-        uint32_t w = s_wave[tid], wi = w;
+        const uint32_t w = s_wave[tid];
+        uint32_t wi = w;
 #pragma unroll
         for (int d = 1; d < 16; d <<= 1) {
             const uint32_t v = __shfl_up(wi, d, 16);
             if ((int)tid >= d) wi += v;
         }
-        s_wave[tid] = wi - w;  // exclusive wave base
+        s_wave[tid] = wi - w;
+        if (tid == 15) s_wave[16] = wi;
     }
     __syncthreads();
     uint32_t run = s_wave[wave] + incl - sum;
     for (uint32_t i = beg; i < end; ++i) {
-        P.tile_offsets[i] = run;
-        run += P.tile_counts[i];
+        const uint32_t c = a[i];
+        a[i] = run;
+        run += c;
     }
-    if (tid == 1023) {
-        const uint32_t total = run;
-        volatile uint32_t* st = P.status;
-        st[kStTotalPairs] = total;
-        if (total > P.bin_capacity) st[kStOverflow] = 1u;
-        if (total > st[kStMaxPairs]) st[kStMaxPairs] = total;
-        const uint32_t* ct = P.tile_counts + P.ntiles;
-        st[kStTrianglesSetup] = ct[kCtSetup];
-        st[kStDroppedClip] = ct[kCtDropped];
-    }
+    const uint32_t total = s_wave[16];
+    __syncthreads();
+    return total;
 }
 
-// -------------------------------------------------------------------- k_bin
+// ----------------------------------------------------------- k_setup_bin
+//
+// One persistent launch, one 1024-thread workgroup per CU, chunk w of the draw's
+// primitives per workgroup:
+//   phase 1  setup + records, per-workgroup LDS tile histogram -> counts[w][*]
+//   -- grid barrier --
+//   phase 2  column scan: workgroup w owns tile columns; exclusive prefix over
+//            workgroups in place in counts, column totals -> tile_counts
+//   -- grid barrier --
+//   phase 3  tile bases (exclusive scan of tile_counts, redundantly per
+//            workgroup), LDS cursors = base[t] + counts[w][t]
+//   phase 4  scatter the chunk's (tile, primitive) pairs through the cursors.
+// No contended global atomics; two grid barriers instead of six dependent launches.
+#define ZR_STAMP(i)                                                                         \
+    do {                                                                                    \
+        if ((P.debug & kDebugStamps) && tid == 0) P.dbg_ts[w * 8 + (i)] = __builtin_amdgcn_s_memrealtime(); \
+    } while (0)
 
-__global__ __launch_bounds__(kSetupThreads) void k_bin(DrawParams P) {
-    const uint32_t prim = blockIdx.x * kSetupThreads + threadIdx.x;
-    if (prim >= P.prims || P.tri_ntiles[prim] == 0) return;
-    const uint32_t bb0 = P.records[prim].bb0, bb1 = P.records[prim].bb1;
-    const int tx0 = (int)(bb0 & 0xFFFFu) >> kTileShift, tx1 = (int)(bb1 & 0xFFFFu) >> kTileShift;
-    const int ty0 = (int)(bb0 >> 16) >> kTileShift, ty1 = (int)(bb1 >> 16) >> kTileShift;
-    for (int ty = ty0; ty <= ty1; ++ty) {
-        if ((uint32_t)ty % P.shard_count != P.shard_rank) continue;
-        const uint32_t row = ((uint32_t)ty / P.shard_count) * P.tiles_x;
-        for (int tx = tx0; tx <= tx1; ++tx) {
-            const uint32_t pos = atomicAdd(&P.tile_offsets[row + tx], 1u);
-            if (pos < P.bin_capacity) P.bins[pos] = prim;
+__global__ __launch_bounds__(kSetupThreads) void k_setup_bin(DrawParams P) {
+    extern __shared__ __attribute__((aligned(16))) uint32_t s_lds[];  // [ntiles + 1024 + 32]
+    const uint32_t nt = P.ntiles, G = gridDim.x, w = blockIdx.x, tid = threadIdx.x;
+    uint32_t* s_hist = s_lds;            // histogram, then cursors
+    uint32_t* s_part = s_lds + nt;       // phase 2 partial sums [1024]
+    uint32_t* s_misc = s_part + 1024;    // [32]
+    ZR_STAMP(0);
+    for (uint32_t t = tid; t < nt + 1024 + 32; t += kSetupThreads) s_lds[t] = 0;
+    __syncthreads();
+
+    // ---- phase 1
+    int nvalid = 0, ndropped = 0;
+    const uint32_t base = w * kSetupThreads * P.tris_per_thread;
+    constexpr uint32_t kBatch = 4;
+    for (uint32_t k = 0; k < P.tris_per_thread; k += kBatch) {
+        PrimIn in[kBatch];
+#pragma unroll
+        for (uint32_t b = 0; b < kBatch; ++b) {
+            const uint32_t kk = k + b;
+            fetch_indices(P, kk < P.tris_per_thread ? base + kk * kSetupThreads + tid : P.prims, in[b]);
+        }
+#pragma unroll
+        for (uint32_t b = 0; b < kBatch; ++b) fetch_positions(P, in[b]);
+#pragma unroll
+        for (uint32_t b = 0; b < kBatch; ++b) {
+            const uint32_t kk = k + b;
+            setup_finish(P, kk < P.tris_per_thread ? base + kk * kSetupThreads + tid : P.prims, in[b], s_hist,
+                         nvalid, ndropped);
         }
     }
+    if (nvalid) atomicAdd(&s_misc[0], (uint32_t)nvalid);
+    if (ndropped) atomicAdd(&s_misc[1], (uint32_t)ndropped);
+    __syncthreads();
+    if (P.debug & kDebugPhase1Only) return;
+    {
+        uint32_t* row = P.counts + (size_t)w * nt;
+        for (uint32_t t = tid; t < nt; t += kSetupThreads) st_sc1(&row[t], s_hist[t]);
+        if (tid == 0) {
+            if (s_misc[0]) atomicAdd(&P.counters[kCtSetup], s_misc[0]);
+            if (s_misc[1]) atomicAdd(&P.counters[kCtDropped], s_misc[1]);
+        }
+    }
+    ZR_STAMP(1);
+    grid_barrier(&P.counters[kCtBarrier], G, P.status);
+    ZR_STAMP(2);
+
+    // ---- phase 2: columns [c0, c1) of counts, in batches of up to 64 columns
+    {
+        const uint32_t cpw = (nt + G - 1) / G;
+        const uint32_t c0 = min(w * cpw, nt), c1 = min(c0 + cpw, nt);
+        for (uint32_t cb = c0; cb < c1; cb += 64) {
+            const uint32_t nc = min(64u, c1 - cb);
+            const uint32_t pl = nc <= 1 ? 0 : 32 - __clz(nc - 1);  // log2 of the padded width
+            const uint32_t cp = 1u << pl, S = 1024u >> pl;           // slices of rows
+            const uint32_t c = tid & (cp - 1), sl = tid >> pl;
+            const uint32_t R = (G + S - 1) / S;                      // rows per slice (<= 16)
+            const uint32_t r0 = min(sl * R, G), r1 = min(r0 + R, G);
+            const bool col_ok = c < nc;
+            const uint32_t cc = min(cb + c, nt - 1u);
+            uint32_t v[16];
+            uint32_t sum = 0;
+            switch (R) {  // compile-time row counts: every load unconditional (no per-load waits)
+            case 1: sum = load_rows<1>(P.counts, nt, cc, r0, r1, G, col_ok, v); break;
+            case 2: sum = load_rows<2>(P.counts, nt, cc, r0, r1, G, col_ok, v); break;
+            case 3: case 4: sum = load_rows<4>(P.counts, nt, cc, r0, r1, G, col_ok, v); break;
+            case 5: case 6: case 7: case 8: sum = load_rows<8>(P.counts, nt, cc, r0, r1, G, col_ok, v); break;
+            default: sum = load_rows<16>(P.counts, nt, cc, r0, r1, G, col_ok, v); break;
+            }
+            s_part[tid] = sum;
+            __syncthreads();
+            // exclusive scan over the S slices of each column: wave `col` scans column
+            // col, each lane owning S/64 (or 1) consecutive slices
+            {
+                const uint32_t wv = tid >> 6, ln = tid & 63;
+                const uint32_t per = (S + 63) / 64;
+                for (uint32_t col = wv; col < cp; col += kSetupThreads / 64) {
+                    const uint32_t q0 = min(ln * per, S), q1 = min(q0 + per, S);
+                    uint32_t ls = 0;
+                    for (uint32_t q = q0; q < q1; ++q) ls += s_part[q * cp + col];
+                    uint32_t inc = ls;
+#pragma unroll
+                    for (int d = 1; d < 64; d <<= 1) {
+                        const uint32_t y = __shfl_up(inc, d, 64);
+                        if ((int)ln >= d) inc += y;
+                    }
+                    uint32_t run = inc - ls;
+                    for (uint32_t q = q0; q < q1; ++q) {
+                        const uint32_t x = s_part[q * cp + col];
+                        s_part[q * cp + col] = run;
+                        run += x;
+                    }
+                    if (ln == 63 && col < nc) st_sc1(&P.tile_counts[cb + col], inc);
+                }
+            }
+            __syncthreads();
+            uint32_t run = s_part[tid];
+            for (uint32_t i = 0; i < R && col_ok; ++i) {
+                if (r0 + i < r1) st_sc1(&P.counts[(size_t)(r0 + i) * nt + cb + c], run);
+                run += v[i < 16 ? i : 15];
+            }
+            __syncthreads();
+        }
+    }
+    ZR_STAMP(3);
+    grid_barrier(&P.counters[kCtBarrier], 2 * G, P.status);
+    ZR_STAMP(4);
+    if (P.debug & kDebugStopAfterScan) return;
+
+    // ---- phase 3: tile bases and this workgroup's cursors
+    for (uint32_t t = tid; t < nt; t += kSetupThreads) s_hist[t] = ld_sc1(&P.tile_counts[t]);
+    __syncthreads();
+    const uint32_t total = block_exclusive_scan(s_hist, nt, s_misc + 8);
+    if (w == 0) {
+        for (uint32_t t = tid; t < nt; t += kSetupThreads) P.tile_offsets[t] = s_hist[t];
+        if (tid == 0) {
+            volatile uint32_t* st = P.status;
+            st[kStTotalPairs] = total;
+            if (total > P.bin_capacity) st[kStOverflow] = 1u;
+            if (total > st[kStMaxPairs]) st[kStMaxPairs] = total;
+            st[kStTrianglesSetup] = __hip_atomic_load(&P.counters[kCtSetup], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            st[kStDroppedClip] = __hip_atomic_load(&P.counters[kCtDropped], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        }
+    }
+    {
+        const uint32_t* row = P.counts + (size_t)w * nt;
+        for (uint32_t t = tid; t < nt; t += kSetupThreads) s_hist[t] += ld_sc1(&row[t]);
+    }
+    __syncthreads();
+
+    ZR_STAMP(5);
+    // ---- phase 4: scatter
+    for (uint32_t k = 0; k < P.tris_per_thread; ++k) {
+        const uint32_t prim = base + k * kSetupThreads + tid;
+        if (prim >= P.prims) continue;
+        const BBox bb = P.bboxes[prim];
+        if (bb.bb0 == kEmptyBox) continue;
+        const int tx0 = (int)(bb.bb0 & 0xFFFFu) >> kTileShift, tx1 = (int)(bb.bb1 & 0xFFFFu) >> kTileShift;
+        const int ty0 = (int)(bb.bb0 >> 16) >> kTileShift, ty1 = (int)(bb.bb1 >> 16) >> kTileShift;
+        for (int ty = ty0; ty <= ty1; ++ty) {
+            if ((uint32_t)ty % P.shard_count != P.shard_rank) continue;
+            const uint32_t r = ((uint32_t)ty / P.shard_count) * P.tiles_x;
+            const int cy0 = max((int)(bb.bb0 >> 16), ty << kTileShift);
+            const int cy1 = min((int)(bb.bb1 >> 16), (ty << kTileShift) + kTile - 1);
+            for (int tx = tx0; tx <= tx1; ++tx) {
+                const int cx0 = max((int)(bb.bb0 & 0xFFFFu), tx << kTileShift);
+                const int cx1 = min((int)(bb.bb1 & 0xFFFFu), (tx << kTileShift) + kTile - 1);
+                const uint32_t area = (uint32_t)((cx1 - cx0 + 1) * (cy1 - cy0 + 1));
+                const uint32_t bucket = min((area - 1u) >> 2, kSortBuckets - 1u);
+                const uint32_t pos = atomicAdd(&s_hist[r + tx], 1u);
+                if (pos < P.bin_capacity) P.bins[pos] = prim | (bucket << kBinPrimBits);
+            }
+        }
+    }
+    ZR_STAMP(6);
 }
 
 // ------------------------------------------------------------------- k_tile
 
 template <int PROG>
-__device__ __forceinline__ void shade_winner(const DrawParams& P, const TriRecord& r, uint32_t prim, const EdgeEval& e,
-                                             float out[4]) {
-    uint32_t vid[3];
-    prim_vids(P, prim, r.flags, vid);
+__device__ __forceinline__ void shade_winner(const DrawParams& P, const TriRecord& r, const EdgeEval& e, float out[4]) {
     if (PROG == kProgFlat) {
-        const float* c = attr_ptr(P, vid[0], 1);
+        const float* c = attr_ptr(P, r.v0, 1);  // provoking vertex = first (flat)
         out[0] = c[0]; out[1] = c[1]; out[2] = c[2]; out[3] = 1.0f;
         return;
     }
-    const float b0 = (float)e.w0 * r.invA2, b1 = (float)e.w1 * r.invA2, b2 = (float)e.w2 * r.invA2;
-    const float pw0 = b0 * r.invw0, pw1 = b1 * r.invw1, pw2 = b2 * r.invw2;
+    // perspective-correct weights b_i / w_i with w_i = 1 for every built-in vertex stage
+    const float pw0 = (float)e.w0 * r.invA2, pw1 = (float)e.w1 * r.invA2, pw2 = (float)e.w2 * r.invA2;
     const float inv = 1.0f / ((pw0 + pw1) + pw2);
-    const float* a0 = attr_ptr(P, vid[0], 1);
-    const float* a1 = attr_ptr(P, vid[1], 1);
-    const float* a2 = attr_ptr(P, vid[2], 1);
+    const float* a0 = attr_ptr(P, r.v0, 1);
+    const float* a1 = attr_ptr(P, r.v1, 1);
+    const float* a2 = attr_ptr(P, r.v2, 1);
     float f[3];
 #pragma unroll
     for (int i = 0; i < 3; ++i) f[i] = ((pw0 * a0[i] + pw1 * a1[i]) + pw2 * a2[i]) * inv;
@@ -331,9 +551,9 @@ __device__ __forceinline__ void shade_winner(const DrawParams& P, const TriRecor
         out[3] = 1.0f;
         return;
     }
-    const float* k0 = attr_ptr(P, vid[0], 2);
-    const float* k1 = attr_ptr(P, vid[1], 2);
-    const float* k2 = attr_ptr(P, vid[2], 2);
+    const float* k0 = attr_ptr(P, r.v0, 2);
+    const float* k1 = attr_ptr(P, r.v1, 2);
+    const float* k2 = attr_ptr(P, r.v2, 2);
     float kd[3];
 #pragma unroll
     for (int i = 0; i < 3; ++i) kd[i] = ((pw0 * k0[i] + pw1 * k1[i]) + pw2 * k2[i]) * inv;
@@ -371,14 +591,102 @@ __device__ __forceinline__ void store_color(const DrawParams& P, int px, int py,
     }
 }
 
+__device__ __forceinline__ int rl(int v, uint32_t lane) { return __builtin_amdgcn_readlane(v, lane); }
+
+// Rasterize one primitive (wave-uniform record) into the tile's LDS keys: lanes
+// sweep the primitive's bbox ∩ tile, packed power-of-two rows per pass.
+template <int MODE, bool INITD>
+__device__ __forceinline__ void raster_prim(const DrawParams& P, const TriRecord& r, uint32_t seq, int x0, int y0,
+                                            int lane, unsigned long long* s_key, const float* s_initd) {
+    const int bx0 = max((int)(r.bb0 & 0xFFFFu), x0), by0 = max((int)(r.bb0 >> 16), y0);
+    const int bx1 = min((int)(r.bb1 & 0xFFFFu), x0 + kTile - 1), by1 = min((int)(r.bb1 >> 16), y0 + kTile - 1);
+    const int bw = bx1 - bx0 + 1, bh = by1 - by0 + 1;
+    if (bw <= 0 || bh <= 0) return;
+    const int sh = bw <= 1 ? 0 : 32 - __clz(bw - 1);
+    const int rows = 64 >> sh;
+    const int lx = lane & ((1 << sh) - 1), lyo = lane >> sh;
+    const long long bias0 = (r.flags >> 1) & 1, bias1 = (r.flags >> 2) & 1, bias2 = (r.flags >> 3) & 1;
+    for (int ry = 0; ry < bh; ry += rows) {
+        const int ly = ry + lyo;
+        if (lx < bw && ly < bh) {
+            const int px = bx0 + lx, py = by0 + ly;
+            const EdgeEval e = eval_edges(r, px, py);
+            if (e.w0 >= bias0 && e.w1 >= bias1 && e.w2 >= bias2) {
+                const float z = interp_depth(r, e.w1, e.w2);
+                if (z >= P.dlo && z <= P.dhi) {
+                    const int li = (py - y0) * kTile + (px - x0);
+                    if (!INITD || depth_pass(P.depth_op, z, s_initd[li]))
+                        atomicMin(&s_key[li], frag_key<MODE>(z, seq));
+                }
+            }
+        }
+    }
+}
+
+// Lane-parallel path for small primitives (kFlagSmall): each lane walks its own
+// primitive's bbox ∩ tile in row order, stepping the three edge functions
+// incrementally in int32 (exact: |w| <= 2^29 inside a small primitive's bbox).
+template <int MODE, bool INITD>
+__device__ __forceinline__ void raster_lane(const DrawParams& P, const int4 q0, const int4 q1, const int4 q2,
+                                            const int4 q3, uint32_t seq, int x0, int y0,
+                                            unsigned long long* s_key, const float* s_initd) {
+    const int X0 = q0.x, Y0 = q0.y, X1 = q0.z, Y1 = q0.w, X2 = q1.x, Y2 = q1.y;
+    const float z0 = __int_as_float(q1.z), dz1 = __int_as_float(q1.w);
+    const float dz2 = __int_as_float(q2.x), invA2 = __int_as_float(q2.y);
+    const uint32_t bb0 = (uint32_t)q3.y, bb1 = (uint32_t)q3.z, flags = (uint32_t)q3.w;
+    const int bx0 = max((int)(bb0 & 0xFFFFu), x0), by0 = max((int)(bb0 >> 16), y0);
+    const int bx1 = min((int)(bb1 & 0xFFFFu), x0 + kTile - 1), by1 = min((int)(bb1 >> 16), y0 + kTile - 1);
+    const int bw = bx1 - bx0 + 1, bh = by1 - by0 + 1;
+    if (bw <= 0 || bh <= 0) return;
+    const int Sx = bx0 * 256 + 128, Sy = by0 * 256 + 128;
+    const int dx0 = X2 - X1, dy0 = Y2 - Y1, dx1 = X0 - X2, dy1 = Y0 - Y2, dx2 = X1 - X0, dy2 = Y1 - Y0;
+    int r0 = dx0 * (Sy - Y1) - dy0 * (Sx - X1);
+    int r1 = dx1 * (Sy - Y2) - dy1 * (Sx - X2);
+    int r2 = dx2 * (Sy - Y0) - dy2 * (Sx - X0);
+    const int sx0 = -dy0 * 256, sx1 = -dy1 * 256, sx2 = -dy2 * 256;  // +1 pixel in x
+    const int sy0 = dx0 * 256, sy1 = dx1 * 256, sy2 = dx2 * 256;     // +1 pixel in y
+    const int b0 = (int)((flags >> 1) & 1u), b1 = (int)((flags >> 2) & 1u), b2 = (int)((flags >> 3) & 1u);
+    const int n = bw * bh;
+    int w0 = r0, w1 = r1, w2 = r2;
+    int ex = 0, li = (by0 - y0) * kTile + (bx0 - x0);
+    for (int k = 0; k < n; ++k) {
+        if (((w0 - b0) | (w1 - b1) | (w2 - b2)) >= 0) {
+            const float fb1 = (float)w1 * invA2, fb2 = (float)w2 * invA2;
+            float z = fmaf(fb2, dz2, fmaf(fb1, dz1, z0));
+            z = z == 0.0f ? 0.0f : z;
+            if (z >= P.dlo && z <= P.dhi && (!INITD || depth_pass(P.depth_op, z, s_initd[li]))) {
+                if (P.debug & kDebugNoAtomic) {
+                    if (z == -1.0f) s_key[li] = frag_key<MODE>(z, seq);  // never true: keeps the work alive
+                } else {
+                    atomicMin(&s_key[li], frag_key<MODE>(z, seq));
+                }
+            }
+        }
+        if (++ex == bw) {
+            ex = 0;
+            r0 += sy0; r1 += sy1; r2 += sy2;
+            w0 = r0; w1 = r1; w2 = r2;
+            li += kTile - bw + 1;
+        } else {
+            w0 += sx0; w1 += sx1; w2 += sx2;
+            ++li;
+        }
+    }
+}
+
 template <int PROG, int MODE, bool INITD>
-__global__ __launch_bounds__(kTileThreads) void k_tile(DrawParams P) {
+__global__ __launch_bounds__(kTileThreads, 8) void k_tile(DrawParams P) {
     __shared__ unsigned long long s_key[kTilePixels];
     __shared__ float s_initd[INITD ? kTilePixels : 1];
+    __shared__ uint32_t s_sorted[kSortCap];
+    __shared__ uint32_t s_bucket[kSortBuckets];
     const uint32_t t = blockIdx.x;
     const uint32_t oy = t / P.tiles_x, tx = t - oy * P.tiles_x;
     const uint32_t ty = oy * P.shard_count + P.shard_rank;
     const int x0 = (int)tx * kTile, y0 = (int)ty * kTile;
+    const bool stamp = (P.debug & kDebugStamps) && threadIdx.x == 0 && t < kMaxTilesPerPass;
+    unsigned long long* ts = P.dbg_ts + 8192 * 8 + (size_t)t * 8;
+    if (stamp) ts[0] = __builtin_amdgcn_s_memrealtime();
 
     for (int i = threadIdx.x; i < kTilePixels; i += kTileThreads) {
         const int px = x0 + (i & (kTile - 1)), py = y0 + (i >> kTileShift);
@@ -389,62 +697,124 @@ __global__ __launch_bounds__(kTileThreads) void k_tile(DrawParams P) {
     }
     __syncthreads();
 
-    const uint32_t cnt = P.tile_counts[t];
-    const uint32_t begin = P.tile_offsets[t] - cnt;  // offsets hold list ends after k_bin
+    const uint32_t begin = P.tile_offsets[t];
+    // entries past bin_capacity were never written (overflowed draw, replayed by the runtime)
+    const uint32_t cnt = begin < P.bin_capacity ? min(P.tile_counts[t], P.bin_capacity - begin) : 0u;
     const uint32_t wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
     const int lane = threadIdx.x & 63;
-    for (uint32_t j = wave; j < cnt; j += kTileThreads / 64) {
-        const uint32_t slot = begin + j;
-        if (slot >= P.bin_capacity) break;  // overflowed draw: replayed by the runtime
-        const uint32_t prim = __builtin_amdgcn_readfirstlane(P.bins[slot]);
-        const TriRecord r = P.records[prim];
-        const int bx0 = max((int)(r.bb0 & 0xFFFFu), x0), by0 = max((int)(r.bb0 >> 16), y0);
-        const int bx1 = min((int)(r.bb1 & 0xFFFFu), x0 + kTile - 1), by1 = min((int)(r.bb1 >> 16), y0 + kTile - 1);
-        const int bw = bx1 - bx0 + 1, bh = by1 - by0 + 1;
-        if (bw <= 0 || bh <= 0) continue;
-        const int sh = bw <= 1 ? 0 : 32 - __clz(bw - 1);
-        const int rows = 64 >> sh;
-        const int lx = lane & ((1 << sh) - 1), lyo = lane >> sh;
-        const long long bias0 = (r.flags >> 1) & 1, bias1 = (r.flags >> 2) & 1, bias2 = (r.flags >> 3) & 1;
-        for (int ry = 0; ry < bh; ry += rows) {
-            const int ly = ry + lyo;
-            if (lx < bw && ly < bh) {
-                const int px = bx0 + lx, py = by0 + ly;
-                const EdgeEval e = eval_edges(r, px, py);
-                if (e.w0 >= bias0 && e.w1 >= bias1 && e.w2 >= bias2) {
-                    const float z = interp_depth(r, e.w1, e.w2);
-                    if (z >= P.dlo && z <= P.dhi) {
-                        const int li = (py - y0) * kTile + (px - x0);
-                        if (!INITD || depth_pass(P.depth_op, z, s_initd[li]))
-                            atomicMin(&s_key[li], frag_key<MODE>(z, prim + 1u));
-                    }
+    if (stamp) ts[1] = __builtin_amdgcn_s_memrealtime();
+    if (!(P.debug & kDebugSkipRaster)) {
+        // The list is processed in segments of kSortCap entries.  Each segment is
+        // counting-sorted in LDS by the primitive's bbox ∩ tile area (lane-path cost)
+        // so that a 64-lane chunk holds primitives of similar cost (the lane loop runs
+        // as long as its largest member).  Then each wave takes every 4th chunk: one
+        // lane per entry loads the 64-B record, and the wave walks the chunk.
+        for (uint32_t seg = 0; seg < cnt; seg += kSortCap) {
+            const uint32_t n = min(kSortCap, cnt - seg);
+            if (threadIdx.x < kSortBuckets) s_bucket[threadIdx.x] = 0u;
+            __syncthreads();
+            uint32_t pr[kSortCap / kTileThreads], bk[kSortCap / kTileThreads], sl[kSortCap / kTileThreads];
+#pragma unroll
+            for (uint32_t k = 0; k < kSortCap / kTileThreads; ++k) {
+                const uint32_t i = threadIdx.x + k * kTileThreads;
+                pr[k] = bk[k] = sl[k] = 0u;
+                if (i < n) {
+                    const uint32_t e = P.bins[begin + seg + i];  // prim | area bucket (k_setup_bin phase 4)
+                    pr[k] = e & kBinPrimMask;
+                    bk[k] = e >> kBinPrimBits;
+                    sl[k] = atomicAdd(&s_bucket[bk[k]], 1u);
                 }
             }
+            __syncthreads();
+            if (threadIdx.x < 64) {  // exclusive scan of the 64 bucket counts (one wave)
+                const uint32_t c = s_bucket[threadIdx.x];
+                uint32_t inc = c;
+#pragma unroll
+                for (int d = 1; d < 64; d <<= 1) {
+                    const uint32_t y = __shfl_up(inc, d, 64);
+                    if ((int)threadIdx.x >= d) inc += y;
+                }
+                s_bucket[threadIdx.x] = inc - c;
+            }
+            __syncthreads();
+#pragma unroll
+            for (uint32_t k = 0; k < kSortCap / kTileThreads; ++k) {
+                const uint32_t i = threadIdx.x + k * kTileThreads;
+                if (i < n) s_sorted[s_bucket[bk[k]] + sl[k]] = pr[k];
+            }
+            __syncthreads();
+            if (stamp && seg == 0) ts[2] = __builtin_amdgcn_s_memrealtime();
+            for (uint32_t cb = wave * 64u; cb < n; cb += kTileThreads) {
+                const uint32_t j = cb + (uint32_t)lane;
+                uint32_t my_prim = 0;
+                int4 q0 = make_int4(0, 0, 0, 0), q1 = q0, q2 = q0, q3 = q0;
+                if (j < n) {
+                    my_prim = s_sorted[j];
+                    const int4* rp = reinterpret_cast<const int4*>(P.records + my_prim);
+                    q0 = rp[0]; q1 = rp[1]; q2 = rp[2]; q3 = rp[3];
+                }
+                const bool valid = j < n && !(P.debug & kDebugLoadOnly);
+                if (P.debug & kDebugLoadOnly) asm volatile("" ::"v"(q0.x), "v"(q1.x), "v"(q2.x), "v"(q3.x), "v"(my_prim));
+                const bool small = valid && (((uint32_t)q3.w & kFlagSmall) != 0u);
+                if (small) raster_lane<MODE, INITD>(P, q0, q1, q2, q3, my_prim + 1u, x0, y0, s_key, s_initd);
+                // large primitives: the whole wave sweeps one primitive at a time
+                unsigned long long big = __ballot(valid && !small);
+                while (big) {
+                    const uint32_t i = (uint32_t)__builtin_ctzll(big);
+                    big &= big - 1ull;
+                    TriRecord r;
+                    r.X0 = rl(q0.x, i); r.Y0 = rl(q0.y, i); r.X1 = rl(q0.z, i); r.Y1 = rl(q0.w, i);
+                    r.X2 = rl(q1.x, i); r.Y2 = rl(q1.y, i);
+                    r.z0 = __int_as_float(rl(q1.z, i)); r.dz1 = __int_as_float(rl(q1.w, i));
+                    r.dz2 = __int_as_float(rl(q2.x, i)); r.invA2 = __int_as_float(rl(q2.y, i));
+                    r.bb0 = (uint32_t)rl(q3.y, i); r.bb1 = (uint32_t)rl(q3.z, i); r.flags = (uint32_t)rl(q3.w, i);
+                    const uint32_t prim = (uint32_t)rl((int)my_prim, i);
+                    raster_prim<MODE, INITD>(P, r, prim + 1u, x0, y0, lane, s_key, s_initd);
+                }
+            }
+            __syncthreads();
         }
     }
     __syncthreads();
+    if (stamp) ts[3] = __builtin_amdgcn_s_memrealtime();
 
-    for (int i = threadIdx.x; i < kTilePixels; i += kTileThreads) {
+    // Resolve: four pixels per thread, loads of all four issued before any store.
+    constexpr int kPer = kTilePixels / kTileThreads;
+    const uint32_t fallback = cnt ? (P.bins[begin] & kBinPrimMask) : 0u;  // any binned primitive: loads in bounds
+    float col[kPer][4];
+    float zw[kPer];
+    bool have[kPer], inside[kPer];
+#pragma unroll
+    for (int k = 0; k < kPer; ++k) {
+        const int i = threadIdx.x + k * kTileThreads;
         const int px = x0 + (i & (kTile - 1)), py = y0 + (i >> kTileShift);
-        if (px < P.ra_x0 || px > P.ra_x1 || py < P.ra_y0 || py > P.ra_y1) continue;
+        inside[k] = !(px < P.ra_x0 || px > P.ra_x1 || py < P.ra_y0 || py > P.ra_y1);
         const unsigned long long key = s_key[i];
-        const uint32_t seq = winner_seq<MODE>(key);
-        float c[4] = {0.f, 0.f, 0.f, 0.f};
-        float zw = 0.0f;
-        if (seq) {
-            const uint32_t prim = seq - 1u;
+        const uint32_t seq = inside[k] ? winner_seq<MODE>(key) : 0u;
+        have[k] = seq != 0;
+        const uint32_t prim = have[k] ? seq - 1u : fallback;
+        col[k][0] = col[k][1] = col[k][2] = col[k][3] = 0.0f;
+        zw[k] = 0.0f;
+        if (cnt) {
             const TriRecord r = P.records[prim];
             const EdgeEval e = eval_edges(r, px, py);
-            if (P.color_bpp) shade_winner<PROG>(P, r, prim, e, c);
-            zw = (MODE == kDepthLastWins) ? interp_depth(r, e.w1, e.w2) : key_depth<MODE>(key);
+            if (P.color_bpp && !(P.debug & kDebugSkipShade)) shade_winner<PROG>(P, r, e, col[k]);
+            zw[k] = (MODE == kDepthLastWins) ? interp_depth(r, e.w1, e.w2) : key_depth<MODE>(key);
         }
-        if (P.color_bpp) store_color(P, px, py, seq != 0, c);
+    }
+#pragma unroll
+    for (int k = 0; k < kPer; ++k) {
+        if (!inside[k]) continue;
+        const int i = threadIdx.x + k * kTileThreads;
+        const int px = x0 + (i & (kTile - 1)), py = y0 + (i >> kTileShift);
+        if (P.color_bpp) store_color(P, px, py, have[k], col[k]);
         if (P.depth) {
             float* dp = P.depth + (size_t)py * P.fb_w + px;
-            if (seq && P.depth_write_out) *dp = zw;
+            if (have[k] && P.depth_write_out) *dp = zw[k];
             else if (P.clear_depth_enable) *dp = P.clear_depth;
         }
     }
+    if (stamp) ts[4] = __builtin_amdgcn_s_memrealtime();
 }
 
 __global__ __launch_bounds__(kTileThreads) void k_clear(DrawParams P) {
@@ -465,19 +835,12 @@ __global__ __launch_bounds__(kTileThreads) void k_clear(DrawParams P) {
 
 static inline uint32_t blocks_for(uint32_t n, uint32_t per) { return (n + per - 1) / per; }
 
-void launch_setup(const DrawParams& p, void* stream) {
-    if (p.prims == 0) return;
-    hipLaunchKernelGGL(k_setup, dim3(blocks_for(p.prims, kSetupThreads)), dim3(kSetupThreads), 0,
-                       (hipStream_t)stream, p);
-}
+size_t setup_bin_lds_bytes(uint32_t ntiles) { return (ntiles + 1024 + 32) * sizeof(uint32_t); }
 
-void launch_scan(const DrawParams& p, void* stream) {
-    hipLaunchKernelGGL(k_scan, dim3(1), dim3(1024), 0, (hipStream_t)stream, p);
-}
+const void* setup_bin_kernel() { return reinterpret_cast<const void*>(&k_setup_bin); }
 
-void launch_bin(const DrawParams& p, void* stream) {
-    if (p.prims == 0) return;
-    hipLaunchKernelGGL(k_bin, dim3(blocks_for(p.prims, kSetupThreads)), dim3(kSetupThreads), 0,
+void launch_setup_bin(const DrawParams& p, void* stream) {
+    hipLaunchKernelGGL(k_setup_bin, dim3(p.setup_wgs), dim3(kSetupThreads), setup_bin_lds_bytes(p.ntiles),
                        (hipStream_t)stream, p);
 }
 

@@ -9,6 +9,7 @@
 
 #include <algorithm>
 #include <cstdio>
+#include <cstdlib>
 #include <cstring>
 #include <map>
 #include <string>
@@ -166,12 +167,25 @@ struct zr_device_t {
     // scratch (grow-only)
     TriRecord* records = nullptr;
     uint64_t records_cap = 0;  // primitives
-    uint32_t* tri_ntiles = nullptr;
+    BBox* bboxes = nullptr;
+    uint64_t bboxes_cap = 0;
+    uint32_t* counts = nullptr;
+    uint64_t counts_cap = 0;
+    int cu_count = 0;
+    uint32_t occupancy_checked_tiles = 0;
     uint32_t* tile_counts = nullptr;
     uint32_t* tile_offsets = nullptr;
     uint64_t tiles_cap = 0;
+    uint64_t tiles_cap2 = 0;
+    uint32_t* counters = nullptr;
+    uint64_t counters_cap = 0;
     uint32_t* bins = nullptr;
     uint64_t bins_cap = 0;
+    uint32_t debug = 0;
+    uint64_t initial_bins = 0;  // 0 = max(2^20, 2 * primitives of the first draw)
+    unsigned long long* dbg_ts = nullptr;  // kDebugStamps
+    uint32_t dbg_wgs = 0, dbg_tiles = 0;
+    std::string dbg_ts_path;
     uint32_t* status_host = nullptr;
     uint32_t* status_dev = nullptr;
     // replay + stats
@@ -249,6 +263,58 @@ zr_result grow(zr_device* d, T*& ptr, uint64_t& cap, uint64_t need, uint64_t ele
 
 zr_result execute(zr_device* d, zr_cmd* cmd);
 
+// kDebugStamps: per-phase durations of k_setup_bin across workgroups (us, 100 MHz clock).
+void dump_stamps(zr_device* d) {
+    std::vector<unsigned long long> ts(d->dbg_wgs * 8);
+    if (hipMemcpy(ts.data(), d->dbg_ts, ts.size() * 8, hipMemcpyDeviceToHost) != hipSuccess) return;
+    FILE* f = fopen(d->dbg_ts_path.c_str(), "a");
+    if (!f) return;
+    unsigned long long t0 = ~0ull;
+    for (uint32_t w = 0; w < d->dbg_wgs; ++w) t0 = std::min(t0, ts[w * 8]);
+    fprintf(f, "wgs=%u", d->dbg_wgs);
+    for (int i = 0; i <= 6; ++i) {
+        double mn = 1e30, mx = 0, sum = 0;
+        for (uint32_t w = 0; w < d->dbg_wgs; ++w) {
+            const double v = (double)(ts[w * 8 + i] - t0) * 0.01;
+            mn = std::min(mn, v); mx = std::max(mx, v); sum += v;
+        }
+        fprintf(f, " s%d[min %.1f avg %.1f max %.1f]", i, mn, sum / d->dbg_wgs, mx);
+    }
+    // phase-1 duration per workgroup, by blockIdx % 8 (a label for workgroups that share an XCD)
+    double xs[8] = {0}, xn[8] = {0};
+    fprintf(f, "\n  p1 by w%%8:");
+    for (uint32_t w = 0; w < d->dbg_wgs; ++w) {
+        xs[w % 8] += (double)(ts[w * 8 + 1] - ts[w * 8]) * 0.01;
+        xn[w % 8] += 1;
+    }
+    for (int x = 0; x < 8; ++x) fprintf(f, " %.1f", xn[x] ? xs[x] / xn[x] : 0.0);
+    {
+        std::vector<unsigned long long> tt(d->dbg_tiles * 8);
+        if (d->dbg_tiles && hipMemcpy(tt.data(), d->dbg_ts + 8192 * 8, tt.size() * 8, hipMemcpyDeviceToHost) == hipSuccess) {
+            unsigned long long t1 = ~0ull;
+            for (uint32_t w = 0; w < d->dbg_tiles; ++w) t1 = std::min(t1, tt[w * 8]);
+            fprintf(f, "\n  tile(us from first tile start; dur = per-tile phase length):");
+            for (int i = 0; i <= 4; ++i) {
+                double mn = 1e30, mx = 0, sum = 0, dsum = 0, dmx = 0;
+                for (uint32_t w = 0; w < d->dbg_tiles; ++w) {
+                    const double v = (double)(tt[w * 8 + i] - t1) * 0.01;
+                    mn = std::min(mn, v); mx = std::max(mx, v); sum += v;
+                    if (i) { const double dd = (double)(tt[w * 8 + i] - tt[w * 8 + i - 1]) * 0.01; dsum += dd; dmx = std::max(dmx, dd); }
+                }
+                fprintf(f, " t%d[min %.1f avg %.1f max %.1f dur avg %.1f max %.1f]", i, mn, sum / d->dbg_tiles, mx,
+                        dsum / d->dbg_tiles, dmx);
+            }
+        }
+    }
+    fprintf(f, "\n  p1 first 16 wgs:");
+    for (uint32_t w = 0; w < std::min(16u, d->dbg_wgs); ++w) fprintf(f, " %.1f", (double)(ts[w * 8 + 1] - ts[w * 8]) * 0.01);
+    fprintf(f, "\n  p1 last 16 wgs:");
+    for (uint32_t w = d->dbg_wgs > 16 ? d->dbg_wgs - 16 : 0; w < d->dbg_wgs; ++w)
+        fprintf(f, " %.1f", (double)(ts[w * 8 + 1] - ts[w * 8]) * 0.01);
+    fprintf(f, "\n");
+    fclose(f);
+}
+
 zr_result device_sync(zr_device* d) {
     zr_result rc = set_device(d);
     if (rc) return rc;
@@ -261,6 +327,12 @@ zr_result device_sync(zr_device* d) {
         d->last.triangles_dropped_clip = st[kStDroppedClip];
         d->last.bin_capacity = d->bins_cap;
         d->last.replays = d->replays;
+        if (st[kStBarrierTimeout]) {
+            st[kStBarrierTimeout] = 0;
+            d->pending.clear();
+            return fail(ZR_ERROR_DEVICE_LOST, "k_setup_bin grid barrier timed out (workgroups not co-resident)");
+        }
+        if (d->dbg_ts && !d->dbg_ts_path.empty()) dump_stamps(d);
         if (!st[kStOverflow]) {
             d->pending.clear();
             return ZR_SUCCESS;
@@ -364,25 +436,28 @@ zr_result fill_target(const ExecState& s, DrawParams& P) {
     return ZR_SUCCESS;
 }
 
-zr_result ensure_scratch(zr_device* d, uint64_t prims, uint64_t ntiles) {
+zr_result ensure_scratch(zr_device* d, DrawParams& P) {
     zr_result rc;
-    if (prims > d->records_cap || !d->records) {
-        uint64_t cap = d->records_cap, cap2 = d->records_cap;
-        if ((rc = grow(d, d->records, cap, prims, sizeof(TriRecord)))) return rc;
-        if ((rc = grow(d, d->tri_ntiles, cap2, prims, 4))) return rc;
-        d->records_cap = std::min(cap, cap2);
-    }
-    if (ntiles + kCtWords > d->tiles_cap || !d->tile_counts) {
-        uint64_t cap = d->tiles_cap, cap2 = d->tiles_cap;
-        if ((rc = grow(d, d->tile_counts, cap, ntiles + kCtWords, 4))) return rc;
-        if ((rc = grow(d, d->tile_offsets, cap2, ntiles + kCtWords, 4))) return rc;
-        d->tiles_cap = std::min(cap, cap2);
-    }
+    const uint64_t prims = std::max<uint64_t>(P.prims, 1);
+    if ((rc = grow(d, d->records, d->records_cap, prims, sizeof(TriRecord)))) return rc;
+    if ((rc = grow(d, d->bboxes, d->bboxes_cap, prims, sizeof(BBox)))) return rc;
+    if ((rc = grow(d, d->counts, d->counts_cap, (uint64_t)P.setup_wgs * P.ntiles + 1, 4))) return rc;
+    if ((rc = grow(d, d->tile_counts, d->tiles_cap, P.ntiles + 1, 4))) return rc;
+    if ((rc = grow(d, d->tile_offsets, d->tiles_cap2, P.ntiles + 1, 4))) return rc;
+    if ((rc = grow(d, d->counters, d->counters_cap, kCtWords, 4))) return rc;
     if (!d->bins) {
-        uint64_t cap = 0;
-        if ((rc = grow(d, d->bins, cap, std::max<uint64_t>(1u << 20, prims * 3), 4))) return rc;
-        d->bins_cap = cap;
+        const uint64_t want = d->initial_bins ? d->initial_bins : std::max<uint64_t>(1u << 20, prims * 2);
+        if ((rc = grow(d, d->bins, d->bins_cap, want, 4))) return rc;
     }
+    P.records = d->records;
+    P.bboxes = d->bboxes;
+    P.counts = d->counts;
+    P.tile_counts = d->tile_counts;
+    P.tile_offsets = d->tile_offsets;
+    P.counters = d->counters;
+    P.bins = d->bins;
+    P.bin_capacity = (uint32_t)std::min<uint64_t>(d->bins_cap, 0xFFFFFFFFull);
+    P.status = d->status_dev;
     return ZR_SUCCESS;
 }
 
@@ -408,7 +483,7 @@ zr_result exec_draw(zr_device* d, ExecState& s, const Cmd& c, bool indexed) {
     const uint64_t count = c.a, instances = c.b;
     const uint64_t tpi = count / 3u;
     const uint64_t prims = tpi * instances;
-    if (prims >= 0xFFFFFFFFull) return fail(ZR_ERROR_FEATURE_NOT_PRESENT, "more than 2^32-2 primitives in one draw");
+    if (prims > kBinPrimMask) return fail(ZR_ERROR_FEATURE_NOT_PRESENT, "more than 2^26-1 primitives in one draw");
     if (P.fb_w > 16384 || P.fb_h > 16384) return fail(ZR_ERROR_FEATURE_NOT_PRESENT, "attachment larger than 16384");
 
     const zr_buffer* vb = s.vb[0].buf;
@@ -468,22 +543,37 @@ zr_result exec_draw(zr_device* d, ExecState& s, const Cmd& c, bool indexed) {
             P.time_ptr = (const float*)((const uint8_t*)it->second.first->ptr + it->second.second);
         }
     }
-    // scratch
-    if ((rc = ensure_scratch(d, prims, P.ntiles))) return rc;
-    P.records = d->records;
-    P.tri_ntiles = d->tri_ntiles;
-    P.tile_counts = d->tile_counts;
-    P.tile_offsets = d->tile_offsets;
-    P.bins = d->bins;
-    P.bin_capacity = (uint32_t)std::min<uint64_t>(d->bins_cap, 0xFFFFFFFFull);
-    P.status = d->status_dev;
+    // binning geometry: k_setup_bin runs one kSetupThreads workgroup per CU at most
+    // (every workgroup resident: it synchronises through grid barriers)
+    if (P.ntiles > kMaxTilesPerPass)
+        return fail(ZR_ERROR_FEATURE_NOT_PRESENT, "more than 16384 owned 32x32 tiles in one pass");
+    if (d->occupancy_checked_tiles != P.ntiles) {
+        int nb = 0;
+        ZR_HIP(hipOccupancyMaxActiveBlocksPerMultiprocessor(&nb, setup_bin_kernel(), kSetupThreads,
+                                                            setup_bin_lds_bytes(P.ntiles)));
+        if (nb < 1) return fail(ZR_ERROR_FEATURE_NOT_PRESENT, "k_setup_bin cannot be resident on a CU");
+        d->occupancy_checked_tiles = P.ntiles;
+    }
+    {
+        const uint64_t cus = (uint64_t)std::max(d->cu_count, 1);
+        const uint64_t per_wave = (uint64_t)kSetupThreads * cus;
+        P.tris_per_thread = (uint32_t)std::max<uint64_t>(1, (prims + per_wave - 1) / per_wave);
+        const uint64_t chunk = (uint64_t)kSetupThreads * P.tris_per_thread;
+        P.setup_wgs = (uint32_t)std::max<uint64_t>(1, (prims + chunk - 1) / chunk);
+    }
+    P.debug = d->debug;
+    if (d->debug & kDebugStamps) {
+        if (!d->dbg_ts) ZR_HIP(hipMalloc((void**)&d->dbg_ts, (8192 + kMaxTilesPerPass) * 8 * sizeof(unsigned long long)));
+        P.dbg_ts = d->dbg_ts;
+        d->dbg_wgs = P.setup_wgs;
+        d->dbg_tiles = P.ntiles;
+    }
+    if ((rc = ensure_scratch(d, P))) return rc;
     d->last_prims = prims;
     d->last.triangles_in = prims;
 
-    ZR_HIP(hipMemsetAsync(P.tile_counts, 0, (P.ntiles + kCtWords) * 4, d->stream));
-    timed_launch(d, "setup", [&] { launch_setup(P, d->stream); });
-    timed_launch(d, "scan", [&] { launch_scan(P, d->stream); });
-    timed_launch(d, "bin", [&] { launch_bin(P, d->stream); });
+    ZR_HIP(hipMemsetAsync(P.counters, 0, kCtWords * 4, d->stream));
+    timed_launch(d, "setup_bin", [&] { launch_setup_bin(P, d->stream); });
     timed_launch(d, "tile", [&] { launch_tile(P, d->stream); });
     ZR_HIP(hipGetLastError());
     s.color_clear_pending = false;
@@ -563,8 +653,12 @@ ZR_API zr_result zr_device_create(int32_t hip_device, zr_device** out) {
     zr_device* d = new (std::nothrow) zr_device_t();
     if (!d) return fail(ZR_ERROR_OUT_OF_HOST_MEMORY, "device alloc");
     d->hip_device = hip_device;
+    if (const char* dbg = getenv("ZR_DEBUG")) d->debug = (uint32_t)strtoul(dbg, nullptr, 0);
+    if (const char* p = getenv("ZR_DEBUG_TS")) d->dbg_ts_path = p;
+    if (const char* cap = getenv("ZR_BIN_CAPACITY")) d->initial_bins = std::max<uint64_t>(64, strtoull(cap, nullptr, 0));
     ZR_HIP(hipSetDevice(hip_device));
     ZR_HIP(hipStreamCreateWithFlags(&d->stream, hipStreamNonBlocking));
+    ZR_HIP(hipDeviceGetAttribute(&d->cu_count, hipDeviceAttributeMultiprocessorCount, hip_device));
     void* st = nullptr;
     ZR_HIP(hipHostMalloc(&st, kStWords * 4, hipHostMallocMapped));
     memset(st, 0, kStWords * 4);
@@ -582,11 +676,9 @@ ZR_API void zr_device_destroy(zr_device* d) {
     (void)hipStreamSynchronize(d->stream);
     collect_timings(d);
     for (hipEvent_t e : d->event_pool) (void)hipEventDestroy(e);
-    (void)hipFree(d->records);
-    (void)hipFree(d->tri_ntiles);
-    (void)hipFree(d->tile_counts);
-    (void)hipFree(d->tile_offsets);
-    (void)hipFree(d->bins);
+    for (void* p : {(void*)d->dbg_ts, (void*)d->records, (void*)d->bboxes, (void*)d->counts,
+                    (void*)d->tile_counts, (void*)d->tile_offsets, (void*)d->counters, (void*)d->bins})
+        if (p) (void)hipFree(p);
     (void)hipHostFree(d->status_host);
     (void)hipStreamDestroy(d->stream);
     delete d;

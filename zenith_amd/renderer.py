@@ -154,9 +154,9 @@ class SceneRenderer:
             enc.bind_vertex_buffers(0, [self.vertex_buffer], [0])
             if self.index_buffer is not None:
                 enc.bind_index_buffer(self.index_buffer, 0, s.index_type)
-                enc.draw_indexed(s.draw_count, 1, 0, 0, 0)
+                enc.draw_indexed(s.draw_count, s.instance_count, s.first, s.vertex_offset, 0)
             else:
-                enc.draw(s.draw_count, 1, 0, 0)
+                enc.draw(s.draw_count, s.instance_count, s.first, 0)
             ctx.end_rendering()
 
         rhi.execute_graphic_node(self.device, self.encoder, self.pipeline, [color], depth, job)

@@ -61,6 +61,10 @@ class Scene:
     depth_clear: float = 1.0
     time: float = 0.0                                # Time.time, pinned for goldens
     write_mask: int = 0xF
+    instance_count: int = 1                          # draw_indexed(count, instances, first, offset, 0)
+    first: int = 0                                   # first_index / first_vertex
+    vertex_offset: int = 0
+    count: int | None = None                         # default: all indices / vertices
 
     @property
     def stride(self) -> int:
@@ -74,11 +78,13 @@ class Scene:
 
     @property
     def draw_count(self) -> int:
+        if self.count is not None:
+            return int(self.count)
         return int(self.indices.size if self.indices is not None else self.vertices.shape[0])
 
     @property
     def triangles(self) -> int:
-        return self.draw_count // 3
+        return (self.draw_count // 3) * self.instance_count
 
     def vertex_bytes(self) -> bytes:
         return np.ascontiguousarray(self.vertices, dtype=np.float32).tobytes()
