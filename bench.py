@@ -38,34 +38,39 @@ def parse():
     p.add_argument("--steps", type=int, default=100)
     p.add_argument("--warmup", type=int, default=10)
     p.add_argument("--config", default="c2", choices=sorted(scenes.CONFIGS))
-    p.add_argument("--cpu-frames", type=int, default=5)
+    p.add_argument("--cpu-seconds", type=float, default=10.0, help="CPU baseline sample length")
     p.add_argument("--no-cpu-baseline", action="store_true")
-    p.add_argument("--pmc", default=os.path.join(ROOT, "profiles", "r01_pmc_tile.json"),
+    p.add_argument("--pmc", default=os.path.join(ROOT, "profiles", "r01_pmc_c2.json"),
                    help="rocprofv3 PMC summary for roofline.traffic (tools/pmc_summary.py)")
     return p.parse_args()
 
 
 def algorithmic_bytes(kernel, n_tris, b_in, pairs, pixels):
-    """Per-launch algorithmic bytes of each pass (SURVEY.md §8d per-pass accounting)."""
-    if kernel == "setup":
-        return n_tris * b_in + n_tris * RECORD_BYTES
-    if kernel == "bin":
-        return pairs * BIN_ENTRY_BYTES + n_tris * RECORD_BYTES
+    """Per-launch algorithmic bytes of each pass.
+
+    setup_bin: read index+vertex data once (b_in per triangle), write one 64-B
+               record per triangle and one 4-B bin entry per (tile, triangle) pair.
+    tile:      read each pair's bin entry + record once, write the colour + depth
+               texel of every owned pixel (4 + 4 B).
+    """
+    if kernel == "setup_bin":
+        return n_tris * (b_in + RECORD_BYTES) + pairs * BIN_ENTRY_BYTES
     if kernel == "tile":
         return pairs * (BIN_ENTRY_BYTES + RECORD_BYTES) + pixels * 8
-    if kernel == "scan":
-        return 0
     return 0
 
 
-def cpu_baseline(scene, frames):
-    """The CPU oracle (oracle/, OpenMP over tile-row bands) on the same scene."""
+def cpu_baseline(scene, seconds, max_frames=500):
+    """The CPU oracle (oracle/, OpenMP over tile-row bands) on the same scene:
+    1 warm-up frame, then whole frames until ``seconds`` of wall time have passed."""
     from oracle import oracle
     threads = min(16, os.cpu_count() or 1)
     oracle.render(scene, nthreads=threads)  # warm-up
+    frames = 0
     t0 = time.perf_counter()
-    for _ in range(frames):
+    while frames < max_frames and (frames < 3 or time.perf_counter() - t0 < seconds):
         oracle.render(scene, nthreads=threads)
+        frames += 1
     dt = time.perf_counter() - t0
     return {"value": round(scene.triangles * frames / dt / 1e6, 3), "unit": "Mtri/s", "cores": threads,
             "kind": "port",
@@ -143,8 +148,8 @@ def main():
     if os.path.exists(a.pmc):
         with open(a.pmc) as fh:
             pmc = json.load(fh)
-        if pmc.get("kernel") == dom and pmc.get("config") == a.config:
-            traffic = pmc.get("hbm_bytes_per_launch")
+        if pmc.get("config") == a.config and dom in pmc.get("kernels", {}):
+            traffic = pmc["kernels"][dom]["hbm_bytes_per_launch"]
     achieved = dk.get("gbps") or 0.0
 
     ms_per_step = elapsed / a.steps * 1e3
@@ -171,7 +176,7 @@ def main():
         "triangles_setup": stats["triangles_setup"],
     }
     if rank == 0 and world == 1 and not a.no_cpu_baseline:
-        out["cpu_baseline"] = cpu_baseline(scene, a.cpu_frames)
+        out["cpu_baseline"] = cpu_baseline(scene, a.cpu_seconds)
     elif rank == 0:
         out["cpu_baseline"] = None
     if rank == 0:

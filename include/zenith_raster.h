@@ -102,12 +102,12 @@ typedef struct zr_fence_t zr_fence;
 ZR_API zr_result zr_device_create(int32_t hip_device, zr_device **out);
 ZR_API void zr_device_destroy(zr_device *dev);
 /* RenderDevice::wait_idle analogue; also the point where a bin-capacity overflow
- * is detected and the pending submissions are replayed (DESIGN.md §4.5). */
+ * is detected and the pending submissions are replayed (DESIGN.md §4). */
 ZR_API zr_result zr_device_wait_idle(zr_device *dev);
 /* Per-kernel HIP-event timing of every draw (off by default). */
 ZR_API zr_result zr_device_set_profiling(zr_device *dev, int32_t enable);
-/* Accumulated timings since the last reset: for each kernel name (setup, scan,
- * bin, tile, clear, ...) total ms and launch count.  Returns the number of
+/* Accumulated timings since the last reset: for each kernel name (setup_bin,
+ * tile, clear) total ms and launch count.  Returns the number of
  * entries written (<= capacity). */
 typedef struct zr_kernel_time {
     char name[32];

@@ -71,7 +71,9 @@ enum StatusWord : uint32_t {
     kStWords = 16,
 };
 // Device-side counters (zeroed with the tile counts before each draw).
-enum CounterWord : uint32_t { kCtSetup = 0, kCtDropped = 1, kCtBarrier = 2, kCtWords = 4 };
+// Device counters of k_setup_bin.  Zero between draws: the last workgroup to
+// finish (kCtExit) resets them, so a draw needs no memset launch.
+enum CounterWord : uint32_t { kCtSetup = 0, kCtDropped = 1, kCtBarrier = 2, kCtExit = 3, kCtWords = 4 };
 
 struct DrawParams {
     // vertex input (binding 0) and index buffer

@@ -523,6 +523,17 @@ __global__ __launch_bounds__(kSetupThreads) void k_setup_bin(DrawParams P) {
         }
     }
     ZR_STAMP(6);
+    // Every workgroup has left both barriers once it counts itself out here, so the
+    // last one can return the counters to zero for the next draw.
+    if (tid == 0) {
+        const uint32_t prev = __hip_atomic_fetch_add(&P.counters[kCtExit], 1u, __ATOMIC_RELAXED,
+                                                     __HIP_MEMORY_SCOPE_AGENT);
+        if (prev == G - 1u) {
+#pragma unroll
+            for (uint32_t i = 0; i < kCtWords; ++i)
+                __hip_atomic_store(&P.counters[i], 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        }
+    }
 }
 
 // ------------------------------------------------------------------- k_tile
@@ -560,13 +571,15 @@ __device__ __forceinline__ void shade_winner(const DrawParams& P, const TriRecor
     shade_blinn_phong(f[0], f[1], f[2], kd[0], kd[1], kd[2], out);
 }
 
-__device__ __forceinline__ void store_color(const DrawParams& P, int px, int py, bool have, const float c[4]) {
+// T: the sRGB threshold table (LDS copy in k_tile).
+__device__ __forceinline__ void store_color(const DrawParams& P, int px, int py, bool have, const float c[4],
+                                            const float* T) {
     const size_t idx = (size_t)py * P.fb_w + (size_t)px;
     if (P.color_bpp == 4) {
         uint32_t* cp = (uint32_t*)P.color + idx;
         const uint32_t m = rgba8_write_mask(P.write_mask, P.color_format);
         if (have) {
-            const uint32_t texel = pack_rgba8(c, P.color_format, c_srgbT);
+            const uint32_t texel = pack_rgba8_fast(c, P.color_format, T);
             if (m == 0xFFFFFFFFu) {
                 *cp = texel;
             } else {
@@ -680,6 +693,7 @@ __global__ __launch_bounds__(kTileThreads, 8) void k_tile(DrawParams P) {
     __shared__ float s_initd[INITD ? kTilePixels : 1];
     __shared__ uint32_t s_sorted[kSortCap];
     __shared__ uint32_t s_bucket[kSortBuckets];
+    __shared__ float s_srgb[256];
     const uint32_t t = blockIdx.x;
     const uint32_t oy = t / P.tiles_x, tx = t - oy * P.tiles_x;
     const uint32_t ty = oy * P.shard_count + P.shard_rank;
@@ -695,6 +709,7 @@ __global__ __launch_bounds__(kTileThreads, 8) void k_tile(DrawParams P) {
         s_key[i] = init_key<MODE>(d);
         if (INITD) s_initd[i] = d;
     }
+    if (threadIdx.x < 255) s_srgb[threadIdx.x] = c_srgbT[threadIdx.x];
     __syncthreads();
 
     const uint32_t begin = P.tile_offsets[t];
@@ -807,7 +822,7 @@ __global__ __launch_bounds__(kTileThreads, 8) void k_tile(DrawParams P) {
         if (!inside[k]) continue;
         const int i = threadIdx.x + k * kTileThreads;
         const int px = x0 + (i & (kTile - 1)), py = y0 + (i >> kTileShift);
-        if (P.color_bpp) store_color(P, px, py, have[k], col[k]);
+        if (P.color_bpp) store_color(P, px, py, have[k], col[k], s_srgb);
         if (P.depth) {
             float* dp = P.depth + (size_t)py * P.fb_w + px;
             if (have[k] && P.depth_write_out) *dp = zw[k];
@@ -826,7 +841,7 @@ __global__ __launch_bounds__(kTileThreads) void k_clear(DrawParams P) {
     for (int i = threadIdx.x; i < kTilePixels; i += kTileThreads) {
         const int px = x0 + (i & (kTile - 1)), py = y0 + (i >> kTileShift);
         if (px < P.ra_x0 || px > P.ra_x1 || py < P.ra_y0 || py > P.ra_y1) continue;
-        if (P.color_bpp && P.clear_color_enable) store_color(P, px, py, false, c);
+        if (P.color_bpp && P.clear_color_enable) store_color(P, px, py, false, c, c_srgbT);
         if (P.depth && P.clear_depth_enable) P.depth[(size_t)py * P.fb_w + px] = P.clear_depth;
     }
 }

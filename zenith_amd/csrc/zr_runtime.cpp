@@ -444,7 +444,10 @@ zr_result ensure_scratch(zr_device* d, DrawParams& P) {
     if ((rc = grow(d, d->counts, d->counts_cap, (uint64_t)P.setup_wgs * P.ntiles + 1, 4))) return rc;
     if ((rc = grow(d, d->tile_counts, d->tiles_cap, P.ntiles + 1, 4))) return rc;
     if ((rc = grow(d, d->tile_offsets, d->tiles_cap2, P.ntiles + 1, 4))) return rc;
-    if ((rc = grow(d, d->counters, d->counters_cap, kCtWords, 4))) return rc;
+    if (!d->counters) {  // zeroed once; k_setup_bin leaves them zero after every draw
+        if ((rc = grow(d, d->counters, d->counters_cap, kCtWords, 4))) return rc;
+        ZR_HIP(hipMemset(d->counters, 0, d->counters_cap * 4));
+    }
     if (!d->bins) {
         const uint64_t want = d->initial_bins ? d->initial_bins : std::max<uint64_t>(1u << 20, prims * 2);
         if ((rc = grow(d, d->bins, d->bins_cap, want, 4))) return rc;
@@ -572,7 +575,8 @@ zr_result exec_draw(zr_device* d, ExecState& s, const Cmd& c, bool indexed) {
     d->last_prims = prims;
     d->last.triangles_in = prims;
 
-    ZR_HIP(hipMemsetAsync(P.counters, 0, kCtWords * 4, d->stream));
+    // debug early exits skip the self-reset at the end of k_setup_bin
+    if (d->debug) ZR_HIP(hipMemsetAsync(P.counters, 0, kCtWords * 4, d->stream));
     timed_launch(d, "setup_bin", [&] { launch_setup_bin(P, d->stream); });
     timed_launch(d, "tile", [&] { launch_tile(P, d->stream); });
     ZR_HIP(hipGetLastError());

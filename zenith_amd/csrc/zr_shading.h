@@ -89,6 +89,36 @@ ZR_HD uint32_t pack_rgba8(const float c[4], int32_t fmt, const float* T) {
     return format_is_bgra(fmt) ? (b | (g << 8) | (r << 16) | (a << 24)) : (r | (g << 8) | (b << 16) | (a << 24));
 }
 
+#if defined(__HIPCC__)
+// Device fast path with the same result as encode_srgb8: estimate the code with
+// the hardware log2/exp2, then move it onto the threshold table (T in LDS) until
+// T[k-1] <= c < T[k].  The estimate is within one code of the exact result; two
+// fix-up rounds make the result exact by construction (the table defines it).
+__device__ __forceinline__ uint32_t encode_srgb8_fast(float c, const float* T) {
+    c = clamp01(c);
+    const float e = c <= 0.0031308f ? c * 12.92f : fmaf(1.055f, __builtin_amdgcn_exp2f(__builtin_amdgcn_logf(c) * (1.0f / 2.4f)), -0.055f);
+    int k = (int)fmaf(e, 255.0f, 0.5f);
+    k = k < 0 ? 0 : (k > 255 ? 255 : k);
+#pragma unroll
+    for (int it = 0; it < 2; ++it) {
+        const float lo = k > 0 ? T[k - 1] : -1.0f;
+        const float hi = k < 255 ? T[k] : 2.0f;
+        k += (c >= hi) ? 1 : 0;
+        k -= (c < lo) ? 1 : 0;
+    }
+    return (uint32_t)k;
+}
+
+__device__ __forceinline__ uint32_t pack_rgba8_fast(const float c[4], int32_t fmt, const float* T) {
+    const bool srgb = format_is_srgb(fmt);
+    const uint32_t r = srgb ? encode_srgb8_fast(c[0], T) : encode_unorm8(c[0]);
+    const uint32_t g = srgb ? encode_srgb8_fast(c[1], T) : encode_unorm8(c[1]);
+    const uint32_t b = srgb ? encode_srgb8_fast(c[2], T) : encode_unorm8(c[2]);
+    const uint32_t a = encode_unorm8(c[3]);
+    return format_is_bgra(fmt) ? (b | (g << 8) | (r << 16) | (a << 24)) : (r | (g << 8) | (b << 16) | (a << 24));
+}
+#endif
+
 // Byte mask of the 32-bit texel selected by a VkColorComponentFlags write mask.
 ZR_HD uint32_t rgba8_write_mask(uint32_t mask, int32_t fmt) {
     const uint32_t rpos = format_is_bgra(fmt) ? 16u : 0u, bpos = format_is_bgra(fmt) ? 0u : 16u;
