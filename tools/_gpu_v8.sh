@@ -1,0 +1,11 @@
+# atomic tile reservation (one grid barrier): full parity, schedules x batch, stamps
+set -o pipefail
+export TMPDIR=/tmp
+O=gpurun_out/v8
+mkdir -p $O
+timeout -k 10 700 python -m pytest tests -m gpu -x -q > $O/pytest.log 2>&1 || exit 1
+for sc in 0 1; do for b in 1 2 4; do
+  ZR_SETUP_SCHED=$sc ZR_SETUP_BATCH=$b timeout -k 10 200 python bench.py --no-cpu-baseline > $O/bench_s${sc}_b$b.json 2>> $O/bench.err || exit 2
+done; done
+ZR_DEBUG=128 ZR_DEBUG_TS=$O/stamps.txt timeout -k 10 200 python bench.py --steps 3 --warmup 1 --no-cpu-baseline > /dev/null 2>> $O/bench.err || exit 4
+echo done

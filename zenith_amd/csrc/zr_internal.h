@@ -121,14 +121,16 @@ struct DrawParams {
     // scratch (binning without contended global atomics)
     TriRecord* records;       // [prims]
     BBox* bboxes;             // [prims]; bb0 == kEmptyBox when culled / no owned tile
-    uint32_t* counts;         // M[setup_wgs][ntiles]: per-workgroup tile histograms, then offsets
     uint32_t* tile_counts;    // [ntiles]
     uint32_t* tile_offsets;   // [ntiles] exclusive scan (list starts)
     uint32_t* counters;       // [kCtWords]
     uint32_t* bins;           // [bin_capacity] primitive ids grouped by tile
     uint32_t bin_capacity;
     uint32_t setup_wgs;       // workgroups of k_setup_bin (<= CUs: all resident)
-    uint32_t tris_per_thread; // primitives per setup thread (chunk = kSetupThreads * this)
+    uint32_t unit_shift;      // log2 primitives per claim unit (64 lanes * batch * rounds)
+    uint32_t units;           // claim units of the draw: ceil(prims / unit size)
+    uint32_t setup_batch;     // primitives per lane in flight (template instance of k_setup_bin)
+    uint32_t setup_sched;     // unit schedule: 0 contiguous per workgroup, 1 interleaved (u % G)
     uint32_t debug;           // kDebug* bits (timing experiments only)
     unsigned long long* dbg_ts; // [setup_wgs][8] s_memrealtime stamps (kDebugStamps only)
     uint32_t* status;         // host-mapped
@@ -137,7 +139,7 @@ struct DrawParams {
 // Launchers (zr_kernels.hip).  All enqueue on `stream`; no host synchronisation.
 void launch_setup_bin(const DrawParams& p, void* stream);  // persistent: setup + scan + scatter
 size_t setup_bin_lds_bytes(uint32_t ntiles);
-const void* setup_bin_kernel();
+const void* setup_bin_kernel(uint32_t batch);
 void launch_tile(const DrawParams& p, void* stream);
 void launch_clear(const DrawParams& p, void* stream);
 

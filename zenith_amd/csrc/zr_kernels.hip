@@ -296,22 +296,6 @@ __device__ __forceinline__ uint32_t ld_sc1(const uint32_t* p) {
     return __hip_atomic_load(const_cast<uint32_t*>(p), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
 }
 
-template <int R>
-__device__ __forceinline__ uint32_t load_rows(const uint32_t* counts, uint32_t nt, uint32_t cc, uint32_t r0, uint32_t r1,
-                                              uint32_t G, bool col_ok, uint32_t (&v)[16]) {
-    uint32_t sum = 0;
-#pragma unroll
-    for (int i = 0; i < R; ++i) v[i] = ld_sc1(&counts[(size_t)min(r0 + (uint32_t)i, G - 1u) * nt + cc]);
-#pragma unroll
-    for (int i = 0; i < R; ++i) {
-        v[i] = (col_ok && r0 + (uint32_t)i < r1) ? v[i] : 0u;
-        sum += v[i];
-    }
-#pragma unroll
-    for (int i = R; i < 16; ++i) v[i] = 0u;
-    return sum;
-}
-
 // Exclusive scan of a[0..n) in LDS by a 1024-thread workgroup; returns the total.
 __device__ __forceinline__ uint32_t block_exclusive_scan(uint32_t* a, uint32_t n, uint32_t* s_wave) {
     const uint32_t tid = threadIdx.x;
@@ -353,137 +337,96 @@ __device__ __forceinline__ uint32_t block_exclusive_scan(uint32_t* a, uint32_t n
 
 // ----------------------------------------------------------- k_setup_bin
 //
-// One persistent launch, one 1024-thread workgroup per CU, chunk w of the draw's
-// primitives per workgroup:
-//   phase 1  setup + records, per-workgroup LDS tile histogram -> counts[w][*]
+// One persistent launch, one 1024-thread workgroup per CU (fewer for small draws):
+//   phase 1  vertex stage + setup in units of 64 * KB * rounds primitives, one
+//            wave per unit (units assigned statically, P.setup_sched); records and
+//            tile bboxes to HBM, pairs counted in an LDS histogram of all tiles
+//   phase 2  the histogram is added into the global per-tile counters with
+//            returning atomics (a wave's adds to consecutive tiles leave L2 as
+//            64-B requests); the value returned is this workgroup's offset inside
+//            each tile's list.  Order inside a tile's list is therefore arbitrary,
+//            which is free: visibility keys carry the primitive sequence (k_tile).
 //   -- grid barrier --
-//   phase 2  column scan: workgroup w owns tile columns; exclusive prefix over
-//            workgroups in place in counts, column totals -> tile_counts
-//   -- grid barrier --
-//   phase 3  tile bases (exclusive scan of tile_counts, redundantly per
-//            workgroup), LDS cursors = base[t] + counts[w][t]
-//   phase 4  scatter the chunk's (tile, primitive) pairs through the cursors.
-// No contended global atomics; two grid barriers instead of six dependent launches.
+//   phase 3  tile bases (exclusive scan of the totals, redundantly per workgroup);
+//            LDS cursors = base[t] + own offset[t]
+//   phase 4  scatter the workgroup's (tile, primitive) pairs through the cursors.
+// The last workgroup to finish returns the tile counters and the grid counters to
+// zero, so a draw needs no memset.
 #define ZR_STAMP(i)                                                                         \
     do {                                                                                    \
         if ((P.debug & kDebugStamps) && tid == 0) P.dbg_ts[w * 8 + (i)] = __builtin_amdgcn_s_memrealtime(); \
     } while (0)
 
+// i-th unit of primitives owned by workgroup w (static schedules).
+__device__ __forceinline__ uint32_t own_unit(const DrawParams& P, uint32_t w, uint32_t G, uint32_t i) {
+    if (P.setup_sched == 0) {
+        const uint32_t upw = (P.units + G - 1u) / G;
+        return i < upw ? w * upw + i : P.units;
+    }
+    return w + i * G;
+}
+
+template <uint32_t KB>
 __global__ __launch_bounds__(kSetupThreads) void k_setup_bin(DrawParams P) {
-    extern __shared__ __attribute__((aligned(16))) uint32_t s_lds[];  // [ntiles + 1024 + 32]
+    extern __shared__ __attribute__((aligned(16))) uint32_t s_lds[];  // [2 * ntiles + 32]
     const uint32_t nt = P.ntiles, G = gridDim.x, w = blockIdx.x, tid = threadIdx.x;
-    uint32_t* s_hist = s_lds;            // histogram, then cursors
-    uint32_t* s_part = s_lds + nt;       // phase 2 partial sums [1024]
-    uint32_t* s_misc = s_part + 1024;    // [32]
+    uint32_t* s_hist = s_lds;            // histogram -> own offsets -> cursors
+    uint32_t* s_base = s_lds + nt;       // tile totals -> tile bases
+    uint32_t* s_misc = s_base + nt;      // [32]
     ZR_STAMP(0);
-    for (uint32_t t = tid; t < nt + 1024 + 32; t += kSetupThreads) s_lds[t] = 0;
+    for (uint32_t t = tid; t < nt; t += kSetupThreads) s_hist[t] = 0;
+    if (tid < 32) s_misc[tid] = 0;
     __syncthreads();
 
     // ---- phase 1
     int nvalid = 0, ndropped = 0;
-    const uint32_t base = w * kSetupThreads * P.tris_per_thread;
-    constexpr uint32_t kBatch = 4;
-    for (uint32_t k = 0; k < P.tris_per_thread; k += kBatch) {
-        PrimIn in[kBatch];
+    {
+        const uint32_t lane = tid & 63u, wave = tid >> 6;
+        const uint32_t rounds = (1u << P.unit_shift) / (64u * KB);
+        for (uint32_t i = 0;; ++i) {
+            const uint32_t u = own_unit(P, w, G, wave + i * (kSetupThreads / 64u));
+            if (u >= P.units) break;
+            for (uint32_t r = 0; r < rounds; ++r) {
+                const uint32_t pb = (u << P.unit_shift) + r * 64u * KB + lane;
+                PrimIn in[KB];
 #pragma unroll
-        for (uint32_t b = 0; b < kBatch; ++b) {
-            const uint32_t kk = k + b;
-            fetch_indices(P, kk < P.tris_per_thread ? base + kk * kSetupThreads + tid : P.prims, in[b]);
-        }
+                for (uint32_t b = 0; b < KB; ++b) fetch_indices(P, min(pb + b * 64u, P.prims), in[b]);
 #pragma unroll
-        for (uint32_t b = 0; b < kBatch; ++b) fetch_positions(P, in[b]);
+                for (uint32_t b = 0; b < KB; ++b) fetch_positions(P, in[b]);
 #pragma unroll
-        for (uint32_t b = 0; b < kBatch; ++b) {
-            const uint32_t kk = k + b;
-            setup_finish(P, kk < P.tris_per_thread ? base + kk * kSetupThreads + tid : P.prims, in[b], s_hist,
-                         nvalid, ndropped);
+                for (uint32_t b = 0; b < KB; ++b)
+                    setup_finish(P, min(pb + b * 64u, P.prims), in[b], s_hist, nvalid, ndropped);
+            }
         }
     }
     if (nvalid) atomicAdd(&s_misc[0], (uint32_t)nvalid);
     if (ndropped) atomicAdd(&s_misc[1], (uint32_t)ndropped);
     __syncthreads();
-    if (P.debug & kDebugPhase1Only) return;
-    {
-        uint32_t* row = P.counts + (size_t)w * nt;
-        for (uint32_t t = tid; t < nt; t += kSetupThreads) st_sc1(&row[t], s_hist[t]);
-        if (tid == 0) {
-            if (s_misc[0]) atomicAdd(&P.counters[kCtSetup], s_misc[0]);
-            if (s_misc[1]) atomicAdd(&P.counters[kCtDropped], s_misc[1]);
-        }
-    }
     ZR_STAMP(1);
-    grid_barrier(&P.counters[kCtBarrier], G, P.status);
-    ZR_STAMP(2);
+    if (P.debug & kDebugPhase1Only) return;
 
-    // ---- phase 2: columns [c0, c1) of counts, in batches of up to 64 columns
-    {
-        const uint32_t cpw = (nt + G - 1) / G;
-        const uint32_t c0 = min(w * cpw, nt), c1 = min(c0 + cpw, nt);
-        for (uint32_t cb = c0; cb < c1; cb += 64) {
-            const uint32_t nc = min(64u, c1 - cb);
-            const uint32_t pl = nc <= 1 ? 0 : 32 - __clz(nc - 1);  // log2 of the padded width
-            const uint32_t cp = 1u << pl, S = 1024u >> pl;           // slices of rows
-            const uint32_t c = tid & (cp - 1), sl = tid >> pl;
-            const uint32_t R = (G + S - 1) / S;                      // rows per slice (<= 16)
-            const uint32_t r0 = min(sl * R, G), r1 = min(r0 + R, G);
-            const bool col_ok = c < nc;
-            const uint32_t cc = min(cb + c, nt - 1u);
-            uint32_t v[16];
-            uint32_t sum = 0;
-            switch (R) {  // compile-time row counts: every load unconditional (no per-load waits)
-            case 1: sum = load_rows<1>(P.counts, nt, cc, r0, r1, G, col_ok, v); break;
-            case 2: sum = load_rows<2>(P.counts, nt, cc, r0, r1, G, col_ok, v); break;
-            case 3: case 4: sum = load_rows<4>(P.counts, nt, cc, r0, r1, G, col_ok, v); break;
-            case 5: case 6: case 7: case 8: sum = load_rows<8>(P.counts, nt, cc, r0, r1, G, col_ok, v); break;
-            default: sum = load_rows<16>(P.counts, nt, cc, r0, r1, G, col_ok, v); break;
-            }
-            s_part[tid] = sum;
-            __syncthreads();
-            // exclusive scan over the S slices of each column: wave `col` scans column
-            // col, each lane owning S/64 (or 1) consecutive slices
-            {
-                const uint32_t wv = tid >> 6, ln = tid & 63;
-                const uint32_t per = (S + 63) / 64;
-                for (uint32_t col = wv; col < cp; col += kSetupThreads / 64) {
-                    const uint32_t q0 = min(ln * per, S), q1 = min(q0 + per, S);
-                    uint32_t ls = 0;
-                    for (uint32_t q = q0; q < q1; ++q) ls += s_part[q * cp + col];
-                    uint32_t inc = ls;
-#pragma unroll
-                    for (int d = 1; d < 64; d <<= 1) {
-                        const uint32_t y = __shfl_up(inc, d, 64);
-                        if ((int)ln >= d) inc += y;
-                    }
-                    uint32_t run = inc - ls;
-                    for (uint32_t q = q0; q < q1; ++q) {
-                        const uint32_t x = s_part[q * cp + col];
-                        s_part[q * cp + col] = run;
-                        run += x;
-                    }
-                    if (ln == 63 && col < nc) st_sc1(&P.tile_counts[cb + col], inc);
-                }
-            }
-            __syncthreads();
-            uint32_t run = s_part[tid];
-            for (uint32_t i = 0; i < R && col_ok; ++i) {
-                if (r0 + i < r1) st_sc1(&P.counts[(size_t)(r0 + i) * nt + cb + c], run);
-                run += v[i < 16 ? i : 15];
-            }
-            __syncthreads();
-        }
+    // ---- phase 2: reserve this workgroup's slots in every tile's list
+    for (uint32_t t = tid; t < nt; t += kSetupThreads) {
+        const uint32_t c = s_hist[t];
+        s_hist[t] = c ? __hip_atomic_fetch_add(&P.tile_counts[t], c, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) : 0u;
     }
+    if (tid == 0) {
+        if (s_misc[0]) atomicAdd(&P.counters[kCtSetup], s_misc[0]);
+        if (s_misc[1]) atomicAdd(&P.counters[kCtDropped], s_misc[1]);
+    }
+    ZR_STAMP(2);
+    grid_barrier(&P.counters[kCtBarrier], G, P.status);
     ZR_STAMP(3);
-    grid_barrier(&P.counters[kCtBarrier], 2 * G, P.status);
-    ZR_STAMP(4);
     if (P.debug & kDebugStopAfterScan) return;
 
     // ---- phase 3: tile bases and this workgroup's cursors
-    for (uint32_t t = tid; t < nt; t += kSetupThreads) s_hist[t] = ld_sc1(&P.tile_counts[t]);
+    for (uint32_t t = tid; t < nt; t += kSetupThreads) s_base[t] = ld_sc1(&P.tile_counts[t]);
     __syncthreads();
-    const uint32_t total = block_exclusive_scan(s_hist, nt, s_misc + 8);
+    const uint32_t total = block_exclusive_scan(s_base, nt, s_misc + 8);
     if (w == 0) {
-        for (uint32_t t = tid; t < nt; t += kSetupThreads) P.tile_offsets[t] = s_hist[t];
+        for (uint32_t t = tid; t < nt; t += kSetupThreads) P.tile_offsets[t] = s_base[t];
         if (tid == 0) {
+            P.tile_offsets[nt] = total;
             volatile uint32_t* st = P.status;
             st[kStTotalPairs] = total;
             if (total > P.bin_capacity) st[kStOverflow] = 1u;
@@ -492,48 +435,53 @@ __global__ __launch_bounds__(kSetupThreads) void k_setup_bin(DrawParams P) {
             st[kStDroppedClip] = __hip_atomic_load(&P.counters[kCtDropped], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
         }
     }
-    {
-        const uint32_t* row = P.counts + (size_t)w * nt;
-        for (uint32_t t = tid; t < nt; t += kSetupThreads) s_hist[t] += ld_sc1(&row[t]);
-    }
+    for (uint32_t t = tid; t < nt; t += kSetupThreads) s_hist[t] += s_base[t];
     __syncthreads();
+    ZR_STAMP(4);
 
-    ZR_STAMP(5);
-    // ---- phase 4: scatter
-    for (uint32_t k = 0; k < P.tris_per_thread; ++k) {
-        const uint32_t prim = base + k * kSetupThreads + tid;
-        if (prim >= P.prims) continue;
-        const BBox bb = P.bboxes[prim];
-        if (bb.bb0 == kEmptyBox) continue;
-        const int tx0 = (int)(bb.bb0 & 0xFFFFu) >> kTileShift, tx1 = (int)(bb.bb1 & 0xFFFFu) >> kTileShift;
-        const int ty0 = (int)(bb.bb0 >> 16) >> kTileShift, ty1 = (int)(bb.bb1 >> 16) >> kTileShift;
-        for (int ty = ty0; ty <= ty1; ++ty) {
-            if ((uint32_t)ty % P.shard_count != P.shard_rank) continue;
-            const uint32_t r = ((uint32_t)ty / P.shard_count) * P.tiles_x;
-            const int cy0 = max((int)(bb.bb0 >> 16), ty << kTileShift);
-            const int cy1 = min((int)(bb.bb1 >> 16), (ty << kTileShift) + kTile - 1);
-            for (int tx = tx0; tx <= tx1; ++tx) {
-                const int cx0 = max((int)(bb.bb0 & 0xFFFFu), tx << kTileShift);
-                const int cx1 = min((int)(bb.bb1 & 0xFFFFu), (tx << kTileShift) + kTile - 1);
-                const uint32_t area = (uint32_t)((cx1 - cx0 + 1) * (cy1 - cy0 + 1));
-                const uint32_t bucket = min((area - 1u) >> 2, kSortBuckets - 1u);
-                const uint32_t pos = atomicAdd(&s_hist[r + tx], 1u);
-                if (pos < P.bin_capacity) P.bins[pos] = prim | (bucket << kBinPrimBits);
+    // ---- phase 4: scatter the pairs of this workgroup's units, flattened over
+    // (own unit, primitive in unit) so every thread has work
+    {
+        const uint32_t usz = 1u << P.unit_shift;
+        uint32_t nown = 0;
+        while (own_unit(P, w, G, nown) < P.units) ++nown;
+        for (uint32_t j = tid; j < (nown << P.unit_shift); j += kSetupThreads) {
+            const uint32_t prim = (own_unit(P, w, G, j >> P.unit_shift) << P.unit_shift) + (j & (usz - 1u));
+            if (prim >= P.prims) continue;
+            const BBox bb = P.bboxes[prim];
+            if (bb.bb0 == kEmptyBox) continue;
+            const int tx0 = (int)(bb.bb0 & 0xFFFFu) >> kTileShift, tx1 = (int)(bb.bb1 & 0xFFFFu) >> kTileShift;
+            const int ty0 = (int)(bb.bb0 >> 16) >> kTileShift, ty1 = (int)(bb.bb1 >> 16) >> kTileShift;
+            for (int ty = ty0; ty <= ty1; ++ty) {
+                if ((uint32_t)ty % P.shard_count != P.shard_rank) continue;
+                const uint32_t r = ((uint32_t)ty / P.shard_count) * P.tiles_x;
+                const int cy0 = max((int)(bb.bb0 >> 16), ty << kTileShift);
+                const int cy1 = min((int)(bb.bb1 >> 16), (ty << kTileShift) + kTile - 1);
+                for (int tx = tx0; tx <= tx1; ++tx) {
+                    const int cx0 = max((int)(bb.bb0 & 0xFFFFu), tx << kTileShift);
+                    const int cx1 = min((int)(bb.bb1 & 0xFFFFu), (tx << kTileShift) + kTile - 1);
+                    const uint32_t area = (uint32_t)((cx1 - cx0 + 1) * (cy1 - cy0 + 1));
+                    const uint32_t bucket = min((area - 1u) >> 2, kSortBuckets - 1u);
+                    const uint32_t pos = atomicAdd(&s_hist[r + tx], 1u);
+                    if (pos < P.bin_capacity) P.bins[pos] = prim | (bucket << kBinPrimBits);
+                }
             }
         }
     }
-    ZR_STAMP(6);
-    // Every workgroup has left both barriers once it counts itself out here, so the
-    // last one can return the counters to zero for the next draw.
+    ZR_STAMP(5);
+    // Every workgroup has left the barrier and read the tile totals once it counts
+    // itself out here, so the last one can zero the counters for the next draw.
     if (tid == 0) {
         const uint32_t prev = __hip_atomic_fetch_add(&P.counters[kCtExit], 1u, __ATOMIC_RELAXED,
                                                      __HIP_MEMORY_SCOPE_AGENT);
-        if (prev == G - 1u) {
-#pragma unroll
-            for (uint32_t i = 0; i < kCtWords; ++i)
-                __hip_atomic_store(&P.counters[i], 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-        }
+        s_misc[2] = prev == G - 1u ? 1u : 0u;
     }
+    __syncthreads();
+    if (s_misc[2]) {
+        for (uint32_t t = tid; t < nt; t += kSetupThreads) st_sc1(&P.tile_counts[t], 0u);
+        if (tid < kCtWords) st_sc1(&P.counters[tid], 0u);
+    }
+    ZR_STAMP(6);
 }
 
 // ------------------------------------------------------------------- k_tile
@@ -712,9 +660,9 @@ __global__ __launch_bounds__(kTileThreads, 8) void k_tile(DrawParams P) {
     if (threadIdx.x < 255) s_srgb[threadIdx.x] = c_srgbT[threadIdx.x];
     __syncthreads();
 
-    const uint32_t begin = P.tile_offsets[t];
+    const uint32_t begin = P.tile_offsets[t], end = P.tile_offsets[t + 1];
     // entries past bin_capacity were never written (overflowed draw, replayed by the runtime)
-    const uint32_t cnt = begin < P.bin_capacity ? min(P.tile_counts[t], P.bin_capacity - begin) : 0u;
+    const uint32_t cnt = begin < P.bin_capacity ? min(end - begin, P.bin_capacity - begin) : 0u;
     const uint32_t wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
     const int lane = threadIdx.x & 63;
     if (stamp) ts[1] = __builtin_amdgcn_s_memrealtime();
@@ -850,13 +798,24 @@ __global__ __launch_bounds__(kTileThreads) void k_clear(DrawParams P) {
 
 static inline uint32_t blocks_for(uint32_t n, uint32_t per) { return (n + per - 1) / per; }
 
-size_t setup_bin_lds_bytes(uint32_t ntiles) { return (ntiles + 1024 + 32) * sizeof(uint32_t); }
+size_t setup_bin_lds_bytes(uint32_t ntiles) { return (2 * (size_t)ntiles + 32) * sizeof(uint32_t); }
 
-const void* setup_bin_kernel() { return reinterpret_cast<const void*>(&k_setup_bin); }
+const void* setup_bin_kernel(uint32_t batch) {
+    switch (batch) {
+    case 1: return reinterpret_cast<const void*>(&k_setup_bin<1>);
+    case 2: return reinterpret_cast<const void*>(&k_setup_bin<2>);
+    default: return reinterpret_cast<const void*>(&k_setup_bin<4>);
+    }
+}
 
 void launch_setup_bin(const DrawParams& p, void* stream) {
-    hipLaunchKernelGGL(k_setup_bin, dim3(p.setup_wgs), dim3(kSetupThreads), setup_bin_lds_bytes(p.ntiles),
-                       (hipStream_t)stream, p);
+    const size_t lds = setup_bin_lds_bytes(p.ntiles);
+    const hipStream_t s = (hipStream_t)stream;
+    switch (p.setup_batch) {
+    case 1: hipLaunchKernelGGL(k_setup_bin<1>, dim3(p.setup_wgs), dim3(kSetupThreads), lds, s, p); break;
+    case 2: hipLaunchKernelGGL(k_setup_bin<2>, dim3(p.setup_wgs), dim3(kSetupThreads), lds, s, p); break;
+    default: hipLaunchKernelGGL(k_setup_bin<4>, dim3(p.setup_wgs), dim3(kSetupThreads), lds, s, p); break;
+    }
 }
 
 template <int PROG, int MODE>

@@ -169,8 +169,6 @@ struct zr_device_t {
     uint64_t records_cap = 0;  // primitives
     BBox* bboxes = nullptr;
     uint64_t bboxes_cap = 0;
-    uint32_t* counts = nullptr;
-    uint64_t counts_cap = 0;
     int cu_count = 0;
     uint32_t occupancy_checked_tiles = 0;
     uint32_t* tile_counts = nullptr;
@@ -179,6 +177,8 @@ struct zr_device_t {
     uint64_t tiles_cap2 = 0;
     uint32_t* counters = nullptr;
     uint64_t counters_cap = 0;
+    uint32_t setup_sched = 1;  // k_setup_bin unit schedule (ZR_SETUP_SCHED: 0 contiguous, 1 interleaved)
+    uint32_t setup_batch = 2;  // k_setup_bin primitives per lane in flight (ZR_SETUP_BATCH: 1, 2, 4)
     uint32_t* bins = nullptr;
     uint64_t bins_cap = 0;
     uint32_t debug = 0;
@@ -441,8 +441,11 @@ zr_result ensure_scratch(zr_device* d, DrawParams& P) {
     const uint64_t prims = std::max<uint64_t>(P.prims, 1);
     if ((rc = grow(d, d->records, d->records_cap, prims, sizeof(TriRecord)))) return rc;
     if ((rc = grow(d, d->bboxes, d->bboxes_cap, prims, sizeof(BBox)))) return rc;
-    if ((rc = grow(d, d->counts, d->counts_cap, (uint64_t)P.setup_wgs * P.ntiles + 1, 4))) return rc;
-    if ((rc = grow(d, d->tile_counts, d->tiles_cap, P.ntiles + 1, 4))) return rc;
+    {  // per-tile counters start at zero; k_setup_bin leaves them zero after every draw
+        const uint64_t cap = d->tiles_cap;
+        if ((rc = grow(d, d->tile_counts, d->tiles_cap, P.ntiles + 1, 4))) return rc;
+        if (d->tiles_cap != cap) ZR_HIP(hipMemset(d->tile_counts, 0, d->tiles_cap * 4));
+    }
     if ((rc = grow(d, d->tile_offsets, d->tiles_cap2, P.ntiles + 1, 4))) return rc;
     if (!d->counters) {  // zeroed once; k_setup_bin leaves them zero after every draw
         if ((rc = grow(d, d->counters, d->counters_cap, kCtWords, 4))) return rc;
@@ -454,7 +457,6 @@ zr_result ensure_scratch(zr_device* d, DrawParams& P) {
     }
     P.records = d->records;
     P.bboxes = d->bboxes;
-    P.counts = d->counts;
     P.tile_counts = d->tile_counts;
     P.tile_offsets = d->tile_offsets;
     P.counters = d->counters;
@@ -550,19 +552,26 @@ zr_result exec_draw(zr_device* d, ExecState& s, const Cmd& c, bool indexed) {
     // (every workgroup resident: it synchronises through grid barriers)
     if (P.ntiles > kMaxTilesPerPass)
         return fail(ZR_ERROR_FEATURE_NOT_PRESENT, "more than 16384 owned 32x32 tiles in one pass");
+    P.setup_batch = d->setup_batch;
+    P.setup_sched = d->setup_sched;
     if (d->occupancy_checked_tiles != P.ntiles) {
         int nb = 0;
-        ZR_HIP(hipOccupancyMaxActiveBlocksPerMultiprocessor(&nb, setup_bin_kernel(), kSetupThreads,
+        ZR_HIP(hipOccupancyMaxActiveBlocksPerMultiprocessor(&nb, setup_bin_kernel(P.setup_batch), kSetupThreads,
                                                             setup_bin_lds_bytes(P.ntiles)));
         if (nb < 1) return fail(ZR_ERROR_FEATURE_NOT_PRESENT, "k_setup_bin cannot be resident on a CU");
         d->occupancy_checked_tiles = P.ntiles;
     }
     {
+        // one workgroup per CU (fewer for small draws); a wave processes units of
+        // 64 * batch * 2^k primitives, at most ~64 units per workgroup on average
         const uint64_t cus = (uint64_t)std::max(d->cu_count, 1);
-        const uint64_t per_wave = (uint64_t)kSetupThreads * cus;
-        P.tris_per_thread = (uint32_t)std::max<uint64_t>(1, (prims + per_wave - 1) / per_wave);
-        const uint64_t chunk = (uint64_t)kSetupThreads * P.tris_per_thread;
-        P.setup_wgs = (uint32_t)std::max<uint64_t>(1, (prims + chunk - 1) / chunk);
+        const uint64_t per_wg = (uint64_t)kSetupThreads * P.setup_batch;
+        P.setup_wgs = (uint32_t)std::max<uint64_t>(1, std::min<uint64_t>(cus, (prims + per_wg - 1) / per_wg));
+        uint32_t shift = 6;
+        while ((1u << shift) < 64u * P.setup_batch) ++shift;
+        while (((prims + (1ull << shift) - 1) >> shift) > 64ull * P.setup_wgs) ++shift;
+        P.unit_shift = shift;
+        P.units = (uint32_t)std::max<uint64_t>(1, (prims + (1ull << shift) - 1) >> shift);
     }
     P.debug = d->debug;
     if (d->debug & kDebugStamps) {
@@ -576,7 +585,10 @@ zr_result exec_draw(zr_device* d, ExecState& s, const Cmd& c, bool indexed) {
     d->last.triangles_in = prims;
 
     // debug early exits skip the self-reset at the end of k_setup_bin
-    if (d->debug) ZR_HIP(hipMemsetAsync(P.counters, 0, kCtWords * 4, d->stream));
+    if (d->debug) {
+        ZR_HIP(hipMemsetAsync(P.counters, 0, kCtWords * 4, d->stream));
+        ZR_HIP(hipMemsetAsync(P.tile_counts, 0, (size_t)P.ntiles * 4, d->stream));
+    }
     timed_launch(d, "setup_bin", [&] { launch_setup_bin(P, d->stream); });
     timed_launch(d, "tile", [&] { launch_tile(P, d->stream); });
     ZR_HIP(hipGetLastError());
@@ -660,6 +672,11 @@ ZR_API zr_result zr_device_create(int32_t hip_device, zr_device** out) {
     if (const char* dbg = getenv("ZR_DEBUG")) d->debug = (uint32_t)strtoul(dbg, nullptr, 0);
     if (const char* p = getenv("ZR_DEBUG_TS")) d->dbg_ts_path = p;
     if (const char* cap = getenv("ZR_BIN_CAPACITY")) d->initial_bins = std::max<uint64_t>(64, strtoull(cap, nullptr, 0));
+    if (const char* sc = getenv("ZR_SETUP_SCHED")) d->setup_sched = std::min<uint32_t>(1, (uint32_t)strtoul(sc, nullptr, 0));
+    if (const char* b = getenv("ZR_SETUP_BATCH")) {
+        const unsigned long v = strtoul(b, nullptr, 0);
+        d->setup_batch = v >= 4 ? 4u : (v >= 2 ? 2u : 1u);
+    }
     ZR_HIP(hipSetDevice(hip_device));
     ZR_HIP(hipStreamCreateWithFlags(&d->stream, hipStreamNonBlocking));
     ZR_HIP(hipDeviceGetAttribute(&d->cu_count, hipDeviceAttributeMultiprocessorCount, hip_device));
@@ -680,8 +697,8 @@ ZR_API void zr_device_destroy(zr_device* d) {
     (void)hipStreamSynchronize(d->stream);
     collect_timings(d);
     for (hipEvent_t e : d->event_pool) (void)hipEventDestroy(e);
-    for (void* p : {(void*)d->dbg_ts, (void*)d->records, (void*)d->bboxes, (void*)d->counts,
-                    (void*)d->tile_counts, (void*)d->tile_offsets, (void*)d->counters, (void*)d->bins})
+    for (void* p : {(void*)d->dbg_ts, (void*)d->records, (void*)d->bboxes, (void*)d->tile_counts,
+                    (void*)d->tile_offsets, (void*)d->counters, (void*)d->bins})
         if (p) (void)hipFree(p);
     (void)hipHostFree(d->status_host);
     (void)hipStreamDestroy(d->stream);
