@@ -1,0 +1,9 @@
+# bin loads hoisted to kernel start
+set -o pipefail
+export TMPDIR=/tmp
+O=gpurun_out/v20
+mkdir -p $O
+timeout -k 10 700 python -m pytest tests -m gpu -x -q > $O/pytest.log 2>&1 || exit 1
+timeout -k 10 200 python bench.py --no-cpu-baseline > $O/bench.json 2>> $O/bench.err || exit 2
+ZR_DEBUG=128 ZR_DEBUG_TS=$O/n.txt timeout -k 10 200 python bench.py --steps 3 --warmup 1 --no-cpu-baseline > /dev/null 2>> $O/bench.err || exit 3
+echo done

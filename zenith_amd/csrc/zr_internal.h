@@ -10,7 +10,7 @@ constexpr int kTileShift = 5;
 constexpr int kTilePixels = kTile * kTile;
 constexpr int kTileThreads = 256;  // 4 waves of 64
 constexpr uint32_t kSortCap = 1024;     // tile-list segment sorted by area in LDS
-constexpr uint32_t kSortBuckets = 64;   // 4-pixel-wide area buckets (last: > 252 px)
+constexpr uint32_t kSortBuckets = 64;   // bbox-shape classes: 8 width classes x 8 height classes
 constexpr int kSetupThreads = 1024;  // setup / bin workgroups (one LDS histogram each)
 
 enum Program : int32_t { kProgTriangle = 0, kProgFlat = 1, kProgBlinn = 2, kProgCount = 3 };
@@ -48,7 +48,14 @@ enum : uint32_t { kFlagSwapped = 1u, kFlagBias0 = 2u, kFlagBias1 = 4u, kFlagBias
 // raster path steps edges incrementally in 32-bit integers.
 constexpr int32_t kSmallExtent = 64 * 256;
 constexpr uint32_t kEmptyBox = 0xFFFFFFFFu;
-// Bin entry = primitive id | (area bucket of its bbox ∩ tile) << kBinPrimBits
+// Bin entry = primitive id | (shape class of its bbox ∩ tile, shape_bucket()) << kBinPrimBits
+// Size class of a bbox extent in pixels: 1, 2, 3, 4, 5-6, 7-8, 9-12, 13+.
+__host__ __device__ inline uint32_t extent_class(int d) {
+    return d <= 4 ? (uint32_t)(d - 1) : d <= 6 ? 4u : d <= 8 ? 5u : d <= 12 ? 6u : 7u;
+}
+// k_tile sorts a tile's entries by this so a 64-lane chunk shares one bbox shape
+// (the lane raster's nested row/column loops then hardly diverge).
+__host__ __device__ inline uint32_t shape_bucket(int w, int h) { return extent_class(w) * 8u + extent_class(h); }
 constexpr uint32_t kBinPrimBits = 26;
 constexpr uint32_t kBinPrimMask = (1u << kBinPrimBits) - 1u;
 struct alignas(8) BBox {
@@ -57,8 +64,9 @@ struct alignas(8) BBox {
 constexpr uint32_t kMaxTilesPerPass = 16384;  // LDS histogram of the setup pass (64 KB)
 
 // Timing-experiment switches (ZR_DEBUG env var); never set in production runs.
-enum : uint32_t { kDebugSkipRaster = 1u, kDebugSkipShade = 2u, kDebugNoAtomic = 8u, kDebugLoadOnly = 16u,
-                  kDebugPhase1Only = 32u, kDebugStopAfterScan = 64u, kDebugStamps = 128u };
+enum : uint32_t { kDebugSkipRaster = 1u, kDebugSkipShade = 2u, kDebugLoadOnly = 16u,
+                  kDebugPhase1Only = 32u, kDebugStopAfterScan = 64u, kDebugStamps = 128u,
+                  kDebugReverseTiles = 256u };
 
 // Status words in host-mapped pinned memory (read by the runtime at sync points).
 enum StatusWord : uint32_t {

@@ -26,6 +26,14 @@
 
 namespace zr {
 
+// Build-time tuning knobs of k_tile (A/B builds: tools/build_variant.sh).
+#ifndef ZR_TILE_WGS
+#define ZR_TILE_WGS 8        // k_tile workgroups per CU the register budget is sized for
+#endif
+#ifndef ZR_TILE_PREFETCH
+#define ZR_TILE_PREFETCH 0   // request the next chunk's records before rasterizing this one
+#endif
+
 __constant__ float c_srgbT[255] = ZR_SRGB_THRESHOLDS_INIT;
 
 // ------------------------------------------------------------------ helpers
@@ -192,7 +200,7 @@ __device__ __forceinline__ void setup_finish(const DrawParams& P, uint32_t prim,
             if (!(fabsf(xf) < 4194304.0f && fabsf(yf) < 4194304.0f)) { ++ndropped; ok = false; break; }
             X[k] = (int32_t)rintf(xf * 256.0f);
             Y[k] = (int32_t)rintf(yf * 256.0f);
-            z[k] = fmaf(zd, P.dr, P.dmin);
+            z[k] = fmaf(zd, P.dr, P.dmin) + 0.0f;  // -0 -> +0 (k_tile relies on it)
         }
     }
     if (ok) {
@@ -607,48 +615,67 @@ __device__ __forceinline__ void raster_lane(const DrawParams& P, const int4 q0, 
     const int sx0 = -dy0 * 256, sx1 = -dy1 * 256, sx2 = -dy2 * 256;  // +1 pixel in x
     const int sy0 = dx0 * 256, sy1 = dx1 * 256, sy2 = dx2 * 256;     // +1 pixel in y
     const int b0 = (int)((flags >> 1) & 1u), b1 = (int)((flags >> 2) & 1u), b2 = (int)((flags >> 3) & 1u);
+    // Sweep the bbox in row order, stepping the edge values: +sx per pixel, and at
+    // the end of a row the jump back to the next row's first pixel, chosen with
+    // selects (no divergent branch).  The top-left bias is folded into the edge
+    // values, so coverage is one sign test; depth adds it back.  Fragment depth is
+    // never -0 here: setup canonicalised the vertex depths to +0 (the oracle's
+    // per-fragment -0 -> +0 rule therefore gives the same bits).
     const int n = bw * bh;
-    int w0 = r0, w1 = r1, w2 = r2;
-    int ex = 0, li = (by0 - y0) * kTile + (bx0 - x0);
+    const int j0 = sy0 - (bw - 1) * sx0, j1 = sy1 - (bw - 1) * sx1, j2 = sy2 - (bw - 1) * sx2;
+    int w0 = r0 - b0, w1 = r1 - b1, w2 = r2 - b2;
+    int ex = 0;
+    uint32_t la = (uint32_t)(((by0 - y0) * kTile + (bx0 - x0)) * 8);  // byte offset of the key
+    const uint32_t lj = (uint32_t)((kTile - bw + 1) * 8);
     for (int k = 0; k < n; ++k) {
-        if (((w0 - b0) | (w1 - b1) | (w2 - b2)) >= 0) {
-            const float fb1 = (float)w1 * invA2, fb2 = (float)w2 * invA2;
-            float z = fmaf(fb2, dz2, fmaf(fb1, dz1, z0));
-            z = z == 0.0f ? 0.0f : z;
-            if (z >= P.dlo && z <= P.dhi && (!INITD || depth_pass(P.depth_op, z, s_initd[li]))) {
-                if (P.debug & kDebugNoAtomic) {
-                    if (z == -1.0f) s_key[li] = frag_key<MODE>(z, seq);  // never true: keeps the work alive
-                } else {
-                    atomicMin(&s_key[li], frag_key<MODE>(z, seq));
-                }
-            }
+        if ((w0 | w1 | w2) >= 0) {
+            const float fb1 = (float)(w1 + b1) * invA2, fb2 = (float)(w2 + b2) * invA2;
+            const float z = fmaf(fb2, dz2, fmaf(fb1, dz1, z0));
+            if (z >= P.dlo && z <= P.dhi && (!INITD || depth_pass(P.depth_op, z, s_initd[la >> 3])))
+                atomicMin(reinterpret_cast<unsigned long long*>(reinterpret_cast<char*>(s_key) + la),
+                          frag_key<MODE>(z, seq));
         }
-        if (++ex == bw) {
-            ex = 0;
-            r0 += sy0; r1 += sy1; r2 += sy2;
-            w0 = r0; w1 = r1; w2 = r2;
-            li += kTile - bw + 1;
-        } else {
-            w0 += sx0; w1 += sx1; w2 += sx2;
-            ++li;
-        }
+        const bool wrap = ++ex == bw;
+        ex = wrap ? 0 : ex;
+        w0 += wrap ? j0 : sx0;
+        w1 += wrap ? j1 : sx1;
+        w2 += wrap ? j2 : sx2;
+        la += wrap ? lj : 8u;
     }
 }
 
 template <int PROG, int MODE, bool INITD>
-__global__ __launch_bounds__(kTileThreads, 8) void k_tile(DrawParams P) {
+__global__ __launch_bounds__(kTileThreads, ZR_TILE_WGS) void k_tile(DrawParams P) {
     __shared__ unsigned long long s_key[kTilePixels];
     __shared__ float s_initd[INITD ? kTilePixels : 1];
     __shared__ uint32_t s_sorted[kSortCap];
     __shared__ uint32_t s_bucket[kSortBuckets];
     __shared__ float s_srgb[256];
-    const uint32_t t = blockIdx.x;
+    const uint32_t t = (P.debug & kDebugReverseTiles) ? P.ntiles - 1u - blockIdx.x : blockIdx.x;
     const uint32_t oy = t / P.tiles_x, tx = t - oy * P.tiles_x;
     const uint32_t ty = oy * P.shard_count + P.shard_rank;
     const int x0 = (int)tx * kTile, y0 = (int)ty * kTile;
     const bool stamp = (P.debug & kDebugStamps) && threadIdx.x == 0 && t < kMaxTilesPerPass;
     unsigned long long* ts = P.dbg_ts + 8192 * 8 + (size_t)t * 8;
     if (stamp) ts[0] = __builtin_amdgcn_s_memrealtime();
+
+    // The tile's list bounds and its first segment of bin entries are requested
+    // before anything else: workgroups dispatched last would otherwise queue these
+    // loads behind the record gathers of every tile that started earlier.
+    const uint32_t begin = P.tile_offsets[t], end = P.tile_offsets[t + 1];
+    // entries past bin_capacity were never written (overflowed draw, replayed by the runtime)
+    const uint32_t cnt = begin < P.bin_capacity ? min(end - begin, P.bin_capacity - begin) : 0u;
+    constexpr uint32_t kPerThread = kSortCap / kTileThreads;
+    uint32_t ent[kPerThread];
+    auto load_segment = [&](uint32_t seg) {
+        const uint32_t n = min(kSortCap, cnt - seg);
+#pragma unroll
+        for (uint32_t k = 0; k < kPerThread; ++k) {
+            const uint32_t i = threadIdx.x + k * kTileThreads;
+            ent[k] = i < n ? P.bins[begin + seg + i] : 0u;  // prim | area bucket (k_setup_bin phase 4)
+        }
+    };
+    if (cnt && !(P.debug & kDebugSkipRaster)) load_segment(0);
 
     for (int i = threadIdx.x; i < kTilePixels; i += kTileThreads) {
         const int px = x0 + (i & (kTile - 1)), py = y0 + (i >> kTileShift);
@@ -660,9 +687,6 @@ __global__ __launch_bounds__(kTileThreads, 8) void k_tile(DrawParams P) {
     if (threadIdx.x < 255) s_srgb[threadIdx.x] = c_srgbT[threadIdx.x];
     __syncthreads();
 
-    const uint32_t begin = P.tile_offsets[t], end = P.tile_offsets[t + 1];
-    // entries past bin_capacity were never written (overflowed draw, replayed by the runtime)
-    const uint32_t cnt = begin < P.bin_capacity ? min(end - begin, P.bin_capacity - begin) : 0u;
     const uint32_t wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
     const int lane = threadIdx.x & 63;
     if (stamp) ts[1] = __builtin_amdgcn_s_memrealtime();
@@ -674,17 +698,17 @@ __global__ __launch_bounds__(kTileThreads, 8) void k_tile(DrawParams P) {
         // lane per entry loads the 64-B record, and the wave walks the chunk.
         for (uint32_t seg = 0; seg < cnt; seg += kSortCap) {
             const uint32_t n = min(kSortCap, cnt - seg);
+            if (seg) load_segment(seg);
             if (threadIdx.x < kSortBuckets) s_bucket[threadIdx.x] = 0u;
             __syncthreads();
-            uint32_t pr[kSortCap / kTileThreads], bk[kSortCap / kTileThreads], sl[kSortCap / kTileThreads];
+            uint32_t pr[kPerThread], bk[kPerThread], sl[kPerThread];
 #pragma unroll
-            for (uint32_t k = 0; k < kSortCap / kTileThreads; ++k) {
+            for (uint32_t k = 0; k < kPerThread; ++k) {
                 const uint32_t i = threadIdx.x + k * kTileThreads;
                 pr[k] = bk[k] = sl[k] = 0u;
                 if (i < n) {
-                    const uint32_t e = P.bins[begin + seg + i];  // prim | area bucket (k_setup_bin phase 4)
-                    pr[k] = e & kBinPrimMask;
-                    bk[k] = e >> kBinPrimBits;
+                    pr[k] = ent[k] & kBinPrimMask;
+                    bk[k] = ent[k] >> kBinPrimBits;
                     sl[k] = atomicAdd(&s_bucket[bk[k]], 1u);
                 }
             }
@@ -701,21 +725,32 @@ __global__ __launch_bounds__(kTileThreads, 8) void k_tile(DrawParams P) {
             }
             __syncthreads();
 #pragma unroll
-            for (uint32_t k = 0; k < kSortCap / kTileThreads; ++k) {
+            for (uint32_t k = 0; k < kPerThread; ++k) {
                 const uint32_t i = threadIdx.x + k * kTileThreads;
                 if (i < n) s_sorted[s_bucket[bk[k]] + sl[k]] = pr[k];
             }
             __syncthreads();
             if (stamp && seg == 0) ts[2] = __builtin_amdgcn_s_memrealtime();
-            for (uint32_t cb = wave * 64u; cb < n; cb += kTileThreads) {
-                const uint32_t j = cb + (uint32_t)lane;
-                uint32_t my_prim = 0;
-                int4 q0 = make_int4(0, 0, 0, 0), q1 = q0, q2 = q0, q3 = q0;
+            // One lane per entry loads its 64-B record.  With ZR_TILE_PREFETCH the
+            // next chunk's records are requested before the current chunk is
+            // rasterized (the gather hides behind the raster loop).
+            uint32_t nprim = 0;
+            int4 n0 = make_int4(0, 0, 0, 0), n1 = n0, n2 = n0, n3 = n0;
+            auto fetch = [&](uint32_t cbx) {
+                const uint32_t j = cbx + (uint32_t)lane;
                 if (j < n) {
-                    my_prim = s_sorted[j];
-                    const int4* rp = reinterpret_cast<const int4*>(P.records + my_prim);
-                    q0 = rp[0]; q1 = rp[1]; q2 = rp[2]; q3 = rp[3];
+                    nprim = s_sorted[j];
+                    const int4* rp = reinterpret_cast<const int4*>(P.records + nprim);
+                    n0 = rp[0]; n1 = rp[1]; n2 = rp[2]; n3 = rp[3];
                 }
+            };
+            if (ZR_TILE_PREFETCH) fetch(wave * 64u);
+            for (uint32_t cb = wave * 64u; cb < n; cb += kTileThreads) {
+                if (!ZR_TILE_PREFETCH) fetch(cb);
+                const uint32_t j = cb + (uint32_t)lane;
+                const uint32_t my_prim = nprim;
+                const int4 q0 = n0, q1 = n1, q2 = n2, q3 = n3;
+                if (ZR_TILE_PREFETCH) fetch(cb + kTileThreads);
                 const bool valid = j < n && !(P.debug & kDebugLoadOnly);
                 if (P.debug & kDebugLoadOnly) asm volatile("" ::"v"(q0.x), "v"(q1.x), "v"(q2.x), "v"(q3.x), "v"(my_prim));
                 const bool small = valid && (((uint32_t)q3.w & kFlagSmall) != 0u);
@@ -777,7 +812,14 @@ __global__ __launch_bounds__(kTileThreads, 8) void k_tile(DrawParams P) {
             else if (P.clear_depth_enable) *dp = P.clear_depth;
         }
     }
-    if (stamp) ts[4] = __builtin_amdgcn_s_memrealtime();
+    if (stamp) {
+        ts[4] = __builtin_amdgcn_s_memrealtime();
+        uint32_t hw, xcc;
+        asm volatile("s_getreg_b32 %0, hwreg(HW_REG_HW_ID)" : "=s"(hw));
+        asm volatile("s_getreg_b32 %0, hwreg(HW_REG_XCC_ID)" : "=s"(xcc));
+        ts[5] = ((unsigned long long)xcc << 32) | hw;
+        ts[6] = cnt;
+    }
 }
 
 __global__ __launch_bounds__(kTileThreads) void k_clear(DrawParams P) {

@@ -148,6 +148,15 @@ struct zr_cmd_t {
     zr_result err = ZR_SUCCESS;
     std::string err_msg;
     bool in_rendering = false;
+    // Replay of an unchanged command list: its launches captured once into a HIP
+    // graph (valid while the device's scratch generation is unchanged).
+    hipGraphExec_t graph = nullptr;
+    uint64_t graph_gen = 0;
+    uint32_t eager_runs = 0;
+    void drop_graph() {
+        if (graph) (void)hipGraphExecDestroy(graph);
+        graph = nullptr;
+    }
 };
 
 struct zr_fence_t {
@@ -195,6 +204,9 @@ struct zr_device_t {
     uint64_t last_prims = 0;
     // profiling
     bool profiling = false;
+    bool use_graphs = false;    // ZR_GRAPH=1: replay resubmitted command lists as HIP graphs
+    bool capturing = false;     // inside hipStreamBeginCapture: no allocation allowed
+    uint64_t scratch_gen = 0;   // bumped whenever a scratch buffer is reallocated
     std::vector<TimedLaunch> timed;
     std::vector<hipEvent_t> event_pool;
     std::map<std::string, std::pair<double, uint64_t>> times;
@@ -250,6 +262,8 @@ void timed_launch(zr_device* d, const char* name, F&& fn) {
 template <typename T>
 zr_result grow(zr_device* d, T*& ptr, uint64_t& cap, uint64_t need, uint64_t elem_bytes) {
     if (need <= cap && ptr) return ZR_SUCCESS;
+    if (d->capturing) return ZR_NOT_READY;  // graph capture aborted: the caller runs eagerly
+    d->scratch_gen++;
     ZR_HIP(hipStreamSynchronize(d->stream));
     if (ptr) (void)hipFree(ptr);
     ptr = nullptr;
@@ -306,6 +320,23 @@ void dump_stamps(zr_device* d) {
             }
         }
     }
+    {  // raw per-tile stamps for offline analysis: <path>.tiles.csv
+        std::vector<unsigned long long> tt(d->dbg_tiles * 8);
+        if (d->dbg_tiles && hipMemcpy(tt.data(), d->dbg_ts + 8192 * 8, tt.size() * 8, hipMemcpyDeviceToHost) == hipSuccess) {
+            FILE* g = fopen((d->dbg_ts_path + ".tiles.csv").c_str(), "a");
+            if (g) {
+                unsigned long long t1 = ~0ull;
+                for (uint32_t w = 0; w < d->dbg_tiles; ++w) t1 = std::min(t1, tt[w * 8]);
+                fprintf(g, "tile,t0,t1,t2,t3,t4,hwid,xcc,count\n");
+                for (uint32_t w = 0; w < d->dbg_tiles; ++w) {
+                    fprintf(g, "%u", w);
+                    for (int i = 0; i <= 4; ++i) fprintf(g, ",%.2f", (double)(tt[w * 8 + i] - t1) * 0.01);
+                    fprintf(g, ",%llu,%llu,%llu\n", tt[w * 8 + 5] & 0xFFFFFFFFull, tt[w * 8 + 5] >> 32, tt[w * 8 + 6]);
+                }
+                fclose(g);
+            }
+        }
+    }
     fprintf(f, "\n  p1 first 16 wgs:");
     for (uint32_t w = 0; w < std::min(16u, d->dbg_wgs); ++w) fprintf(f, " %.1f", (double)(ts[w * 8 + 1] - ts[w * 8]) * 0.01);
     fprintf(f, "\n  p1 last 16 wgs:");
@@ -343,6 +374,7 @@ zr_result device_sync(zr_device* d) {
         st[kStOverflow] = 0;
         ZR_HIP(hipFree(d->bins));
         d->bins = nullptr;
+        d->scratch_gen++;
         void* p = nullptr;
         ZR_HIP(hipMalloc(&p, need * 4));
         d->bins = (uint32_t*)p;
@@ -672,6 +704,7 @@ ZR_API zr_result zr_device_create(int32_t hip_device, zr_device** out) {
     if (const char* dbg = getenv("ZR_DEBUG")) d->debug = (uint32_t)strtoul(dbg, nullptr, 0);
     if (const char* p = getenv("ZR_DEBUG_TS")) d->dbg_ts_path = p;
     if (const char* cap = getenv("ZR_BIN_CAPACITY")) d->initial_bins = std::max<uint64_t>(64, strtoull(cap, nullptr, 0));
+    if (const char* g = getenv("ZR_GRAPH")) d->use_graphs = strtoul(g, nullptr, 0) != 0;
     if (const char* sc = getenv("ZR_SETUP_SCHED")) d->setup_sched = std::min<uint32_t>(1, (uint32_t)strtoul(sc, nullptr, 0));
     if (const char* b = getenv("ZR_SETUP_BATCH")) {
         const unsigned long v = strtoul(b, nullptr, 0);
@@ -1081,6 +1114,7 @@ ZR_API void zr_cmd_destroy(zr_cmd* c) {
     if (!c) return;
     auto& pend = c->dev->pending;
     if (std::find(pend.begin(), pend.end(), c) != pend.end()) device_sync(c->dev);
+    c->drop_graph();
     delete c;
 }
 
@@ -1095,6 +1129,8 @@ ZR_API zr_result zr_cmd_begin(zr_cmd* c) {
     c->err = ZR_SUCCESS;
     c->err_msg.clear();
     c->in_rendering = false;
+    c->drop_graph();
+    c->eager_runs = 0;
     return ZR_SUCCESS;
 }
 
@@ -1281,13 +1317,51 @@ ZR_API void zr_fence_destroy(zr_fence* f) {
     delete f;
 }
 
+// Executes a command list on the device stream.  The first submission runs eagerly
+// (sizing scratch); the second captures the same launches into a HIP graph, later
+// ones replay it (one launch per frame instead of one per kernel).
+static zr_result submit_graph_or_eager(zr_device* d, zr_cmd* c) {
+    const bool graphs = d->use_graphs && !d->profiling && !d->debug;
+    if (!graphs || c->eager_runs == 0) {
+        c->eager_runs++;
+        return execute(d, c);
+    }
+    if (c->graph && c->graph_gen == d->scratch_gen) {
+        ZR_HIP(hipGraphLaunch(c->graph, d->stream));
+        return ZR_SUCCESS;
+    }
+    c->drop_graph();
+    const uint64_t gen = d->scratch_gen;
+    ZR_HIP(hipStreamBeginCapture(d->stream, hipStreamCaptureModeRelaxed));
+    d->capturing = true;
+    zr_result rc = execute(d, c);
+    d->capturing = false;
+    hipGraph_t g = nullptr;
+    const hipError_t e = hipStreamEndCapture(d->stream, &g);
+    if (rc == ZR_SUCCESS && e == hipSuccess && g && d->scratch_gen == gen) {
+        const hipError_t ie = hipGraphInstantiate(&c->graph, g, nullptr, nullptr, 0);
+        (void)hipGraphDestroy(g);
+        if (ie == hipSuccess) {
+            c->graph_gen = gen;
+            ZR_HIP(hipGraphLaunch(c->graph, d->stream));
+            return ZR_SUCCESS;
+        }
+        c->graph = nullptr;
+    } else if (g) {
+        (void)hipGraphDestroy(g);
+    }
+    if (rc != ZR_SUCCESS && rc != ZR_NOT_READY) return rc;
+    c->eager_runs++;
+    return execute(d, c);  // scratch had to grow (or capture failed): run eagerly
+}
+
 ZR_API zr_result zr_submit(zr_device* d, zr_cmd* c, zr_fence* f) {
     if (!d || !c) return fail(ZR_ERROR_VALIDATION_FAILED, "NULL argument");
     if (c->err) return fail(c->err, c->err_msg);
     if (c->in_rendering) return fail(ZR_ERROR_VALIDATION_FAILED, "submitted inside a render pass");
     zr_result rc = set_device(d);
     if (rc) return rc;
-    rc = execute(d, c);
+    rc = submit_graph_or_eager(d, c);
     if (rc) return rc;
     d->pending.push_back(c);
     if (f) {

@@ -13,7 +13,8 @@ import ctypes as C
 import os
 
 _HERE = os.path.dirname(os.path.abspath(__file__))
-LIB_PATH = os.path.join(_HERE, "lib", "libzenith_raster.so")
+# ZR_LIB_PATH: an alternative build of the same library (A/B experiments)
+LIB_PATH = os.environ.get("ZR_LIB_PATH") or os.path.join(_HERE, "lib", "libzenith_raster.so")
 
 # ----------------------------------------------------------------- constants
 SUCCESS, NOT_READY, TIMEOUT = 0, 1, 2
