@@ -8,7 +8,10 @@ namespace zr {
 constexpr int kTile = 32;          // screen-tile edge in pixels (one workgroup per tile)
 constexpr int kTileShift = 5;
 constexpr int kTilePixels = kTile * kTile;
-constexpr int kTileThreads = 256;  // 4 waves of 64
+#ifndef ZR_TILE_THREADS
+#define ZR_TILE_THREADS 256
+#endif
+constexpr int kTileThreads = ZR_TILE_THREADS;  // k_tile workgroup: 4 waves of 64 (build knob)
 constexpr uint32_t kSortCap = 1024;     // tile-list segment sorted by area in LDS
 constexpr uint32_t kSortBuckets = 64;   // bbox-shape classes: 8 width classes x 8 height classes
 constexpr int kSetupThreads = 1024;  // setup / bin workgroups (one LDS histogram each)
@@ -41,6 +44,21 @@ struct alignas(16) TriRecord {
     uint32_t flags;           // bit0 swapped v1<->v2, bits1..3 edge bias (0 = top-left edge), bit4 small
 };
 static_assert(sizeof(TriRecord) == 64, "TriRecord must be 64 B");
+
+// Compact per-primitive record, the one k_tile gathers for every (tile, primitive)
+// pair: vertex 0 in 24.8 fixed point, vertices 1 and 2 as int16
+// deltas from it (exact for kFlagSmall primitives: extents <= 64 px * 256), the
+// depth terms, and 1/A2 with the orientation swap (kFlagSwapped) in its sign bit
+// (A2 > 0 after orientation, so the bit is free).  Bias flags and the pixel bbox
+// are recomputed from the vertices.  A primitive too large for int16 deltas has
+// dx1 == kCompactLarge and its full TriRecord in records_big.
+struct alignas(16) TriCompact {
+    int32_t X0, Y0;
+    int16_t dx1, dy1, dx2, dy2;
+    float z0, dz1, dz2, invA2s;
+};
+static_assert(sizeof(TriCompact) == 32, "TriCompact must be 32 B");
+constexpr int16_t kCompactLarge = -32768;
 
 enum : uint32_t { kFlagSwapped = 1u, kFlagBias0 = 2u, kFlagBias1 = 4u, kFlagBias2 = 8u, kFlagSmall = 16u };
 // A primitive is "small" when its fixed-point bbox spans <= 64 px in x and y: every
@@ -127,7 +145,8 @@ struct DrawParams {
     // tiling / sharding
     uint32_t tiles_x, tiles_y, shard_rank, shard_count, owned_rows, ntiles;
     // scratch (binning without contended global atomics)
-    TriRecord* records;       // [prims]
+    TriCompact* records;      // [prims] compact records (every binned primitive)
+    TriRecord* records_big;   // [prims] full records, written for large primitives only
     BBox* bboxes;             // [prims]; bb0 == kEmptyBox when culled / no owned tile
     uint32_t* tile_counts;    // [ntiles]
     uint32_t* tile_offsets;   // [ntiles] exclusive scan (list starts)

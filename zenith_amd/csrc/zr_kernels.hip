@@ -30,6 +30,9 @@ namespace zr {
 #ifndef ZR_TILE_WGS
 #define ZR_TILE_WGS 8        // k_tile workgroups per CU the register budget is sized for
 #endif
+#ifndef ZR_EXP_EXTRA_VALU
+#define ZR_EXP_EXTRA_VALU 0  // experiment only: dummy VALU ops per lane-raster step
+#endif
 #ifndef ZR_TILE_PREFETCH
 #define ZR_TILE_PREFETCH 0   // request the next chunk's records before rasterizing this one
 #endif
@@ -47,6 +50,25 @@ __device__ __forceinline__ bool fetch_index(const DrawParams& P, uint64_t e, int
     const uint32_t ix = P.index_size == 2 ? (uint32_t)((const uint16_t*)P.ib)[e] : ((const uint32_t*)P.ib)[e];
     v = (int64_t)ix + (int64_t)P.vertex_offset;
     return true;
+}
+
+// Vertex ids of a primitive that k_setup_bin already validated (it won a pixel, so
+// its indices were in range): no bounds checks, 32-bit arithmetic (a valid id fits).
+__device__ __forceinline__ void winner_vids(const DrawParams& P, uint32_t prim, uint32_t v[3]) {
+    const uint32_t tri = (P.tris_per_instance == P.prims) ? prim : prim % P.tris_per_instance;
+    const uint32_t e0 = P.first + tri * 3u;
+    if (P.index_size == 4) {
+        const uint3 ix = *reinterpret_cast<const uint3*>(P.ib + (uint64_t)e0 * 4);
+        v[0] = ix.x; v[1] = ix.y; v[2] = ix.z;
+    } else if (P.index_size == 2) {
+        const uint16_t* ib = reinterpret_cast<const uint16_t*>(P.ib) + e0;
+        v[0] = ib[0]; v[1] = ib[1]; v[2] = ib[2];
+    } else {
+        v[0] = e0; v[1] = e0 + 1u; v[2] = e0 + 2u;
+        return;
+    }
+    const uint32_t off = (uint32_t)P.vertex_offset;  // two's complement: id + offset wraps to the valid id
+    v[0] += off; v[1] += off; v[2] += off;
 }
 
 __device__ __forceinline__ const float* attr_ptr(const DrawParams& P, uint32_t vid, uint32_t loc) {
@@ -124,10 +146,42 @@ __device__ __forceinline__ EdgeEval eval_edges(const TriRecord& r, int px, int p
     return e;
 }
 
-__device__ __forceinline__ float interp_depth(const TriRecord& r, long long w1, long long w2) {
-    const float b1 = (float)w1 * r.invA2, b2 = (float)w2 * r.invA2;
+__device__ __forceinline__ float interp_depth_f(const TriRecord& r, float fw1, float fw2) {
+    const float b1 = fw1 * r.invA2, b2 = fw2 * r.invA2;
     float z = fmaf(b2, r.dz2, fmaf(b1, r.dz1, r.z0));
     return z == 0.0f ? 0.0f : z;
+}
+
+__device__ __forceinline__ float interp_depth(const TriRecord& r, long long w1, long long w2) {
+    return interp_depth_f(r, (float)w1, (float)w2);
+}
+
+// Edge values at a pixel centre as floats (resolve: the winner's barycentrics).
+// A small primitive's values fit int32 exactly (bbox <= 64 px a side),
+// so (float)int32 equals (float)int64 there and the 64-bit products are skipped.
+struct EdgeEvalF {
+    float f0, f1, f2;
+};
+
+__device__ __forceinline__ EdgeEvalF eval_edges_f(const TriRecord& r, int px, int py) {
+    const int Sx = px * 256 + 128, Sy = py * 256 + 128;
+    EdgeEvalF e;
+    if (r.flags & kFlagSmall) {
+        // unsigned products: defined wraparound for the (discarded) fallback primitive
+        // of pixels no fragment won, which may lie far outside its bbox
+        auto ew = [](int ax, int ay, int bx, int by) {
+            return (float)(int)((uint32_t)ax * (uint32_t)ay - (uint32_t)bx * (uint32_t)by);
+        };
+        e.f0 = ew(r.X2 - r.X1, Sy - r.Y1, r.Y2 - r.Y1, Sx - r.X1);
+        e.f1 = ew(r.X0 - r.X2, Sy - r.Y2, r.Y0 - r.Y2, Sx - r.X2);
+        e.f2 = ew(r.X1 - r.X0, Sy - r.Y0, r.Y1 - r.Y0, Sx - r.X0);
+    } else {
+        const EdgeEval w = eval_edges(r, px, py);
+        e.f0 = (float)w.w0;
+        e.f1 = (float)w.w1;
+        e.f2 = (float)w.w2;
+    }
+    return e;
 }
 
 // ------------------------------------------------------------------ k_setup
@@ -247,19 +301,32 @@ __device__ __forceinline__ void setup_finish(const DrawParams& P, uint32_t prim,
                 owned += (uint32_t)(tx1 - tx0 + 1);
             }
             if (owned) {
-                TriRecord r;
-                r.X0 = X[0]; r.Y0 = Y[0]; r.X1 = X[1]; r.Y1 = Y[1]; r.X2 = X[2]; r.Y2 = Y[2];
-                r.z0 = z[0];
-                r.dz1 = z[1] - z[0];
-                r.dz2 = z[2] - z[0];
-                r.invA2 = 1.0f / (float)A2;
-                r.v0 = rv[0]; r.v1 = rv[1]; r.v2 = rv[2];
-                r.bb0 = (uint32_t)px0 | ((uint32_t)py0 << 16);
-                r.bb1 = (uint32_t)px1 | ((uint32_t)py1 << 16);
-                r.flags = flags;
-                P.records[prim] = r;
-                box.bb0 = r.bb0;
-                box.bb1 = r.bb1;
+                const float invA2 = 1.0f / (float)A2;
+                const bool small = (flags & kFlagSmall) != 0u;
+                TriCompact c;
+                c.X0 = X[0]; c.Y0 = Y[0];
+                c.dx1 = small ? (int16_t)(X[1] - X[0]) : kCompactLarge;
+                c.dy1 = small ? (int16_t)(Y[1] - Y[0]) : (int16_t)0;
+                c.dx2 = small ? (int16_t)(X[2] - X[0]) : (int16_t)0;
+                c.dy2 = small ? (int16_t)(Y[2] - Y[0]) : (int16_t)0;
+                c.z0 = z[0];
+                c.dz1 = z[1] - z[0];
+                c.dz2 = z[2] - z[0];
+                c.invA2s = (flags & kFlagSwapped) ? -invA2 : invA2;
+                P.records[prim] = c;
+                box.bb0 = (uint32_t)px0 | ((uint32_t)py0 << 16);
+                box.bb1 = (uint32_t)px1 | ((uint32_t)py1 << 16);
+                if (!small) {
+                    TriRecord r;
+                    r.X0 = X[0]; r.Y0 = Y[0]; r.X1 = X[1]; r.Y1 = Y[1]; r.X2 = X[2]; r.Y2 = Y[2];
+                    r.z0 = c.z0; r.dz1 = c.dz1; r.dz2 = c.dz2;
+                    r.invA2 = invA2;
+                    r.v0 = rv[0]; r.v1 = rv[1]; r.v2 = rv[2];
+                    r.bb0 = box.bb0;
+                    r.bb1 = box.bb1;
+                    r.flags = flags;
+                    P.records_big[prim] = r;
+                }
             }
         }
     }
@@ -495,14 +562,14 @@ __global__ __launch_bounds__(kSetupThreads) void k_setup_bin(DrawParams P) {
 // ------------------------------------------------------------------- k_tile
 
 template <int PROG>
-__device__ __forceinline__ void shade_winner(const DrawParams& P, const TriRecord& r, const EdgeEval& e, float out[4]) {
+__device__ __forceinline__ void shade_winner(const DrawParams& P, const TriRecord& r, const EdgeEvalF& e, float out[4]) {
     if (PROG == kProgFlat) {
         const float* c = attr_ptr(P, r.v0, 1);  // provoking vertex = first (flat)
         out[0] = c[0]; out[1] = c[1]; out[2] = c[2]; out[3] = 1.0f;
         return;
     }
     // perspective-correct weights b_i / w_i with w_i = 1 for every built-in vertex stage
-    const float pw0 = (float)e.w0 * r.invA2, pw1 = (float)e.w1 * r.invA2, pw2 = (float)e.w2 * r.invA2;
+    const float pw0 = e.f0 * r.invA2, pw1 = e.f1 * r.invA2, pw2 = e.f2 * r.invA2;
     const float inv = 1.0f / ((pw0 + pw1) + pw2);
     const float* a0 = attr_ptr(P, r.v0, 1);
     const float* a1 = attr_ptr(P, r.v1, 1);
@@ -564,6 +631,57 @@ __device__ __forceinline__ int rl(int v, uint32_t lane) { return __builtin_amdgc
 
 // Rasterize one primitive (wave-uniform record) into the tile's LDS keys: lanes
 // sweep the primitive's bbox ∩ tile, packed power-of-two rows per pass.
+// Expands a compact record (two 16-B words, TriCompact) into the TriRecord fields
+// the raster and resolve use: vertices, depth terms, |1/A2|, kFlagSmall/Swapped,
+// and with `full` also the top-left bias flags and the clipped pixel bbox, computed
+// exactly as k_setup_bin computed them.  v0..v2 are not part of the compact form.
+__device__ __forceinline__ TriRecord decode_compact(const DrawParams& P, const int4 q0, const int4 q1, bool full) {
+    TriRecord r;
+    r.X0 = q0.x; r.Y0 = q0.y;
+    r.X1 = q0.x + (int)(int16_t)(q0.z & 0xFFFF); r.Y1 = q0.y + (q0.z >> 16);
+    r.X2 = q0.x + (int)(int16_t)(q0.w & 0xFFFF); r.Y2 = q0.y + (q0.w >> 16);
+    r.z0 = __int_as_float(q1.x); r.dz1 = __int_as_float(q1.y); r.dz2 = __int_as_float(q1.z);
+    r.invA2 = fabsf(__int_as_float(q1.w));
+    uint32_t flags = kFlagSmall | ((q1.w < 0) ? kFlagSwapped : 0u);
+    r.v0 = r.v1 = r.v2 = 0u;
+    r.bb0 = r.bb1 = 0u;
+    if (full) {
+        const int X[3] = {r.X0, r.X1, r.X2}, Y[3] = {r.Y0, r.Y1, r.Y2};
+#pragma unroll
+        for (int i = 0; i < 3; ++i) {  // top-left rule (y-down), edge i opposite vertex i
+            const int a = (i + 1) % 3, b = (i + 2) % 3;
+            const int dx = X[b] - X[a], dy = Y[b] - Y[a];
+            if (!((dy < 0) || (dy == 0 && dx > 0))) flags |= (kFlagBias0 << i);
+        }
+        const int minX = min(X[0], min(X[1], X[2])), maxX = max(X[0], max(X[1], X[2]));
+        const int minY = min(Y[0], min(Y[1], Y[2])), maxY = max(Y[0], max(Y[1], Y[2]));
+        const int px0 = max((minX - 128 + 255) >> 8, P.clip_x0), px1 = min((maxX - 128) >> 8, P.clip_x1);
+        const int py0 = max((minY - 128 + 255) >> 8, P.clip_y0), py1 = min((maxY - 128) >> 8, P.clip_y1);
+        r.bb0 = (uint32_t)px0 | ((uint32_t)py0 << 16);
+        r.bb1 = (uint32_t)px1 | ((uint32_t)py1 << 16);
+    }
+    r.flags = flags;
+    return r;
+}
+
+// A wave-uniform full record, moved to scalar registers right after the load so
+// the wave path does not hold 16 more VGPRs.
+__device__ __forceinline__ TriRecord load_uniform_record(const TriRecord* p) {
+    const int4* q = reinterpret_cast<const int4*>(p);
+    int4 a = q[0], b = q[1], c = q[2], d = q[3];
+    auto u = [](int v) { return __builtin_amdgcn_readfirstlane(v); };
+    TriRecord r;
+    r.X0 = u(a.x); r.Y0 = u(a.y); r.X1 = u(a.z); r.Y1 = u(a.w);
+    r.X2 = u(b.x); r.Y2 = u(b.y);
+    r.z0 = __int_as_float(u(b.z)); r.dz1 = __int_as_float(u(b.w));
+    r.dz2 = __int_as_float(u(c.x)); r.invA2 = __int_as_float(u(c.y));
+    r.v0 = (uint32_t)u(c.z); r.v1 = (uint32_t)u(c.w); r.v2 = (uint32_t)u(d.x);
+    r.bb0 = (uint32_t)u(d.y); r.bb1 = (uint32_t)u(d.z); r.flags = (uint32_t)u(d.w);
+    return r;
+}
+
+__device__ __forceinline__ bool compact_is_large(const int4 q0) { return (int16_t)(q0.z & 0xFFFF) == kCompactLarge; }
+
 template <int MODE, bool INITD>
 __device__ __forceinline__ void raster_prim(const DrawParams& P, const TriRecord& r, uint32_t seq, int x0, int y0,
                                             int lane, unsigned long long* s_key, const float* s_initd) {
@@ -596,13 +714,11 @@ __device__ __forceinline__ void raster_prim(const DrawParams& P, const TriRecord
 // primitive's bbox ∩ tile in row order, stepping the three edge functions
 // incrementally in int32 (exact: |w| <= 2^29 inside a small primitive's bbox).
 template <int MODE, bool INITD>
-__device__ __forceinline__ void raster_lane(const DrawParams& P, const int4 q0, const int4 q1, const int4 q2,
-                                            const int4 q3, uint32_t seq, int x0, int y0,
+__device__ __forceinline__ void raster_lane(const DrawParams& P, const TriRecord& r, uint32_t seq, int x0, int y0,
                                             unsigned long long* s_key, const float* s_initd) {
-    const int X0 = q0.x, Y0 = q0.y, X1 = q0.z, Y1 = q0.w, X2 = q1.x, Y2 = q1.y;
-    const float z0 = __int_as_float(q1.z), dz1 = __int_as_float(q1.w);
-    const float dz2 = __int_as_float(q2.x), invA2 = __int_as_float(q2.y);
-    const uint32_t bb0 = (uint32_t)q3.y, bb1 = (uint32_t)q3.z, flags = (uint32_t)q3.w;
+    const int X0 = r.X0, Y0 = r.Y0, X1 = r.X1, Y1 = r.Y1, X2 = r.X2, Y2 = r.Y2;
+    const float z0 = r.z0, dz1 = r.dz1, dz2 = r.dz2, invA2 = r.invA2;
+    const uint32_t bb0 = r.bb0, bb1 = r.bb1, flags = r.flags;
     const int bx0 = max((int)(bb0 & 0xFFFFu), x0), by0 = max((int)(bb0 >> 16), y0);
     const int bx1 = min((int)(bb1 & 0xFFFFu), x0 + kTile - 1), by1 = min((int)(bb1 >> 16), y0 + kTile - 1);
     const int bw = bx1 - bx0 + 1, bh = by1 - by0 + 1;
@@ -635,6 +751,14 @@ __device__ __forceinline__ void raster_lane(const DrawParams& P, const int4 q0, 
                 atomicMin(reinterpret_cast<unsigned long long*>(reinterpret_cast<char*>(s_key) + la),
                           frag_key<MODE>(z, seq));
         }
+#if ZR_EXP_EXTRA_VALU
+        {  // experiment: extra dependent VALU work per pixel step (sensitivity probe)
+            float acc = (float)w0;
+#pragma unroll
+            for (int i = 0; i < ZR_EXP_EXTRA_VALU; ++i) acc = fmaf(acc, 1.0001f, 0.5f);
+            if (acc == 1234.5f) s_key[0] = 0;
+        }
+#endif
         const bool wrap = ++ex == bw;
         ex = wrap ? 0 : ex;
         w0 += wrap ? j0 : sx0;
@@ -741,7 +865,7 @@ __global__ __launch_bounds__(kTileThreads, ZR_TILE_WGS) void k_tile(DrawParams P
                 if (j < n) {
                     nprim = s_sorted[j];
                     const int4* rp = reinterpret_cast<const int4*>(P.records + nprim);
-                    n0 = rp[0]; n1 = rp[1]; n2 = rp[2]; n3 = rp[3];
+                    n0 = rp[0]; n1 = rp[1];  // 32-B compact record
                 }
             };
             if (ZR_TILE_PREFETCH) fetch(wave * 64u);
@@ -749,24 +873,22 @@ __global__ __launch_bounds__(kTileThreads, ZR_TILE_WGS) void k_tile(DrawParams P
                 if (!ZR_TILE_PREFETCH) fetch(cb);
                 const uint32_t j = cb + (uint32_t)lane;
                 const uint32_t my_prim = nprim;
-                const int4 q0 = n0, q1 = n1, q2 = n2, q3 = n3;
+                const int4 q0 = n0, q1 = n1;
                 if (ZR_TILE_PREFETCH) fetch(cb + kTileThreads);
                 const bool valid = j < n && !(P.debug & kDebugLoadOnly);
-                if (P.debug & kDebugLoadOnly) asm volatile("" ::"v"(q0.x), "v"(q1.x), "v"(q2.x), "v"(q3.x), "v"(my_prim));
-                const bool small = valid && (((uint32_t)q3.w & kFlagSmall) != 0u);
-                if (small) raster_lane<MODE, INITD>(P, q0, q1, q2, q3, my_prim + 1u, x0, y0, s_key, s_initd);
-                // large primitives: the whole wave sweeps one primitive at a time
-                unsigned long long big = __ballot(valid && !small);
+                if (P.debug & kDebugLoadOnly) asm volatile("" ::"v"(q0.x), "v"(q1.x), "v"(my_prim));
+                const bool large = compact_is_large(q0);
+                if (valid && !large) {
+                    const TriRecord r = decode_compact(P, q0, q1, true);
+                    raster_lane<MODE, INITD>(P, r, my_prim + 1u, x0, y0, s_key, s_initd);
+                }
+                // large primitives: the whole wave sweeps one primitive at a time (full record)
+                unsigned long long big = __ballot(valid && large);
                 while (big) {
                     const uint32_t i = (uint32_t)__builtin_ctzll(big);
                     big &= big - 1ull;
-                    TriRecord r;
-                    r.X0 = rl(q0.x, i); r.Y0 = rl(q0.y, i); r.X1 = rl(q0.z, i); r.Y1 = rl(q0.w, i);
-                    r.X2 = rl(q1.x, i); r.Y2 = rl(q1.y, i);
-                    r.z0 = __int_as_float(rl(q1.z, i)); r.dz1 = __int_as_float(rl(q1.w, i));
-                    r.dz2 = __int_as_float(rl(q2.x, i)); r.invA2 = __int_as_float(rl(q2.y, i));
-                    r.bb0 = (uint32_t)rl(q3.y, i); r.bb1 = (uint32_t)rl(q3.z, i); r.flags = (uint32_t)rl(q3.w, i);
                     const uint32_t prim = (uint32_t)rl((int)my_prim, i);
+                    const TriRecord r = load_uniform_record(P.records_big + prim);
                     raster_prim<MODE, INITD>(P, r, prim + 1u, x0, y0, lane, s_key, s_initd);
                 }
             }
@@ -794,10 +916,21 @@ __global__ __launch_bounds__(kTileThreads, ZR_TILE_WGS) void k_tile(DrawParams P
         col[k][0] = col[k][1] = col[k][2] = col[k][3] = 0.0f;
         zw[k] = 0.0f;
         if (cnt) {
-            const TriRecord r = P.records[prim];
-            const EdgeEval e = eval_edges(r, px, py);
+            const int4* cp = reinterpret_cast<const int4*>(P.records + prim);
+            const int4 c0 = cp[0], c1 = cp[1];
+            uint32_t vid[3];  // vertex ids are not in the compact record: refetch the indices
+            winner_vids(P, prim, vid);
+            TriRecord r = decode_compact(P, c0, c1, false);
+            if (__ballot(compact_is_large(c0))) {  // rare, wave-uniform: some winner is a large primitive
+                if (compact_is_large(c0)) r = P.records_big[prim];
+            }
+            const bool sw = (r.flags & kFlagSwapped) != 0u;
+            r.v0 = vid[0];
+            r.v1 = sw ? vid[2] : vid[1];
+            r.v2 = sw ? vid[1] : vid[2];
+            const EdgeEvalF e = eval_edges_f(r, px, py);
             if (P.color_bpp && !(P.debug & kDebugSkipShade)) shade_winner<PROG>(P, r, e, col[k]);
-            zw[k] = (MODE == kDepthLastWins) ? interp_depth(r, e.w1, e.w2) : key_depth<MODE>(key);
+            zw[k] = (MODE == kDepthLastWins) ? interp_depth_f(r, e.f1, e.f2) : key_depth<MODE>(key);
         }
     }
 #pragma unroll

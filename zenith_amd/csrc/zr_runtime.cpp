@@ -165,6 +165,26 @@ struct zr_fence_t {
     bool submitted = false;
 };
 
+struct ScratchSet {
+    TriCompact* records = nullptr;
+    uint64_t records_cap = 0;  // primitives
+    TriRecord* records_big = nullptr;
+    uint64_t records_big_cap = 0;
+    BBox* bboxes = nullptr;
+    uint64_t bboxes_cap = 0;
+    uint32_t* tile_counts = nullptr;
+    uint64_t tiles_cap = 0;
+    uint32_t* tile_offsets = nullptr;
+    uint64_t tiles_cap2 = 0;
+    uint32_t* counters = nullptr;
+    uint64_t counters_cap = 0;
+    uint32_t* bins = nullptr;
+    uint64_t bins_cap = 0;
+    hipEvent_t setup_done = nullptr;  // k_setup_bin of the last draw that used this set
+    hipEvent_t tile_done = nullptr;   // k_tile of the last draw that used this set
+    bool tile_done_valid = false;
+};
+
 struct TimedLaunch {
     const char* name;
     hipEvent_t start, stop;
@@ -173,23 +193,20 @@ struct TimedLaunch {
 struct zr_device_t {
     int hip_device = 0;
     hipStream_t stream = nullptr;
-    // scratch (grow-only)
-    TriRecord* records = nullptr;
-    uint64_t records_cap = 0;  // primitives
-    BBox* bboxes = nullptr;
-    uint64_t bboxes_cap = 0;
+    // Scratch (grow-only) in two sets: consecutive draws alternate, so the setup of
+    // draw i+1 (on setup_stream) only waits for the tile pass of draw i-1, the last
+    // reader of its set, and runs while the tile pass of draw i finishes.
+    ScratchSet sets[2];
+    uint32_t cur_set = 0;
+    hipStream_t setup_stream = nullptr;
+    // ZR_OVERLAP=1: overlap draws (measured slower on C2: the persistent setup's
+    // early workgroups hold CU slots at the grid barrier while the tile pass of the
+    // previous draw still needs them).  Default: one stream, set 0.
+    bool overlap = false;
     int cu_count = 0;
     uint32_t occupancy_checked_tiles = 0;
-    uint32_t* tile_counts = nullptr;
-    uint32_t* tile_offsets = nullptr;
-    uint64_t tiles_cap = 0;
-    uint64_t tiles_cap2 = 0;
-    uint32_t* counters = nullptr;
-    uint64_t counters_cap = 0;
     uint32_t setup_sched = 1;  // k_setup_bin unit schedule (ZR_SETUP_SCHED: 0 contiguous, 1 interleaved)
     uint32_t setup_batch = 2;  // k_setup_bin primitives per lane in flight (ZR_SETUP_BATCH: 1, 2, 4)
-    uint32_t* bins = nullptr;
-    uint64_t bins_cap = 0;
     uint32_t debug = 0;
     uint64_t initial_bins = 0;  // 0 = max(2^20, 2 * primitives of the first draw)
     unsigned long long* dbg_ts = nullptr;  // kDebugStamps
@@ -247,16 +264,23 @@ void collect_timings(zr_device* d) {
 }
 
 template <typename F>
-void timed_launch(zr_device* d, const char* name, F&& fn) {
+void timed_launch(zr_device* d, const char* name, hipStream_t stream, F&& fn) {
     if (!d->profiling) {
         fn();
         return;
     }
     TimedLaunch t{name, take_event(d), take_event(d)};
-    (void)hipEventRecord(t.start, d->stream);
+    (void)hipEventRecord(t.start, stream);
     fn();
-    (void)hipEventRecord(t.stop, d->stream);
+    (void)hipEventRecord(t.stop, stream);
     d->timed.push_back(t);
+}
+
+// Both streams idle (scratch may be freed, host-visible status is final).
+zr_result sync_streams(zr_device* d) {
+    ZR_HIP(hipStreamSynchronize(d->setup_stream));
+    ZR_HIP(hipStreamSynchronize(d->stream));
+    return ZR_SUCCESS;
 }
 
 template <typename T>
@@ -264,7 +288,8 @@ zr_result grow(zr_device* d, T*& ptr, uint64_t& cap, uint64_t need, uint64_t ele
     if (need <= cap && ptr) return ZR_SUCCESS;
     if (d->capturing) return ZR_NOT_READY;  // graph capture aborted: the caller runs eagerly
     d->scratch_gen++;
-    ZR_HIP(hipStreamSynchronize(d->stream));
+    zr_result rc = sync_streams(d);
+    if (rc) return rc;
     if (ptr) (void)hipFree(ptr);
     ptr = nullptr;
     uint64_t n = std::max<uint64_t>(need, 1024);
@@ -350,13 +375,13 @@ zr_result device_sync(zr_device* d) {
     zr_result rc = set_device(d);
     if (rc) return rc;
     for (int attempt = 0; attempt < 8; ++attempt) {
-        ZR_HIP(hipStreamSynchronize(d->stream));
+        if ((rc = sync_streams(d))) return rc;
         collect_timings(d);
         volatile uint32_t* st = d->status_host;
         d->last.bin_pairs = st[kStTotalPairs];
         d->last.triangles_setup = st[kStTrianglesSetup];
         d->last.triangles_dropped_clip = st[kStDroppedClip];
-        d->last.bin_capacity = d->bins_cap;
+        d->last.bin_capacity = std::min<uint64_t>(d->sets[0].bins_cap, d->sets[1].bins ? d->sets[1].bins_cap : ~0ull);
         d->last.replays = d->replays;
         if (st[kStBarrierTimeout]) {
             st[kStBarrierTimeout] = 0;
@@ -372,13 +397,16 @@ zr_result device_sync(zr_device* d) {
         // grow it and replay every submission since the last sync, in order.
         const uint64_t need = (uint64_t)st[kStMaxPairs] * 5 / 4 + 4096;
         st[kStOverflow] = 0;
-        ZR_HIP(hipFree(d->bins));
-        d->bins = nullptr;
+        for (ScratchSet& S : d->sets) {
+            if (!S.bins || S.bins_cap >= need) continue;
+            ZR_HIP(hipFree(S.bins));
+            S.bins = nullptr;
+            void* p = nullptr;
+            ZR_HIP(hipMalloc(&p, need * 4));
+            S.bins = (uint32_t*)p;
+            S.bins_cap = need;
+        }
         d->scratch_gen++;
-        void* p = nullptr;
-        ZR_HIP(hipMalloc(&p, need * 4));
-        d->bins = (uint32_t*)p;
-        d->bins_cap = need;
         d->replays++;
         std::vector<zr_cmd*> again;
         again.swap(d->pending);
@@ -468,32 +496,38 @@ zr_result fill_target(const ExecState& s, DrawParams& P) {
     return ZR_SUCCESS;
 }
 
-zr_result ensure_scratch(zr_device* d, DrawParams& P) {
+zr_result ensure_scratch(zr_device* d, ScratchSet& S, DrawParams& P) {
     zr_result rc;
     const uint64_t prims = std::max<uint64_t>(P.prims, 1);
-    if ((rc = grow(d, d->records, d->records_cap, prims, sizeof(TriRecord)))) return rc;
-    if ((rc = grow(d, d->bboxes, d->bboxes_cap, prims, sizeof(BBox)))) return rc;
+    if ((rc = grow(d, S.records, S.records_cap, prims, sizeof(TriCompact)))) return rc;
+    if ((rc = grow(d, S.records_big, S.records_big_cap, prims, sizeof(TriRecord)))) return rc;
+    if ((rc = grow(d, S.bboxes, S.bboxes_cap, prims, sizeof(BBox)))) return rc;
     {  // per-tile counters start at zero; k_setup_bin leaves them zero after every draw
-        const uint64_t cap = d->tiles_cap;
-        if ((rc = grow(d, d->tile_counts, d->tiles_cap, P.ntiles + 1, 4))) return rc;
-        if (d->tiles_cap != cap) ZR_HIP(hipMemset(d->tile_counts, 0, d->tiles_cap * 4));
+        const uint64_t cap = S.tiles_cap;
+        if ((rc = grow(d, S.tile_counts, S.tiles_cap, P.ntiles + 1, 4))) return rc;
+        if (S.tiles_cap != cap) ZR_HIP(hipMemset(S.tile_counts, 0, S.tiles_cap * 4));
     }
-    if ((rc = grow(d, d->tile_offsets, d->tiles_cap2, P.ntiles + 1, 4))) return rc;
-    if (!d->counters) {  // zeroed once; k_setup_bin leaves them zero after every draw
-        if ((rc = grow(d, d->counters, d->counters_cap, kCtWords, 4))) return rc;
-        ZR_HIP(hipMemset(d->counters, 0, d->counters_cap * 4));
+    if ((rc = grow(d, S.tile_offsets, S.tiles_cap2, P.ntiles + 1, 4))) return rc;
+    if (!S.counters) {  // zeroed once; k_setup_bin leaves them zero after every draw
+        if ((rc = grow(d, S.counters, S.counters_cap, kCtWords, 4))) return rc;
+        ZR_HIP(hipMemset(S.counters, 0, S.counters_cap * 4));
     }
-    if (!d->bins) {
+    if (!S.bins) {
         const uint64_t want = d->initial_bins ? d->initial_bins : std::max<uint64_t>(1u << 20, prims * 2);
-        if ((rc = grow(d, d->bins, d->bins_cap, want, 4))) return rc;
+        if ((rc = grow(d, S.bins, S.bins_cap, want, 4))) return rc;
     }
-    P.records = d->records;
-    P.bboxes = d->bboxes;
-    P.tile_counts = d->tile_counts;
-    P.tile_offsets = d->tile_offsets;
-    P.counters = d->counters;
-    P.bins = d->bins;
-    P.bin_capacity = (uint32_t)std::min<uint64_t>(d->bins_cap, 0xFFFFFFFFull);
+    if (!S.setup_done) {
+        ZR_HIP(hipEventCreateWithFlags(&S.setup_done, hipEventDisableTiming));
+        ZR_HIP(hipEventCreateWithFlags(&S.tile_done, hipEventDisableTiming));
+    }
+    P.records = S.records;
+    P.records_big = S.records_big;
+    P.bboxes = S.bboxes;
+    P.tile_counts = S.tile_counts;
+    P.tile_offsets = S.tile_offsets;
+    P.counters = S.counters;
+    P.bins = S.bins;
+    P.bin_capacity = (uint32_t)std::min<uint64_t>(S.bins_cap, 0xFFFFFFFFull);
     P.status = d->status_dev;
     return ZR_SUCCESS;
 }
@@ -612,17 +646,34 @@ zr_result exec_draw(zr_device* d, ExecState& s, const Cmd& c, bool indexed) {
         d->dbg_wgs = P.setup_wgs;
         d->dbg_tiles = P.ntiles;
     }
-    if ((rc = ensure_scratch(d, P))) return rc;
+    // Draws alternate between the two scratch sets when overlapping (not while
+    // debugging or with graph replay, whose captures bake in set 0: one stream).
+    const bool overlap = d->overlap && !d->debug && !d->use_graphs;
+    ScratchSet& S = d->sets[overlap ? d->cur_set : 0];
+    if (overlap) d->cur_set ^= 1u;
+    if ((rc = ensure_scratch(d, S, P))) return rc;
     d->last_prims = prims;
     d->last.triangles_in = prims;
 
+    const hipStream_t ss = overlap ? d->setup_stream : d->stream;
+    // setup may start once the previous reader of this scratch set (a k_tile two
+    // draws back) is done; it reads only vertex/index buffers besides the set
+    if (overlap && S.tile_done_valid) ZR_HIP(hipStreamWaitEvent(ss, S.tile_done, 0));
     // debug early exits skip the self-reset at the end of k_setup_bin
     if (d->debug) {
-        ZR_HIP(hipMemsetAsync(P.counters, 0, kCtWords * 4, d->stream));
-        ZR_HIP(hipMemsetAsync(P.tile_counts, 0, (size_t)P.ntiles * 4, d->stream));
+        ZR_HIP(hipMemsetAsync(P.counters, 0, kCtWords * 4, ss));
+        ZR_HIP(hipMemsetAsync(P.tile_counts, 0, (size_t)P.ntiles * 4, ss));
     }
-    timed_launch(d, "setup_bin", [&] { launch_setup_bin(P, d->stream); });
-    timed_launch(d, "tile", [&] { launch_tile(P, d->stream); });
+    timed_launch(d, "setup_bin", ss, [&] { launch_setup_bin(P, ss); });
+    if (overlap) {
+        ZR_HIP(hipEventRecord(S.setup_done, ss));
+        ZR_HIP(hipStreamWaitEvent(d->stream, S.setup_done, 0));
+    }
+    timed_launch(d, "tile", d->stream, [&] { launch_tile(P, d->stream); });
+    if (overlap) {
+        ZR_HIP(hipEventRecord(S.tile_done, d->stream));
+        S.tile_done_valid = true;
+    }
     ZR_HIP(hipGetLastError());
     s.color_clear_pending = false;
     s.depth_clear_pending = false;
@@ -635,7 +686,7 @@ zr_result exec_end_rendering(zr_device* d, ExecState& s) {
         memset(&P, 0, sizeof P);
         zr_result rc = fill_target(s, P);
         if (rc) return rc;
-        timed_launch(d, "clear", [&] { launch_clear(P, d->stream); });
+        timed_launch(d, "clear", d->stream, [&] { launch_clear(P, d->stream); });
         ZR_HIP(hipGetLastError());
     }
     s.rendering = false;
@@ -705,6 +756,7 @@ ZR_API zr_result zr_device_create(int32_t hip_device, zr_device** out) {
     if (const char* p = getenv("ZR_DEBUG_TS")) d->dbg_ts_path = p;
     if (const char* cap = getenv("ZR_BIN_CAPACITY")) d->initial_bins = std::max<uint64_t>(64, strtoull(cap, nullptr, 0));
     if (const char* g = getenv("ZR_GRAPH")) d->use_graphs = strtoul(g, nullptr, 0) != 0;
+    if (const char* o = getenv("ZR_OVERLAP")) d->overlap = strtoul(o, nullptr, 0) != 0;
     if (const char* sc = getenv("ZR_SETUP_SCHED")) d->setup_sched = std::min<uint32_t>(1, (uint32_t)strtoul(sc, nullptr, 0));
     if (const char* b = getenv("ZR_SETUP_BATCH")) {
         const unsigned long v = strtoul(b, nullptr, 0);
@@ -712,6 +764,7 @@ ZR_API zr_result zr_device_create(int32_t hip_device, zr_device** out) {
     }
     ZR_HIP(hipSetDevice(hip_device));
     ZR_HIP(hipStreamCreateWithFlags(&d->stream, hipStreamNonBlocking));
+    ZR_HIP(hipStreamCreateWithFlags(&d->setup_stream, hipStreamNonBlocking));
     ZR_HIP(hipDeviceGetAttribute(&d->cu_count, hipDeviceAttributeMultiprocessorCount, hip_device));
     void* st = nullptr;
     ZR_HIP(hipHostMalloc(&st, kStWords * 4, hipHostMallocMapped));
@@ -727,13 +780,20 @@ ZR_API zr_result zr_device_create(int32_t hip_device, zr_device** out) {
 ZR_API void zr_device_destroy(zr_device* d) {
     if (!d) return;
     (void)hipSetDevice(d->hip_device);
+    (void)hipStreamSynchronize(d->setup_stream);
     (void)hipStreamSynchronize(d->stream);
     collect_timings(d);
     for (hipEvent_t e : d->event_pool) (void)hipEventDestroy(e);
-    for (void* p : {(void*)d->dbg_ts, (void*)d->records, (void*)d->bboxes, (void*)d->tile_counts,
-                    (void*)d->tile_offsets, (void*)d->counters, (void*)d->bins})
-        if (p) (void)hipFree(p);
+    if (d->dbg_ts) (void)hipFree(d->dbg_ts);
+    for (ScratchSet& S : d->sets) {
+        for (void* p : {(void*)S.records, (void*)S.records_big, (void*)S.bboxes, (void*)S.tile_counts,
+                        (void*)S.tile_offsets, (void*)S.counters, (void*)S.bins})
+            if (p) (void)hipFree(p);
+        if (S.setup_done) (void)hipEventDestroy(S.setup_done);
+        if (S.tile_done) (void)hipEventDestroy(S.tile_done);
+    }
     (void)hipHostFree(d->status_host);
+    (void)hipStreamDestroy(d->setup_stream);
     (void)hipStreamDestroy(d->stream);
     delete d;
 }
