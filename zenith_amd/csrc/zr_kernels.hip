@@ -480,10 +480,16 @@ __global__ __launch_bounds__(kSetupThreads) void k_setup_bin(DrawParams P) {
     ZR_STAMP(1);
     if (P.debug & kDebugPhase1Only) return;
 
-    // ---- phase 2: reserve this workgroup's slots in every tile's list
-    for (uint32_t t = tid; t < nt; t += kSetupThreads) {
-        const uint32_t c = s_hist[t];
-        s_hist[t] = c ? __hip_atomic_fetch_add(&P.tile_counts[t], c, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) : 0u;
+    // ---- phase 2: reserve this workgroup's slots in every tile's list.  Each
+    // workgroup starts at a different 64-tile block so that the workgroups' adds
+    // spread over the counter lines instead of all queueing on the same ones.
+    {
+        const uint32_t rot = nt ? ((w * 64u) % nt) : 0u;
+        for (uint32_t i = tid; i < nt; i += kSetupThreads) {
+            const uint32_t t = i + rot < nt ? i + rot : i + rot - nt;
+            const uint32_t c = s_hist[t];
+            s_hist[t] = c ? __hip_atomic_fetch_add(&P.tile_counts[t], c, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) : 0u;
+        }
     }
     if (tid == 0) {
         if (s_misc[0]) atomicAdd(&P.counters[kCtSetup], s_misc[0]);
