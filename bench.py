@@ -28,7 +28,7 @@ from zenith_amd import renderer, rhi, scenes, shard, zr  # noqa: E402
 HBM_PEAK_GBPS = 8000.0           # MI355X_MICROARCH.md: HBM3E 8.0 TB/s spec
 HBM_MEASURED_GBPS = 6290.0       # same table: float4 copy achievable
 METRIC = BASELINE_METRIC = "Mtriangles/s + frames/s at 1080p (1M-tri scene), 1/2/4/8 GPU; HBM GB/s vs roofline"
-RECORD_BYTES = 64                # TriRecord (zr_internal.h)
+RECORD_BYTES = 32                # TriCompact, the per-primitive record k_tile reads per pair (zr_internal.h)
 BIN_ENTRY_BYTES = 4
 
 
@@ -48,7 +48,7 @@ def parse():
 def algorithmic_bytes(kernel, n_tris, b_in, pairs, pixels):
     """Per-launch algorithmic bytes of each pass.
 
-    setup_bin: read index+vertex data once (b_in per triangle), write one 64-B
+    setup_bin: read index+vertex data once (b_in per triangle), write one 32-B
                record per triangle and one 4-B bin entry per (tile, triangle) pair.
     tile:      read each pair's bin entry + record once, write the colour + depth
                texel of every owned pixel (4 + 4 B).

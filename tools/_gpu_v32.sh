@@ -1,0 +1,15 @@
+# round-1 deliverables for the current build: full parity, bench with CPU baseline,
+# kernel-trace stats, PMC FETCH/WRITE passes (+ counter calibration)
+set -o pipefail
+export TMPDIR=/tmp
+O=gpurun_out/v32
+mkdir -p $O
+timeout -k 10 700 python -m pytest tests -m gpu -x -q > $O/pytest.log 2>&1 || exit 1
+timeout -k 10 300 python bench.py > $O/bench.json 2> $O/bench.err || exit 2
+for c in c1 c3 c4; do timeout -k 10 200 python bench.py --config $c --no-cpu-baseline > $O/bench_$c.json 2>> $O/bench.err || exit 3; done
+timeout -k 10 200 rocprofv3 --kernel-trace --stats -d $O/kt -o run --output-format csv -- python3 bench.py --steps 50 --warmup 5 --no-cpu-baseline > $O/kt.log 2>&1 || exit 4
+timeout -k 10 200 rocprofv3 --pmc FETCH_SIZE -d $O/pf -o run --output-format csv -- python3 bench.py --steps 5 --warmup 2 --no-cpu-baseline > $O/pf.log 2>&1 || exit 5
+timeout -k 10 200 rocprofv3 --pmc WRITE_SIZE -d $O/pw -o run --output-format csv -- python3 bench.py --steps 5 --warmup 2 --no-cpu-baseline > $O/pw.log 2>&1 || exit 6
+timeout -k 10 120 rocprofv3 --pmc FETCH_SIZE -d $O/cf -o run --output-format csv -- tools/build/pmc_calib > $O/calib_known.txt 2>&1 || exit 7
+timeout -k 10 120 rocprofv3 --pmc WRITE_SIZE -d $O/cw -o run --output-format csv -- tools/build/pmc_calib > $O/calib_w.txt 2>&1 || exit 8
+echo done
