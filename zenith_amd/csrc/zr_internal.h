@@ -15,6 +15,8 @@ constexpr int kTileThreads = ZR_TILE_THREADS;  // k_tile workgroup: 4 waves of 6
 constexpr uint32_t kSortCap = 1024;     // tile-list segment sorted by area in LDS
 constexpr uint32_t kSortBuckets = 64;   // bbox-shape classes: 8 width classes x 8 height classes
 constexpr int kSetupThreads = 1024;  // setup / bin workgroups (one LDS histogram each)
+constexpr uint32_t kSetupLdsBudget = 160u * 1024u;     // one k_setup_bin workgroup per CU owns the LDS
+constexpr uint32_t kSetupBboxLdsBytes = 96u * 1024u;  // cap on the per-workgroup bbox array in LDS
 
 enum Program : int32_t { kProgTriangle = 0, kProgFlat = 1, kProgBlinn = 2, kProgCount = 3 };
 
@@ -158,6 +160,7 @@ struct DrawParams {
     uint32_t units;           // claim units of the draw: ceil(prims / unit size)
     uint32_t setup_batch;     // primitives per lane in flight (template instance of k_setup_bin)
     uint32_t setup_sched;     // unit schedule: 0 contiguous per workgroup, 1 interleaved (u % G)
+    uint32_t bbox_lds;        // 0: bboxes in global memory; else LDS entries per workgroup (own units * unit size)
     uint32_t debug;           // kDebug* bits (timing experiments only)
     unsigned long long* dbg_ts; // [setup_wgs][8] s_memrealtime stamps (kDebugStamps only)
     uint32_t* status;         // host-mapped
@@ -165,7 +168,7 @@ struct DrawParams {
 
 // Launchers (zr_kernels.hip).  All enqueue on `stream`; no host synchronisation.
 void launch_setup_bin(const DrawParams& p, void* stream);  // persistent: setup + scan + scatter
-size_t setup_bin_lds_bytes(uint32_t ntiles);
+size_t setup_bin_lds_bytes(uint32_t ntiles, uint32_t bbox_entries);
 const void* setup_bin_kernel(uint32_t batch);
 void launch_tile(const DrawParams& p, void* stream);
 void launch_clear(const DrawParams& p, void* stream);

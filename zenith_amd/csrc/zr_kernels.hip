@@ -237,6 +237,7 @@ __device__ __forceinline__ void fetch_positions(const DrawParams& P, PrimIn& in)
 }
 
 __device__ __forceinline__ void setup_finish(const DrawParams& P, uint32_t prim, const PrimIn& in, uint32_t* s_hist,
+                                             BBox* bbox_out,
                                              int& nvalid, int& ndropped) {
     if (prim >= P.prims) return;
     bool ok = in.ok;
@@ -330,7 +331,7 @@ __device__ __forceinline__ void setup_finish(const DrawParams& P, uint32_t prim,
             }
         }
     }
-    P.bboxes[prim] = box;
+    *bbox_out = box;
 }
 
 // ------------------------------------------------------------ grid barrier
@@ -341,8 +342,10 @@ __device__ __forceinline__ void setup_finish(const DrawParams& P, uint32_t prim,
 // the workgroup meets, lane 0 releases at agent scope, arrives with a relaxed
 // agent atomic, polls relaxed with s_sleep (bounded), then acquires at agent
 // scope before the workgroup reads other workgroups' data.
-__device__ __forceinline__ void grid_barrier(uint32_t* counter, uint32_t target, uint32_t* status) {
-    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // every storing wave drains its (sc1) stores
+__device__ __forceinline__ void grid_barrier(uint32_t* counter, uint32_t target, uint32_t* status, bool drain) {
+    // every storing wave drains its stores, unless nothing after the barrier reads
+    // what this workgroup stored before it (drain == false)
+    if (drain) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     __syncthreads();
     if (threadIdx.x == 0) {
         __hip_atomic_fetch_add(counter, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
@@ -443,11 +446,15 @@ __device__ __forceinline__ uint32_t own_unit(const DrawParams& P, uint32_t w, ui
 
 template <uint32_t KB>
 __global__ __launch_bounds__(kSetupThreads) void k_setup_bin(DrawParams P) {
-    extern __shared__ __attribute__((aligned(16))) uint32_t s_lds[];  // [2 * ntiles + 32]
+    extern __shared__ __attribute__((aligned(16))) uint32_t s_lds[];  // [2 * ntiles + 32] + bboxes
     const uint32_t nt = P.ntiles, G = gridDim.x, w = blockIdx.x, tid = threadIdx.x;
     uint32_t* s_hist = s_lds;            // histogram -> own offsets -> cursors
     uint32_t* s_base = s_lds + nt;       // tile totals -> tile bases
     uint32_t* s_misc = s_base + nt;      // [32]
+    // this workgroup's primitives' tile bboxes, indexed like phase 4's flattened
+    // (own unit, primitive in unit) space, when they fit (P.bbox_lds): then
+    // nothing read after the grid barrier depends on phase 1's global stores
+    BBox* s_bbox = reinterpret_cast<BBox*>(s_misc + 32);
     ZR_STAMP(0);
     for (uint32_t t = tid; t < nt; t += kSetupThreads) s_hist[t] = 0;
     if (tid < 32) s_misc[tid] = 0;
@@ -461,16 +468,21 @@ __global__ __launch_bounds__(kSetupThreads) void k_setup_bin(DrawParams P) {
         for (uint32_t i = 0;; ++i) {
             const uint32_t u = own_unit(P, w, G, wave + i * (kSetupThreads / 64u));
             if (u >= P.units) break;
+            const uint32_t jw = wave + i * (kSetupThreads / 64u);  // own-unit ordinal
             for (uint32_t r = 0; r < rounds; ++r) {
                 const uint32_t pb = (u << P.unit_shift) + r * 64u * KB + lane;
+                const uint32_t lb = (jw << P.unit_shift) + r * 64u * KB + lane;
                 PrimIn in[KB];
 #pragma unroll
                 for (uint32_t b = 0; b < KB; ++b) fetch_indices(P, min(pb + b * 64u, P.prims), in[b]);
 #pragma unroll
                 for (uint32_t b = 0; b < KB; ++b) fetch_positions(P, in[b]);
 #pragma unroll
-                for (uint32_t b = 0; b < KB; ++b)
-                    setup_finish(P, min(pb + b * 64u, P.prims), in[b], s_hist, nvalid, ndropped);
+                for (uint32_t b = 0; b < KB; ++b) {
+                    const uint32_t prim = min(pb + b * 64u, P.prims);
+                    BBox* out = P.bbox_lds ? &s_bbox[lb + b * 64u] : &P.bboxes[min(prim, P.prims - 1u)];
+                    setup_finish(P, prim, in[b], s_hist, out, nvalid, ndropped);
+                }
             }
         }
     }
@@ -496,7 +508,7 @@ __global__ __launch_bounds__(kSetupThreads) void k_setup_bin(DrawParams P) {
         if (s_misc[1]) atomicAdd(&P.counters[kCtDropped], s_misc[1]);
     }
     ZR_STAMP(2);
-    grid_barrier(&P.counters[kCtBarrier], G, P.status);
+    grid_barrier(&P.counters[kCtBarrier], G, P.status, !P.bbox_lds);
     ZR_STAMP(3);
     if (P.debug & kDebugStopAfterScan) return;
 
@@ -512,8 +524,6 @@ __global__ __launch_bounds__(kSetupThreads) void k_setup_bin(DrawParams P) {
             st[kStTotalPairs] = total;
             if (total > P.bin_capacity) st[kStOverflow] = 1u;
             if (total > st[kStMaxPairs]) st[kStMaxPairs] = total;
-            st[kStTrianglesSetup] = __hip_atomic_load(&P.counters[kCtSetup], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-            st[kStDroppedClip] = __hip_atomic_load(&P.counters[kCtDropped], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
         }
     }
     for (uint32_t t = tid; t < nt; t += kSetupThreads) s_hist[t] += s_base[t];
@@ -529,7 +539,7 @@ __global__ __launch_bounds__(kSetupThreads) void k_setup_bin(DrawParams P) {
         for (uint32_t j = tid; j < (nown << P.unit_shift); j += kSetupThreads) {
             const uint32_t prim = (own_unit(P, w, G, j >> P.unit_shift) << P.unit_shift) + (j & (usz - 1u));
             if (prim >= P.prims) continue;
-            const BBox bb = P.bboxes[prim];
+            const BBox bb = P.bbox_lds ? s_bbox[j] : P.bboxes[prim];
             if (bb.bb0 == kEmptyBox) continue;
             const int tx0 = (int)(bb.bb0 & 0xFFFFu) >> kTileShift, tx1 = (int)(bb.bb1 & 0xFFFFu) >> kTileShift;
             const int ty0 = (int)(bb.bb0 >> 16) >> kTileShift, ty1 = (int)(bb.bb1 >> 16) >> kTileShift;
@@ -556,6 +566,13 @@ __global__ __launch_bounds__(kSetupThreads) void k_setup_bin(DrawParams P) {
         const uint32_t prev = __hip_atomic_fetch_add(&P.counters[kCtExit], 1u, __ATOMIC_RELAXED,
                                                      __HIP_MEMORY_SCOPE_AGENT);
         s_misc[2] = prev == G - 1u ? 1u : 0u;
+        if (prev == G - 1u) {
+            // every workgroup's count adds were performed before its exit add (its
+            // wave 0 waited for the exit add's return, which follows them in order)
+            volatile uint32_t* st = P.status;
+            st[kStTrianglesSetup] = __hip_atomic_load(&P.counters[kCtSetup], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            st[kStDroppedClip] = __hip_atomic_load(&P.counters[kCtDropped], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        }
     }
     __syncthreads();
     if (s_misc[2]) {
@@ -979,7 +996,9 @@ __global__ __launch_bounds__(kTileThreads) void k_clear(DrawParams P) {
 
 static inline uint32_t blocks_for(uint32_t n, uint32_t per) { return (n + per - 1) / per; }
 
-size_t setup_bin_lds_bytes(uint32_t ntiles) { return (2 * (size_t)ntiles + 32) * sizeof(uint32_t); }
+size_t setup_bin_lds_bytes(uint32_t ntiles, uint32_t bbox_entries) {
+    return (2 * (size_t)ntiles + 32) * sizeof(uint32_t) + (size_t)bbox_entries * sizeof(BBox);
+}
 
 const void* setup_bin_kernel(uint32_t batch) {
     switch (batch) {
@@ -990,7 +1009,7 @@ const void* setup_bin_kernel(uint32_t batch) {
 }
 
 void launch_setup_bin(const DrawParams& p, void* stream) {
-    const size_t lds = setup_bin_lds_bytes(p.ntiles);
+    const size_t lds = setup_bin_lds_bytes(p.ntiles, p.bbox_lds);
     const hipStream_t s = (hipStream_t)stream;
     switch (p.setup_batch) {
     case 1: hipLaunchKernelGGL(k_setup_bin<1>, dim3(p.setup_wgs), dim3(kSetupThreads), lds, s, p); break;

@@ -623,7 +623,7 @@ zr_result exec_draw(zr_device* d, ExecState& s, const Cmd& c, bool indexed) {
     if (d->occupancy_checked_tiles != P.ntiles) {
         int nb = 0;
         ZR_HIP(hipOccupancyMaxActiveBlocksPerMultiprocessor(&nb, setup_bin_kernel(P.setup_batch), kSetupThreads,
-                                                            setup_bin_lds_bytes(P.ntiles)));
+                                                            setup_bin_lds_bytes(P.ntiles, 0)));
         if (nb < 1) return fail(ZR_ERROR_FEATURE_NOT_PRESENT, "k_setup_bin cannot be resident on a CU");
         d->occupancy_checked_tiles = P.ntiles;
     }
@@ -638,6 +638,12 @@ zr_result exec_draw(zr_device* d, ExecState& s, const Cmd& c, bool indexed) {
         while (((prims + (1ull << shift) - 1) >> shift) > 64ull * P.setup_wgs) ++shift;
         P.unit_shift = shift;
         P.units = (uint32_t)std::max<uint64_t>(1, (prims + (1ull << shift) - 1) >> shift);
+        // a workgroup's bboxes live in LDS when they fit beside the histograms
+        const uint64_t own_max = ((uint64_t)P.units + P.setup_wgs - 1) / P.setup_wgs;
+        const uint64_t entries = own_max << shift;
+        const uint64_t hist = setup_bin_lds_bytes(P.ntiles, 0);
+        const uint64_t budget = std::min<uint64_t>(kSetupBboxLdsBytes, hist < kSetupLdsBudget ? kSetupLdsBudget - hist : 0);
+        P.bbox_lds = (entries * sizeof(BBox) <= budget) ? (uint32_t)entries : 0u;
     }
     P.debug = d->debug;
     if (d->debug & kDebugStamps) {
@@ -765,6 +771,8 @@ ZR_API zr_result zr_device_create(int32_t hip_device, zr_device** out) {
     ZR_HIP(hipSetDevice(hip_device));
     ZR_HIP(hipStreamCreateWithFlags(&d->stream, hipStreamNonBlocking));
     ZR_HIP(hipStreamCreateWithFlags(&d->setup_stream, hipStreamNonBlocking));
+    for (uint32_t b : {1u, 2u, 4u})  // histograms + bbox array may exceed the 64 KB default
+        ZR_HIP(hipFuncSetAttribute(setup_bin_kernel(b), hipFuncAttributeMaxDynamicSharedMemorySize, (int)kSetupLdsBudget));
     ZR_HIP(hipDeviceGetAttribute(&d->cu_count, hipDeviceAttributeMultiprocessorCount, hip_device));
     void* st = nullptr;
     ZR_HIP(hipHostMalloc(&st, kStWords * 4, hipHostMallocMapped));
