@@ -791,6 +791,91 @@ __device__ __forceinline__ void raster_lane(const DrawParams& P, const TriRecord
     }
 }
 
+// Vertex ids of a winning primitive; IDX32: u32 index buffer (one 12-B load).
+template <bool IDX32>
+__device__ __forceinline__ void resolve_vids(const DrawParams& P, uint32_t prim, uint32_t v[3]) {
+    if (IDX32) {
+        const uint32_t tri = (P.tris_per_instance == P.prims) ? prim : prim % P.tris_per_instance;
+        const uint3 ix = *reinterpret_cast<const uint3*>(P.ib + (uint64_t)(P.first + tri * 3u) * 4);
+        const uint32_t off = (uint32_t)P.vertex_offset;
+        v[0] = ix.x + off; v[1] = ix.y + off; v[2] = ix.z + off;
+    } else {
+        winner_vids(P, prim, v);
+    }
+}
+
+// Resolve of one tile: per pixel the winning primitive is read from its key, its
+// compact record and vertex ids are gathered, its edges evaluated once and the
+// program shaded once (deferred shading); colour and depth are stored.  Two pixels
+// per batch: both pixels' record and index gathers are in flight together.
+template <int PROG, int MODE, bool IDX32>
+__device__ __forceinline__ void resolve_pixels(const DrawParams& P, int x0, int y0, uint32_t cnt, uint32_t fallback,
+                                               const unsigned long long* s_key, const float* s_srgb) {
+    constexpr int kPer = kTilePixels / kTileThreads;
+    constexpr int kB = 2;
+#pragma unroll 1
+    for (int k0 = 0; k0 < kPer; k0 += kB) {
+        int px[kB], py[kB];
+        bool have[kB], inside[kB];
+        unsigned long long key[kB];
+        uint32_t prim[kB], vid[kB][3];
+        int4 c0[kB], c1[kB];
+#pragma unroll
+        for (int b = 0; b < kB; ++b) {
+            const int i = threadIdx.x + (k0 + b) * kTileThreads;
+            px[b] = x0 + (i & (kTile - 1));
+            py[b] = y0 + (i >> kTileShift);
+            inside[b] = !(px[b] < P.ra_x0 || px[b] > P.ra_x1 || py[b] < P.ra_y0 || py[b] > P.ra_y1);
+            key[b] = s_key[i];
+            const uint32_t seq = inside[b] ? winner_seq<MODE>(key[b]) : 0u;
+            have[b] = seq != 0;
+            prim[b] = have[b] ? seq - 1u : fallback;
+        }
+        float col[kB][4];
+        float zw[kB];
+        if (cnt) {
+#pragma unroll
+            for (int b = 0; b < kB; ++b) {  // gathers of the batch
+                const int4* cp = reinterpret_cast<const int4*>(P.records + prim[b]);
+                c0[b] = cp[0];
+                c1[b] = cp[1];
+                resolve_vids<IDX32>(P, prim[b], vid[b]);
+            }
+#pragma unroll
+            for (int b = 0; b < kB; ++b) {
+                TriRecord r = decode_compact(P, c0[b], c1[b], false);
+                if (__ballot(compact_is_large(c0[b]))) {  // rare, wave-uniform: a winner is a large primitive
+                    if (compact_is_large(c0[b])) r = P.records_big[prim[b]];
+                }
+                const bool sw = (r.flags & kFlagSwapped) != 0u;
+                r.v0 = vid[b][0];
+                r.v1 = sw ? vid[b][2] : vid[b][1];
+                r.v2 = sw ? vid[b][1] : vid[b][2];
+                const EdgeEvalF e = eval_edges_f(r, px[b], py[b]);
+                col[b][0] = col[b][1] = col[b][2] = col[b][3] = 0.0f;
+                if (P.color_bpp && !(P.debug & kDebugSkipShade)) shade_winner<PROG>(P, r, e, col[b]);
+                zw[b] = (MODE == kDepthLastWins) ? interp_depth_f(r, e.f1, e.f2) : key_depth<MODE>(key[b]);
+            }
+        } else {
+#pragma unroll
+            for (int b = 0; b < kB; ++b) {
+                col[b][0] = col[b][1] = col[b][2] = col[b][3] = 0.0f;
+                zw[b] = 0.0f;
+            }
+        }
+#pragma unroll
+        for (int b = 0; b < kB; ++b) {
+            if (!inside[b]) continue;
+            if (P.color_bpp) store_color(P, px[b], py[b], have[b], col[b], s_srgb);
+            if (P.depth) {
+                float* dp = P.depth + (size_t)py[b] * P.fb_w + px[b];
+                if (have[b] && P.depth_write_out) *dp = zw[b];
+                else if (P.clear_depth_enable) *dp = P.clear_depth;
+            }
+        }
+    }
+}
+
 template <int PROG, int MODE, bool INITD>
 __global__ __launch_bounds__(kTileThreads, ZR_TILE_WGS) void k_tile(DrawParams P) {
     __shared__ unsigned long long s_key[kTilePixels];
@@ -921,53 +1006,13 @@ __global__ __launch_bounds__(kTileThreads, ZR_TILE_WGS) void k_tile(DrawParams P
     __syncthreads();
     if (stamp) ts[3] = __builtin_amdgcn_s_memrealtime();
 
-    // Resolve: four pixels per thread, loads of all four issued before any store.
-    constexpr int kPer = kTilePixels / kTileThreads;
+    // Resolve: four pixels per thread in two batches of two (the index width is a
+    // template parameter so the batch's gathers are issued back to back).
     const uint32_t fallback = cnt ? (P.bins[begin] & kBinPrimMask) : 0u;  // any binned primitive: loads in bounds
-    float col[kPer][4];
-    float zw[kPer];
-    bool have[kPer], inside[kPer];
-#pragma unroll
-    for (int k = 0; k < kPer; ++k) {
-        const int i = threadIdx.x + k * kTileThreads;
-        const int px = x0 + (i & (kTile - 1)), py = y0 + (i >> kTileShift);
-        inside[k] = !(px < P.ra_x0 || px > P.ra_x1 || py < P.ra_y0 || py > P.ra_y1);
-        const unsigned long long key = s_key[i];
-        const uint32_t seq = inside[k] ? winner_seq<MODE>(key) : 0u;
-        have[k] = seq != 0;
-        const uint32_t prim = have[k] ? seq - 1u : fallback;
-        col[k][0] = col[k][1] = col[k][2] = col[k][3] = 0.0f;
-        zw[k] = 0.0f;
-        if (cnt) {
-            const int4* cp = reinterpret_cast<const int4*>(P.records + prim);
-            const int4 c0 = cp[0], c1 = cp[1];
-            uint32_t vid[3];  // vertex ids are not in the compact record: refetch the indices
-            winner_vids(P, prim, vid);
-            TriRecord r = decode_compact(P, c0, c1, false);
-            if (__ballot(compact_is_large(c0))) {  // rare, wave-uniform: some winner is a large primitive
-                if (compact_is_large(c0)) r = P.records_big[prim];
-            }
-            const bool sw = (r.flags & kFlagSwapped) != 0u;
-            r.v0 = vid[0];
-            r.v1 = sw ? vid[2] : vid[1];
-            r.v2 = sw ? vid[1] : vid[2];
-            const EdgeEvalF e = eval_edges_f(r, px, py);
-            if (P.color_bpp && !(P.debug & kDebugSkipShade)) shade_winner<PROG>(P, r, e, col[k]);
-            zw[k] = (MODE == kDepthLastWins) ? interp_depth_f(r, e.f1, e.f2) : key_depth<MODE>(key);
-        }
-    }
-#pragma unroll
-    for (int k = 0; k < kPer; ++k) {
-        if (!inside[k]) continue;
-        const int i = threadIdx.x + k * kTileThreads;
-        const int px = x0 + (i & (kTile - 1)), py = y0 + (i >> kTileShift);
-        if (P.color_bpp) store_color(P, px, py, have[k], col[k], s_srgb);
-        if (P.depth) {
-            float* dp = P.depth + (size_t)py * P.fb_w + px;
-            if (have[k] && P.depth_write_out) *dp = zw[k];
-            else if (P.clear_depth_enable) *dp = P.clear_depth;
-        }
-    }
+    if (P.index_size == 4)
+        resolve_pixels<PROG, MODE, true>(P, x0, y0, cnt, fallback, s_key, s_srgb);
+    else
+        resolve_pixels<PROG, MODE, false>(P, x0, y0, cnt, fallback, s_key, s_srgb);
     if (stamp) {
         ts[4] = __builtin_amdgcn_s_memrealtime();
         uint32_t hw, xcc;
