@@ -40,6 +40,8 @@ def parse():
     p.add_argument("--config", default="c2", choices=sorted(scenes.CONFIGS))
     p.add_argument("--cpu-seconds", type=float, default=10.0, help="CPU baseline sample length")
     p.add_argument("--no-cpu-baseline", action="store_true")
+    p.add_argument("--emulate-shard", type=int, default=0, metavar="G",
+                   help="diagnostic (1 GPU): run only rank 0's share of a G-way tile-row shard, no gather")
     p.add_argument("--pmc", default=os.path.join(ROOT, "profiles", "r01_pmc_c2.json"),
                    help="rocprofv3 PMC summary for roofline.traffic (tools/pmc_summary.py)")
     return p.parse_args()
@@ -99,7 +101,10 @@ def main():
     color = rhi.Texture(dev, rhi.TextureDesc.new_color("frame.color", W, H, scene.color_format), color_t.data_ptr())
     depth = rhi.Texture(dev, rhi.TextureDesc.new_depth("frame.depth", W, H), depth_t.data_ptr())
     r = renderer.SceneRenderer(dev, scene)
-    enc = r.record(color, depth, shard=(rank, world) if world > 1 else None)
+    if a.emulate_shard and world > 1:
+        raise SystemExit("--emulate-shard is a 1-GPU diagnostic")
+    shard_g = a.emulate_shard if a.emulate_shard > 1 else world
+    enc = r.record(color, depth, shard=(rank, shard_g) if shard_g > 1 else None)
     gather = shard.TileRowGather(H, W * 4, rank, world, cuda) if world > 1 else None
 
     def step():
@@ -143,7 +148,7 @@ def main():
     kt = dev.kernel_times()
     stats = dev.last_draw_stats()
     pairs = stats["bin_pairs"]
-    pixels = int(shard.owned_rows(H, rank, world).numel()) * W
+    pixels = int(shard.owned_rows(H, rank, shard_g).numel()) * W
     b_in = scenes.config_bytes_per_triangle(a.config)
     kernels = {}
     for name, (ms, n) in kt.items():
@@ -182,6 +187,7 @@ def main():
                      "frac": round(achieved / HBM_PEAK_GBPS, 4), "traffic": traffic,
                      "peak_measured_copy": HBM_MEASURED_GBPS},
         "kernels": kernels,
+        **({"emulated_shard": f"rank 0 of {shard_g} (diagnostic, no gather)"} if a.emulate_shard > 1 else {}),
         "bin_pairs": pairs,
         "triangles_setup": stats["triangles_setup"],
     }

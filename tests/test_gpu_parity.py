@@ -124,6 +124,28 @@ def test_bin_overflow_replay(monkeypatch):
         dev.close()
 
 
+@pytest.mark.parametrize("nt", [256, 512])
+def test_tile_workgroup_sizes(monkeypatch, nt):
+    """k_tile at each workgroup size (4 or 8 waves per tile; the runtime picks by
+    tiles per CU, ZR_TILE_NT forces one): exact on every program, the wave path,
+    depth ops and a tile-row shard."""
+    monkeypatch.setenv("ZR_TILE_NT", str(nt))
+    dev = rhi.RenderDevice(0)
+    try:
+        for prog in (scenes.PROGRAM_TRIANGLE, scenes.PROGRAM_FLAT_COLOR, scenes.PROGRAM_BLINN_PHONG):
+            assert_parity(dev, scenes.soup_scene(60 + prog, 4000, 320, 240, 9.0, prog))
+        assert_parity(dev, scenes.soup_scene(63, 300, 512, 384, 150.0, scenes.PROGRAM_BLINN_PHONG))
+        for op, write in ((scenes.OP_LEQUAL, True), (scenes.OP_GREATER, True), (scenes.OP_LESS, False)):
+            s = scenes.soup_scene(64, 3000, 256, 192, 10.0, scenes.PROGRAM_FLAT_COLOR)
+            s.depth_op, s.depth_write = op, write
+            if op == scenes.OP_GREATER:
+                s.depth_clear = 0.0
+            assert_parity(dev, s)
+        assert_parity(dev, scenes.soup_scene(65, 3000, 320, 240, 10.0, scenes.PROGRAM_BLINN_PHONG), shard=(1, 3))
+    finally:
+        dev.close()
+
+
 @pytest.mark.parametrize("fmt", [zr.FORMAT_R8G8B8A8_UNORM, zr.FORMAT_B8G8R8A8_UNORM, zr.FORMAT_R8G8B8A8_SRGB,
                                  zr.FORMAT_R32G32B32A32_SFLOAT])
 def test_color_formats(device, fmt):

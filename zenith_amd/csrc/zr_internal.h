@@ -146,6 +146,7 @@ struct DrawParams {
     const float* time_ptr;    // Time.time uniform (device) or nullptr
     // tiling / sharding
     uint32_t tiles_x, tiles_y, shard_rank, shard_count, owned_rows, ntiles;
+    uint32_t tile_threads;    // k_tile workgroup size: 256 or 512 (tile_threads_for)
     // scratch (binning without contended global atomics)
     TriCompact* records;      // [prims] compact records (every binned primitive)
     TriRecord* records_big;   // [prims] full records, written for large primitives only
@@ -165,6 +166,16 @@ struct DrawParams {
     unsigned long long* dbg_ts; // [setup_wgs][8] s_memrealtime stamps (kDebugStamps only)
     uint32_t* status;         // host-mapped
 };
+
+// k_tile workgroup size for a pass of `ntiles` tiles on `cus` CUs: 4 waves per
+// tile while the pass has >= 6 tiles per CU, else 8 (tile-row shards: a tile's
+// primitives spread over more waves).  Measured on C2 shards (1 GPU, rank 0 of
+// G): G=4 tile pass 44 -> 39 us, G=8 40 -> 33 us; 16 waves per tile was slower
+// than 4 (61 / 43 us), so it is not built.
+inline uint32_t tile_threads_for(uint32_t ntiles, uint32_t cus) {
+    const uint32_t per_cu = ntiles / (cus ? cus : 1u);
+    return per_cu >= 6u ? (uint32_t)kTileThreads : 512u;
+}
 
 // Launchers (zr_kernels.hip).  All enqueue on `stream`; no host synchronisation.
 void launch_setup_bin(const DrawParams& p, void* stream);  // persistent: setup + scan + scatter

@@ -808,11 +808,11 @@ __device__ __forceinline__ void resolve_vids(const DrawParams& P, uint32_t prim,
 // compact record and vertex ids are gathered, its edges evaluated once and the
 // program shaded once (deferred shading); colour and depth are stored.  Two pixels
 // per batch: both pixels' record and index gathers are in flight together.
-template <int PROG, int MODE, bool IDX32>
+template <int PROG, int MODE, bool IDX32, int NT>
 __device__ __forceinline__ void resolve_pixels(const DrawParams& P, int x0, int y0, uint32_t cnt, uint32_t fallback,
                                                const unsigned long long* s_key, const float* s_srgb) {
-    constexpr int kPer = kTilePixels / kTileThreads;
-    constexpr int kB = 2;
+    constexpr int kPer = kTilePixels / NT;
+    constexpr int kB = kPer < 2 ? kPer : 2;
 #pragma unroll 1
     for (int k0 = 0; k0 < kPer; k0 += kB) {
         int px[kB], py[kB];
@@ -822,7 +822,7 @@ __device__ __forceinline__ void resolve_pixels(const DrawParams& P, int x0, int 
         int4 c0[kB], c1[kB];
 #pragma unroll
         for (int b = 0; b < kB; ++b) {
-            const int i = threadIdx.x + (k0 + b) * kTileThreads;
+            const int i = threadIdx.x + (k0 + b) * NT;
             px[b] = x0 + (i & (kTile - 1));
             py[b] = y0 + (i >> kTileShift);
             inside[b] = !(px[b] < P.ra_x0 || px[b] > P.ra_x1 || py[b] < P.ra_y0 || py[b] > P.ra_y1);
@@ -876,8 +876,11 @@ __device__ __forceinline__ void resolve_pixels(const DrawParams& P, int x0, int 
     }
 }
 
-template <int PROG, int MODE, bool INITD>
-__global__ __launch_bounds__(kTileThreads, ZR_TILE_WGS) void k_tile(DrawParams P) {
+// NT threads per tile: 256 when the pass has several tiles per CU, 512 when it
+// has few (tile-row shards, small attachments), so a tile's primitives spread
+// over more waves (P.tile_threads, tile_threads_for).
+template <int PROG, int MODE, bool INITD, int NT>
+__global__ __launch_bounds__(NT, ZR_TILE_WGS * kTileThreads / NT) void k_tile(DrawParams P) {
     __shared__ unsigned long long s_key[kTilePixels];
     __shared__ float s_initd[INITD ? kTilePixels : 1];
     __shared__ uint32_t s_sorted[kSortCap];
@@ -897,19 +900,19 @@ __global__ __launch_bounds__(kTileThreads, ZR_TILE_WGS) void k_tile(DrawParams P
     const uint32_t begin = P.tile_offsets[t], end = P.tile_offsets[t + 1];
     // entries past bin_capacity were never written (overflowed draw, replayed by the runtime)
     const uint32_t cnt = begin < P.bin_capacity ? min(end - begin, P.bin_capacity - begin) : 0u;
-    constexpr uint32_t kPerThread = kSortCap / kTileThreads;
+    constexpr uint32_t kPerThread = kSortCap / NT;
     uint32_t ent[kPerThread];
     auto load_segment = [&](uint32_t seg) {
         const uint32_t n = min(kSortCap, cnt - seg);
 #pragma unroll
         for (uint32_t k = 0; k < kPerThread; ++k) {
-            const uint32_t i = threadIdx.x + k * kTileThreads;
+            const uint32_t i = threadIdx.x + k * NT;
             ent[k] = i < n ? P.bins[begin + seg + i] : 0u;  // prim | area bucket (k_setup_bin phase 4)
         }
     };
     if (cnt && !(P.debug & kDebugSkipRaster)) load_segment(0);
 
-    for (int i = threadIdx.x; i < kTilePixels; i += kTileThreads) {
+    for (int i = threadIdx.x; i < kTilePixels; i += NT) {
         const int px = x0 + (i & (kTile - 1)), py = y0 + (i >> kTileShift);
         float d = P.clear_depth;
         if (P.load_depth && px < (int)P.fb_w && py < (int)P.fb_h) d = P.depth[(size_t)py * P.fb_w + px];
@@ -936,7 +939,7 @@ __global__ __launch_bounds__(kTileThreads, ZR_TILE_WGS) void k_tile(DrawParams P
             uint32_t pr[kPerThread], bk[kPerThread], sl[kPerThread];
 #pragma unroll
             for (uint32_t k = 0; k < kPerThread; ++k) {
-                const uint32_t i = threadIdx.x + k * kTileThreads;
+                const uint32_t i = threadIdx.x + k * NT;
                 pr[k] = bk[k] = sl[k] = 0u;
                 if (i < n) {
                     pr[k] = ent[k] & kBinPrimMask;
@@ -958,7 +961,7 @@ __global__ __launch_bounds__(kTileThreads, ZR_TILE_WGS) void k_tile(DrawParams P
             __syncthreads();
 #pragma unroll
             for (uint32_t k = 0; k < kPerThread; ++k) {
-                const uint32_t i = threadIdx.x + k * kTileThreads;
+                const uint32_t i = threadIdx.x + k * NT;
                 if (i < n) s_sorted[s_bucket[bk[k]] + sl[k]] = pr[k];
             }
             __syncthreads();
@@ -977,12 +980,12 @@ __global__ __launch_bounds__(kTileThreads, ZR_TILE_WGS) void k_tile(DrawParams P
                 }
             };
             if (ZR_TILE_PREFETCH) fetch(wave * 64u);
-            for (uint32_t cb = wave * 64u; cb < n; cb += kTileThreads) {
+            for (uint32_t cb = wave * 64u; cb < n; cb += NT) {
                 if (!ZR_TILE_PREFETCH) fetch(cb);
                 const uint32_t j = cb + (uint32_t)lane;
                 const uint32_t my_prim = nprim;
                 const int4 q0 = n0, q1 = n1;
-                if (ZR_TILE_PREFETCH) fetch(cb + kTileThreads);
+                if (ZR_TILE_PREFETCH) fetch(cb + NT);
                 const bool valid = j < n && !(P.debug & kDebugLoadOnly);
                 if (P.debug & kDebugLoadOnly) asm volatile("" ::"v"(q0.x), "v"(q1.x), "v"(my_prim));
                 const bool large = compact_is_large(q0);
@@ -1010,9 +1013,9 @@ __global__ __launch_bounds__(kTileThreads, ZR_TILE_WGS) void k_tile(DrawParams P
     // template parameter so the batch's gathers are issued back to back).
     const uint32_t fallback = cnt ? (P.bins[begin] & kBinPrimMask) : 0u;  // any binned primitive: loads in bounds
     if (P.index_size == 4)
-        resolve_pixels<PROG, MODE, true>(P, x0, y0, cnt, fallback, s_key, s_srgb);
+        resolve_pixels<PROG, MODE, true, NT>(P, x0, y0, cnt, fallback, s_key, s_srgb);
     else
-        resolve_pixels<PROG, MODE, false>(P, x0, y0, cnt, fallback, s_key, s_srgb);
+        resolve_pixels<PROG, MODE, false, NT>(P, x0, y0, cnt, fallback, s_key, s_srgb);
     if (stamp) {
         ts[4] = __builtin_amdgcn_s_memrealtime();
         uint32_t hw, xcc;
@@ -1063,12 +1066,20 @@ void launch_setup_bin(const DrawParams& p, void* stream) {
     }
 }
 
+template <int PROG, int MODE, int NT>
+static void launch_tile_pmt(const DrawParams& p, hipStream_t s, bool initd) {
+    if (initd)
+        hipLaunchKernelGGL((k_tile<PROG, MODE, true, NT>), dim3(p.ntiles), dim3(NT), 0, s, p);
+    else
+        hipLaunchKernelGGL((k_tile<PROG, MODE, false, NT>), dim3(p.ntiles), dim3(NT), 0, s, p);
+}
+
 template <int PROG, int MODE>
 static void launch_tile_pm(const DrawParams& p, hipStream_t s, bool initd) {
-    if (initd)
-        hipLaunchKernelGGL((k_tile<PROG, MODE, true>), dim3(p.ntiles), dim3(kTileThreads), 0, s, p);
-    else
-        hipLaunchKernelGGL((k_tile<PROG, MODE, false>), dim3(p.ntiles), dim3(kTileThreads), 0, s, p);
+    switch (p.tile_threads) {
+    case 512: launch_tile_pmt<PROG, MODE, 512>(p, s, initd); break;
+    default: launch_tile_pmt<PROG, MODE, kTileThreads>(p, s, initd); break;
+    }
 }
 
 template <int PROG>

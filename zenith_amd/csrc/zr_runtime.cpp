@@ -207,6 +207,7 @@ struct zr_device_t {
     uint32_t occupancy_checked_tiles = 0;
     uint32_t setup_sched = 1;  // k_setup_bin unit schedule (ZR_SETUP_SCHED: 0 contiguous, 1 interleaved)
     uint32_t setup_batch = 2;  // k_setup_bin primitives per lane in flight (ZR_SETUP_BATCH: 1, 2, 4)
+    uint32_t tile_threads = 0; // k_tile workgroup size override (ZR_TILE_NT: 256, 512; 0 = by tile count)
     uint32_t debug = 0;
     uint64_t initial_bins = 0;  // 0 = max(2^20, 2 * primitives of the first draw)
     unsigned long long* dbg_ts = nullptr;  // kDebugStamps
@@ -645,6 +646,7 @@ zr_result exec_draw(zr_device* d, ExecState& s, const Cmd& c, bool indexed) {
         const uint64_t budget = std::min<uint64_t>(kSetupBboxLdsBytes, hist < kSetupLdsBudget ? kSetupLdsBudget - hist : 0);
         P.bbox_lds = (entries * sizeof(BBox) <= budget) ? (uint32_t)entries : 0u;
     }
+    P.tile_threads = d->tile_threads ? d->tile_threads : tile_threads_for(P.ntiles, (uint32_t)std::max(d->cu_count, 1));
     P.debug = d->debug;
     if (d->debug & kDebugStamps) {
         if (!d->dbg_ts) ZR_HIP(hipMalloc((void**)&d->dbg_ts, (8192 + kMaxTilesPerPass) * 8 * sizeof(unsigned long long)));
@@ -764,6 +766,10 @@ ZR_API zr_result zr_device_create(int32_t hip_device, zr_device** out) {
     if (const char* g = getenv("ZR_GRAPH")) d->use_graphs = strtoul(g, nullptr, 0) != 0;
     if (const char* o = getenv("ZR_OVERLAP")) d->overlap = strtoul(o, nullptr, 0) != 0;
     if (const char* sc = getenv("ZR_SETUP_SCHED")) d->setup_sched = std::min<uint32_t>(1, (uint32_t)strtoul(sc, nullptr, 0));
+    if (const char* nt = getenv("ZR_TILE_NT")) {
+        const unsigned long v = strtoul(nt, nullptr, 0);
+        d->tile_threads = v >= 512 ? 512u : v ? 256u : 0u;
+    }
     if (const char* b = getenv("ZR_SETUP_BATCH")) {
         const unsigned long v = strtoul(b, nullptr, 0);
         d->setup_batch = v >= 4 ? 4u : (v >= 2 ? 2u : 1u);
