@@ -101,9 +101,15 @@ typedef struct zr_fence_t zr_fence;
  * (device.rs:93-171): one HIP device, one in-order stream (the graphics queue). */
 ZR_API zr_result zr_device_create(int32_t hip_device, zr_device **out);
 ZR_API void zr_device_destroy(zr_device *dev);
-/* RenderDevice::wait_idle analogue; also the point where a bin-capacity overflow
- * is detected and the pending submissions are replayed. */
+/* RenderDevice::wait_idle analogue; also the point where the stats of the last
+ * draw are read and a bin buffer that overflowed (those draws were rasterized
+ * exactly by the slow all-records scan) is grown for later draws. */
 ZR_API zr_result zr_device_wait_idle(zr_device *dev);
+/* Runs the device's work on the caller's HIP stream (e.g. the one a collective
+ * library orders its work on), NULL = the device's own stream again.  Waits for
+ * the device first.  No reference counterpart (the reference has one queue). */
+ZR_API zr_result zr_device_set_stream(zr_device *dev, void *hip_stream);
+ZR_API void *zr_device_stream(const zr_device *dev);
 /* Per-kernel HIP-event timing of every draw (off by default). */
 ZR_API zr_result zr_device_set_profiling(zr_device *dev, int32_t enable);
 /* Accumulated timings since the last reset: for each kernel name (setup_bin,
@@ -118,7 +124,7 @@ ZR_API int32_t zr_device_kernel_times(zr_device *dev, zr_kernel_time *out, int32
 /* Counters of the last completed draw (after a sync point). */
 typedef struct zr_draw_stats {
     uint64_t triangles_in, triangles_setup, triangles_dropped_clip;
-    uint64_t bin_pairs, bin_capacity, replays;
+    uint64_t bin_pairs, bin_capacity, overflowed_draws;
 } zr_draw_stats;
 ZR_API zr_result zr_device_last_draw_stats(zr_device *dev, zr_draw_stats *out);
 /* Last error message recorded on this thread (for logging; never NULL). */
@@ -318,6 +324,20 @@ ZR_API void zr_cmd_draw_indexed(zr_cmd *cmd, uint32_t index_count, uint32_t inst
 /* Multi-GPU extension (no reference counterpart): subsequent
  * render passes touch only screen-tile rows r with r % count == rank. */
 ZR_API void zr_cmd_set_tile_shard(zr_cmd *cmd, uint32_t rank, uint32_t count);
+/* Partitioned tile-row shards: as zr_cmd_set_tile_shard, but each
+ * draw's primitive setup is split across the ranks too.  Rank r routes only its
+ * 1/count of the primitives to the ranks owning the tile rows they touch; the
+ * routing lists are exchanged by `exchange`, an all-to-all the caller provides
+ * (RCCL, MPI, ...), called from zr_submit once per draw on every rank:
+ *   send: `count` blocks of bytes_per_rank, block d for rank d;
+ *   recv: the block each rank s addressed to this rank, at s * bytes_per_rank.
+ * It must be ordered after earlier work on hip_stream and before later work on
+ * it (enqueue on that stream, or synchronise), and return ZR_SUCCESS or an error
+ * that zr_submit then returns.  count <= 32. */
+typedef zr_result (*zr_exchange_fn)(void *user, void *hip_stream, const void *send, void *recv,
+                                    uint64_t bytes_per_rank);
+ZR_API void zr_cmd_set_tile_shard_exchange(zr_cmd *cmd, uint32_t rank, uint32_t count, zr_exchange_fn exchange,
+                                           void *user);
 
 /* -------------------------------------------------------------- submission */
 

@@ -9,7 +9,7 @@ import numpy as np
 import pytest
 
 from oracle import oracle
-from zenith_amd import renderer, rhi, scenes, zr
+from zenith_amd import renderer, rhi, scenes, shard, zr
 
 pytestmark = pytest.mark.gpu
 
@@ -110,16 +110,25 @@ def test_mixed_sizes(device):
     assert_parity(device, s)
 
 
-def test_bin_overflow_replay(monkeypatch):
-    """A bin buffer too small for the draw's (tile, primitive) pairs is detected,
-    grown and the submission replayed; the image is still exact."""
+def test_bin_overflow_spill(monkeypatch):
+    """A draw with more (tile, primitive) pairs than the bin buffer holds is
+    rasterized exactly by k_tile's all-records scan; the runtime then grows the
+    buffer, and the next draw reads tile lists again."""
     monkeypatch.setenv("ZR_BIN_CAPACITY", "1024")
     dev = rhi.RenderDevice(0)
     try:
         s = scenes.soup_scene(16, 3000, 640, 480, 40.0, scenes.PROGRAM_FLAT_COLOR)
         assert_parity(dev, s)
         st = dev.last_draw_stats()
-        assert st["replays"] >= 1 and st["bin_pairs"] > 1024 and st["bin_capacity"] >= st["bin_pairs"]
+        assert st["overflowed_draws"] == 1 and st["bin_pairs"] > 1024 and st["bin_capacity"] >= st["bin_pairs"]
+        assert_parity(dev, s)
+        assert dev.last_draw_stats()["overflowed_draws"] == 1
+    finally:
+        dev.close()
+    dev = rhi.RenderDevice(0)
+    try:  # the wave path (large primitives) while spilling
+        assert_parity(dev, scenes.soup_scene(17, 300, 512, 384, 150.0, scenes.PROGRAM_BLINN_PHONG))
+        assert dev.last_draw_stats()["overflowed_draws"] == 1
     finally:
         dev.close()
 
@@ -290,3 +299,101 @@ def test_resubmit_soup_graph_replay(resubmit_device):
     enc.destroy()
     color.destroy()
     depth.destroy()
+
+
+# ------------------------------------------- partitioned setup
+def render_partitioned(scene, world, **kw):
+    """All `world` ranks of a partitioned tile-row shard, emulated by threads on
+    one GPU (each with its own RenderDevice); returns each rank's (colour, depth)."""
+    import threading
+    group = shard.ThreadGroupExchange.Group(world, "cuda:0")
+    out = [None] * world
+
+    def run(r):
+        dev = rhi.RenderDevice(0)
+        try:
+            out[r] = renderer.render_scene(dev, scene, shard=(r, world, shard.ThreadGroupExchange(group, r)), **kw)
+            out[r] = out[r] + (dev.last_draw_stats(),)
+        except BaseException as e:  # noqa: BLE001 - reported below
+            out[r] = e
+            group.barrier.abort()
+        finally:
+            dev.close()
+
+    ts = [threading.Thread(target=run, args=(r,)) for r in range(world)]
+    for t in ts:
+        t.start()
+    for t in ts:
+        t.join(timeout=300)
+    for r in range(world):
+        if isinstance(out[r], BaseException):
+            raise out[r]
+    return out
+
+
+def assert_partitioned_parity(scene, world, **kw):
+    oc, od = oracle.render(scene, **kw)
+    for r, (gc, gd, st) in enumerate(render_partitioned(scene, world, **kw)):
+        rows = owned_rows(scene.height, 32, (r, world))
+        bad = np.argwhere(np.any(gc[rows] != oc[rows], axis=-1))
+        assert bad.size == 0, f"rank {r}/{world}: {len(bad)} pixels differ, first {bad[:5].tolist()}"
+        if scene.depth:
+            assert np.array_equal(gd[rows].view(np.uint32), od[rows].view(np.uint32)), f"rank {r}/{world} depth"
+
+
+@pytest.mark.parametrize("world", [1, 2, 3, 8])
+def test_partitioned_shards(world):
+    """Each rank sets up 1/G of the primitives and routes them (k_route) through
+    the exchange; every rank's rows equal the oracle frame.  20k primitives give
+    several route chunks per rank at G=2 and empty ranges at G=8."""
+    assert_partitioned_parity(scenes.soup_scene(70, 20000, 320, 240, 10.0, scenes.PROGRAM_BLINN_PHONG), world)
+
+
+def test_partitioned_paths():
+    """Wave path, mixed sizes, depth ops, instancing and u16 indices under the
+    partitioned setup."""
+    assert_partitioned_parity(scenes.soup_scene(71, 300, 512, 384, 150.0, scenes.PROGRAM_BLINN_PHONG), 3)
+    s = scenes.soup_scene(72, 3000, 200, 160, 14.0, scenes.PROGRAM_FLAT_COLOR)
+    s.depth_op = scenes.OP_LEQUAL
+    assert_partitioned_parity(s, 2)
+    s = scenes.soup_scene(73, 3000, 200, 160, 14.0, scenes.PROGRAM_FLAT_COLOR)
+    s.depth_op, s.depth_clear = scenes.OP_GREATER, 0.0
+    assert_partitioned_parity(s, 4)
+    assert_partitioned_parity(scenes.cube_scene(), 2)
+    assert_partitioned_parity(scenes.triangle_scene(time=1.25), 3)
+
+
+def test_partitioned_c2_full():
+    """C2 (1M triangles, 1920x1080) as 8 partitioned ranks: union = oracle frame."""
+    assert_partitioned_parity(scenes.config_scene("c2"), 8)
+
+
+def test_partitioned_overflow_spill(monkeypatch):
+    monkeypatch.setenv("ZR_BIN_CAPACITY", "256")
+    assert_partitioned_parity(scenes.soup_scene(74, 3000, 320, 240, 30.0, scenes.PROGRAM_FLAT_COLOR), 2)
+
+
+def test_partitioned_rccl_exchange():
+    """The RCCL exchange itself (torch.distributed "nccl", world size 1: the
+    all-to-all is a local copy through RCCL) ordered on torch's stream."""
+    import os
+    import socket
+    import torch
+    import torch.distributed as dist
+    with socket.socket() as so:
+        so.bind(("127.0.0.1", 0))
+        port = so.getsockname()[1]
+    dist.init_process_group("nccl", init_method=f"tcp://127.0.0.1:{port}", rank=0, world_size=1,
+                            device_id=torch.device("cuda", 0))
+    try:
+        dev = rhi.RenderDevice(0)
+        dev.set_stream(torch.cuda.current_stream().cuda_stream)
+        ex = shard.RcclExchange("cuda:0")
+        s = scenes.soup_scene(75, 5000, 256, 192, 10.0, scenes.PROGRAM_BLINN_PHONG)
+        gc, gd = renderer.render_scene(dev, s, shard=(0, 1, ex))
+        oc, od = oracle.render(s)
+        assert ex.calls == 1
+        assert np.array_equal(gc, oc) and np.array_equal(gd.view(np.uint32), od.view(np.uint32))
+        dev.close()
+    finally:
+        dist.destroy_process_group()

@@ -83,6 +83,18 @@ struct alignas(8) BBox {
 };
 constexpr uint32_t kMaxTilesPerPass = 16384;  // LDS histogram of the setup pass (64 KB)
 
+// Partitioned setup for tile-row shards.  Rank r routes the
+// primitives of its range [r * span, (r + 1) * span) in chunks of kRouteChunk
+// (one k_route workgroup each) to the ranks owning their tile rows.  Exchange
+// block for one destination = [chunks] u32 counts, then [chunks][kRouteChunk]
+// u32 primitive ids, each chunk's ids in primitive order.  After the all-to-all,
+// a receiver's blocks in source order, read chunk by chunk, list its primitives
+// in API order, so a block position is an order-preserving primitive sequence.
+constexpr uint32_t kRouteChunk = 4096;
+constexpr uint32_t kRouteChunkShift = 12;
+constexpr int kRouteThreads = 1024;  // 4 primitives per thread
+constexpr uint32_t kMaxShards = 32;  // destination masks are u32
+
 // Timing-experiment switches (ZR_DEBUG env var); never set in production runs.
 enum : uint32_t { kDebugSkipRaster = 1u, kDebugSkipShade = 2u, kDebugLoadOnly = 16u,
                   kDebugPhase1Only = 32u, kDebugStopAfterScan = 64u, kDebugStamps = 128u,
@@ -147,6 +159,15 @@ struct DrawParams {
     // tiling / sharding
     uint32_t tiles_x, tiles_y, shard_rank, shard_count, owned_rows, ntiles;
     uint32_t tile_threads;    // k_tile workgroup size: 256 or 512 (tile_threads_for)
+    // partitioned setup (list mode).  In list mode `prims` counts
+    // block positions (sources * list_span), most of them empty.
+    uint32_t draw_prims;      // primitives of the draw (instances * triangles per instance)
+    const uint32_t* list;     // received exchange blocks, or nullptr (setup over [0, prims))
+    uint32_t list_span;       // positions per source block: list_chunks * kRouteChunk
+    uint32_t list_chunks;
+    uint32_t list_block_words;// list_chunks * (kRouteChunk + 1)
+    uint32_t* route_out;      // k_route: this rank's send blocks ([shard_count][list_block_words])
+    uint32_t route_lo, route_hi; // k_route: this rank's primitive range
     // scratch (binning without contended global atomics)
     TriCompact* records;      // [prims] compact records (every binned primitive)
     TriRecord* records_big;   // [prims] full records, written for large primitives only
@@ -183,5 +204,6 @@ size_t setup_bin_lds_bytes(uint32_t ntiles, uint32_t bbox_entries);
 const void* setup_bin_kernel(uint32_t batch);
 void launch_tile(const DrawParams& p, void* stream);
 void launch_clear(const DrawParams& p, void* stream);
+void launch_route(const DrawParams& p, void* stream);     // partitioned setup: route own range
 
 }  // namespace zr

@@ -54,8 +54,31 @@ __device__ __forceinline__ bool fetch_index(const DrawParams& P, uint64_t e, int
 
 // Vertex ids of a primitive that k_setup_bin already validated (it won a pixel, so
 // its indices were in range): no bounds checks, 32-bit arithmetic (a valid id fits).
+// Triangle (within its instance) of draw primitive `gid` (instance-major order).
+__device__ __forceinline__ uint32_t tri_of(const DrawParams& P, uint32_t gid) {
+    return (P.tris_per_instance == P.draw_prims) ? gid : gid % P.tris_per_instance;
+}
+
+// List mode (partitioned setup, zr_internal.h): the draw primitive at block
+// position `pos`, and whether that position holds one (chunks are partly filled).
+__device__ __forceinline__ bool list_entry(const DrawParams& P, uint32_t pos, uint32_t& gid) {
+    const uint32_t s = pos / P.list_span, jj = pos - s * P.list_span;
+    const uint32_t* blk = P.list + (size_t)s * P.list_block_words;
+    const uint32_t n = blk[jj >> kRouteChunkShift];
+    gid = blk[P.list_chunks + jj];
+    return (jj & (kRouteChunk - 1u)) < n;
+}
+
+// Draw primitive of a setup record index: the index itself, or in list mode the
+// primitive its (valid) block position holds.
+__device__ __forceinline__ uint32_t prim_gid(const DrawParams& P, uint32_t pos) {
+    if (!P.list) return pos;
+    const uint32_t s = pos / P.list_span;
+    return P.list[(size_t)s * P.list_block_words + P.list_chunks + (pos - s * P.list_span)];
+}
+
 __device__ __forceinline__ void winner_vids(const DrawParams& P, uint32_t prim, uint32_t v[3]) {
-    const uint32_t tri = (P.tris_per_instance == P.prims) ? prim : prim % P.tris_per_instance;
+    const uint32_t tri = tri_of(P, prim_gid(P, prim));
     const uint32_t e0 = P.first + tri * 3u;
     if (P.index_size == 4) {
         const uint3 ix = *reinterpret_cast<const uint3*>(P.ib + (uint64_t)e0 * 4);
@@ -199,10 +222,8 @@ struct PrimIn {
     bool ok;
 };
 
-__device__ __forceinline__ void fetch_indices(const DrawParams& P, uint32_t prim, PrimIn& in) {
-    in.ok = prim < P.prims;
-    if (!in.ok) return;
-    const uint32_t tri = (P.tris_per_instance == P.prims) ? prim : prim % P.tris_per_instance;
+__device__ __forceinline__ void fetch_indices_gid(const DrawParams& P, uint32_t gid, PrimIn& in) {
+    const uint32_t tri = tri_of(P, gid);
     const uint64_t e0 = (uint64_t)P.first + (uint64_t)tri * 3u;
     bool ok = true;
     if (P.index_size == 4 && (e0 + 3) * 4 <= P.ib_bytes) {
@@ -223,6 +244,19 @@ __device__ __forceinline__ void fetch_indices(const DrawParams& P, uint32_t prim
     in.ok = ok;
 }
 
+// Record index `pos` of the setup pass: the draw primitive itself, or in list
+// mode the primitive its block position holds (none: in.ok = false).
+__device__ __forceinline__ void fetch_indices(const DrawParams& P, uint32_t pos, PrimIn& in) {
+    in.ok = pos < P.prims;
+    if (!in.ok) return;
+    uint32_t gid = pos;
+    if (P.list && !list_entry(P, pos, gid)) {
+        in.ok = false;
+        return;
+    }
+    fetch_indices_gid(P, gid, in);
+}
+
 __device__ __forceinline__ void fetch_positions(const DrawParams& P, PrimIn& in) {
     if (!in.ok) return;
     bool ok = true;
@@ -236,102 +270,185 @@ __device__ __forceinline__ void fetch_positions(const DrawParams& P, PrimIn& in)
     for (int k = 0; k < 3; ++k) in.p[k] = *reinterpret_cast<const float3*>(attr_ptr(P, in.vid[k], 0));  // 12-B loads
 }
 
+// Setup geometry of one primitive (vertex stage, viewport, snap, facing/cull,
+// orientation, top-left biases, clipped pixel bbox): false when the primitive
+// produces no sample (dropped, culled, degenerate or outside the clip rect).
+// k_route and k_setup_bin both call it, so a routed primitive's bbox is the one
+// its owner's setup computes.
+struct PrimGeom {
+    int32_t X[3], Y[3];
+    float z[3];
+    uint32_t rv[3];
+    uint32_t flags;
+    long long A2;
+    int32_t px0, py0, px1, py1;
+};
+
+__device__ __forceinline__ bool prim_geometry(const DrawParams& P, const PrimIn& in, PrimGeom& g, int& ndropped) {
+    if (!in.ok) return false;
+    g.rv[0] = in.vid[0]; g.rv[1] = in.vid[1]; g.rv[2] = in.vid[2];
+#pragma unroll
+    for (int k = 0; k < 3; ++k) {
+        const float x = in.p[k].x, y = in.p[k].y, zc = in.p[k].z, w = 1.0f;  // vsmain (triangle.slang:22)
+        if (!(w > 0.0f)) { ++ndropped; return false; }
+        const float xd = x / w, yd = y / w, zd = zc / w;
+        const float xf = fmaf(xd, P.hw, P.cx), yf = fmaf(yd, P.hh, P.cy);
+        if (!(fabsf(xf) < 4194304.0f && fabsf(yf) < 4194304.0f)) { ++ndropped; return false; }
+        g.X[k] = (int32_t)rintf(xf * 256.0f);
+        g.Y[k] = (int32_t)rintf(yf * 256.0f);
+        g.z[k] = fmaf(zd, P.dr, P.dmin) + 0.0f;  // -0 -> +0 (k_tile relies on it)
+    }
+    int32_t* X = g.X;
+    int32_t* Y = g.Y;
+    long long A2 = (long long)(X[1] - X[0]) * (Y[2] - Y[0]) - (long long)(X[2] - X[0]) * (Y[1] - Y[0]);
+    const bool ccw = A2 < 0;  // Vulkan: a = -A2/2 > 0 is counter-clockwise
+    const bool front = (P.front_face == 0) ? ccw : !ccw;
+    if (A2 == 0 || ((P.cull_mode & 1u) && front) || ((P.cull_mode & 2u) && !front)) return false;
+    uint32_t flags = 0;
+    if (A2 < 0) {
+        int32_t t = X[1]; X[1] = X[2]; X[2] = t;
+        t = Y[1]; Y[1] = Y[2]; Y[2] = t;
+        const float f = g.z[1]; g.z[1] = g.z[2]; g.z[2] = f;
+        const uint32_t u = g.rv[1]; g.rv[1] = g.rv[2]; g.rv[2] = u;
+        A2 = -A2;
+        flags |= kFlagSwapped;
+    }
+#pragma unroll
+    for (int i = 0; i < 3; ++i) {  // top-left rule (y-down), edge i opposite vertex i
+        const int a = (i + 1) % 3, b = (i + 2) % 3;
+        const int32_t dx = X[b] - X[a], dy = Y[b] - Y[a];
+        const bool tl = (dy < 0) || (dy == 0 && dx > 0);
+        if (!tl) flags |= (kFlagBias0 << i);
+    }
+    const int32_t minX = min(X[0], min(X[1], X[2])), maxX = max(X[0], max(X[1], X[2]));
+    const int32_t minY = min(Y[0], min(Y[1], Y[2])), maxY = max(Y[0], max(Y[1], Y[2]));
+    if (maxX - minX <= kSmallExtent && maxY - minY <= kSmallExtent) flags |= kFlagSmall;
+    g.px0 = max((minX - 128 + 255) >> 8, P.clip_x0);
+    g.px1 = min((maxX - 128) >> 8, P.clip_x1);
+    g.py0 = max((minY - 128 + 255) >> 8, P.clip_y0);
+    g.py1 = min((maxY - 128) >> 8, P.clip_y1);
+    g.flags = flags;
+    g.A2 = A2;
+    return g.px0 <= g.px1 && g.py0 <= g.py1;
+}
+
 __device__ __forceinline__ void setup_finish(const DrawParams& P, uint32_t prim, const PrimIn& in, uint32_t* s_hist,
                                              BBox* bbox_out,
                                              int& nvalid, int& ndropped) {
     if (prim >= P.prims) return;
-    bool ok = in.ok;
-    int32_t X[3], Y[3];
-    float z[3];
-    uint32_t rv[3] = {in.vid[0], in.vid[1], in.vid[2]};
     BBox box{kEmptyBox, 0u};
-    if (ok) {
-#pragma unroll
-        for (int k = 0; k < 3; ++k) {
-            const float x = in.p[k].x, y = in.p[k].y, zc = in.p[k].z, w = 1.0f;  // vsmain (triangle.slang:22)
-            if (!(w > 0.0f)) { ++ndropped; ok = false; break; }
-            const float xd = x / w, yd = y / w, zd = zc / w;
-            const float xf = fmaf(xd, P.hw, P.cx), yf = fmaf(yd, P.hh, P.cy);
-            if (!(fabsf(xf) < 4194304.0f && fabsf(yf) < 4194304.0f)) { ++ndropped; ok = false; break; }
-            X[k] = (int32_t)rintf(xf * 256.0f);
-            Y[k] = (int32_t)rintf(yf * 256.0f);
-            z[k] = fmaf(zd, P.dr, P.dmin) + 0.0f;  // -0 -> +0 (k_tile relies on it)
+    PrimGeom g;
+    if (prim_geometry(P, in, g, ndropped)) {
+        ++nvalid;
+        const int tx0 = g.px0 >> kTileShift, tx1 = g.px1 >> kTileShift;
+        const int ty0 = g.py0 >> kTileShift, ty1 = g.py1 >> kTileShift;
+        uint32_t owned = 0;
+        for (int ty = ty0; ty <= ty1; ++ty) {
+            if ((uint32_t)ty % P.shard_count != P.shard_rank) continue;
+            const uint32_t row = ((uint32_t)ty / P.shard_count) * P.tiles_x;
+            for (int tx = tx0; tx <= tx1; ++tx) atomicAdd(&s_hist[row + tx], 1u);
+            owned += (uint32_t)(tx1 - tx0 + 1);
         }
-    }
-    if (ok) {
-        long long A2 = (long long)(X[1] - X[0]) * (Y[2] - Y[0]) - (long long)(X[2] - X[0]) * (Y[1] - Y[0]);
-        const bool ccw = A2 < 0;  // Vulkan: a = -A2/2 > 0 is counter-clockwise
-        const bool front = (P.front_face == 0) ? ccw : !ccw;
-        ok = A2 != 0 && !((P.cull_mode & 1u) && front) && !((P.cull_mode & 2u) && !front);
-        uint32_t flags = 0;
-        if (ok && A2 < 0) {
-            int32_t t = X[1]; X[1] = X[2]; X[2] = t;
-            t = Y[1]; Y[1] = Y[2]; Y[2] = t;
-            float f = z[1]; z[1] = z[2]; z[2] = f;
-            const uint32_t u = rv[1]; rv[1] = rv[2]; rv[2] = u;
-            A2 = -A2;
-            flags |= kFlagSwapped;
-        }
-        int32_t px0 = 0, py0 = 0, px1 = -1, py1 = -1;
-        if (ok) {
-#pragma unroll
-            for (int i = 0; i < 3; ++i) {  // top-left rule (y-down), edge i opposite vertex i
-                const int a = (i + 1) % 3, b = (i + 2) % 3;
-                const int32_t dx = X[b] - X[a], dy = Y[b] - Y[a];
-                const bool tl = (dy < 0) || (dy == 0 && dx > 0);
-                if (!tl) flags |= (kFlagBias0 << i);
-            }
-            const int32_t minX = min(X[0], min(X[1], X[2])), maxX = max(X[0], max(X[1], X[2]));
-            const int32_t minY = min(Y[0], min(Y[1], Y[2])), maxY = max(Y[0], max(Y[1], Y[2]));
-            if (maxX - minX <= kSmallExtent && maxY - minY <= kSmallExtent) flags |= kFlagSmall;
-            px0 = max((minX - 128 + 255) >> 8, P.clip_x0);
-            px1 = min((maxX - 128) >> 8, P.clip_x1);
-            py0 = max((minY - 128 + 255) >> 8, P.clip_y0);
-            py1 = min((maxY - 128) >> 8, P.clip_y1);
-            ok = px0 <= px1 && py0 <= py1;
-        }
-        if (ok) {
-            ++nvalid;
-            const int tx0 = px0 >> kTileShift, tx1 = px1 >> kTileShift;
-            const int ty0 = py0 >> kTileShift, ty1 = py1 >> kTileShift;
-            uint32_t owned = 0;
-            for (int ty = ty0; ty <= ty1; ++ty) {
-                if ((uint32_t)ty % P.shard_count != P.shard_rank) continue;
-                const uint32_t row = ((uint32_t)ty / P.shard_count) * P.tiles_x;
-                for (int tx = tx0; tx <= tx1; ++tx) atomicAdd(&s_hist[row + tx], 1u);
-                owned += (uint32_t)(tx1 - tx0 + 1);
-            }
-            if (owned) {
-                const float invA2 = 1.0f / (float)A2;
-                const bool small = (flags & kFlagSmall) != 0u;
-                TriCompact c;
-                c.X0 = X[0]; c.Y0 = Y[0];
-                c.dx1 = small ? (int16_t)(X[1] - X[0]) : kCompactLarge;
-                c.dy1 = small ? (int16_t)(Y[1] - Y[0]) : (int16_t)0;
-                c.dx2 = small ? (int16_t)(X[2] - X[0]) : (int16_t)0;
-                c.dy2 = small ? (int16_t)(Y[2] - Y[0]) : (int16_t)0;
-                c.z0 = z[0];
-                c.dz1 = z[1] - z[0];
-                c.dz2 = z[2] - z[0];
-                c.invA2s = (flags & kFlagSwapped) ? -invA2 : invA2;
-                P.records[prim] = c;
-                box.bb0 = (uint32_t)px0 | ((uint32_t)py0 << 16);
-                box.bb1 = (uint32_t)px1 | ((uint32_t)py1 << 16);
-                if (!small) {
-                    TriRecord r;
-                    r.X0 = X[0]; r.Y0 = Y[0]; r.X1 = X[1]; r.Y1 = Y[1]; r.X2 = X[2]; r.Y2 = Y[2];
-                    r.z0 = c.z0; r.dz1 = c.dz1; r.dz2 = c.dz2;
-                    r.invA2 = invA2;
-                    r.v0 = rv[0]; r.v1 = rv[1]; r.v2 = rv[2];
-                    r.bb0 = box.bb0;
-                    r.bb1 = box.bb1;
-                    r.flags = flags;
-                    P.records_big[prim] = r;
-                }
+        if (owned) {
+            const int32_t* X = g.X;
+            const int32_t* Y = g.Y;
+            const float invA2 = 1.0f / (float)g.A2;
+            const bool small = (g.flags & kFlagSmall) != 0u;
+            TriCompact c;
+            c.X0 = X[0]; c.Y0 = Y[0];
+            c.dx1 = small ? (int16_t)(X[1] - X[0]) : kCompactLarge;
+            c.dy1 = small ? (int16_t)(Y[1] - Y[0]) : (int16_t)0;
+            c.dx2 = small ? (int16_t)(X[2] - X[0]) : (int16_t)0;
+            c.dy2 = small ? (int16_t)(Y[2] - Y[0]) : (int16_t)0;
+            c.z0 = g.z[0];
+            c.dz1 = g.z[1] - g.z[0];
+            c.dz2 = g.z[2] - g.z[0];
+            c.invA2s = (g.flags & kFlagSwapped) ? -invA2 : invA2;
+            P.records[prim] = c;
+            box.bb0 = (uint32_t)g.px0 | ((uint32_t)g.py0 << 16);
+            box.bb1 = (uint32_t)g.px1 | ((uint32_t)g.py1 << 16);
+            if (!small) {
+                TriRecord r;
+                r.X0 = X[0]; r.Y0 = Y[0]; r.X1 = X[1]; r.Y1 = Y[1]; r.X2 = X[2]; r.Y2 = Y[2];
+                r.z0 = c.z0; r.dz1 = c.dz1; r.dz2 = c.dz2;
+                r.invA2 = invA2;
+                r.v0 = g.rv[0]; r.v1 = g.rv[1]; r.v2 = g.rv[2];
+                r.bb0 = box.bb0;
+                r.bb1 = box.bb1;
+                r.flags = g.flags;
+                P.records_big[prim] = r;
             }
         }
     }
     *bbox_out = box;
+}
+
+// ----------------------------------------------------------------- k_route
+//
+// Partitioned setup, step 1 (tile-row shards): workgroup c routes
+// primitives [route_lo + c * kRouteChunk, ...) of this rank's range.  Each
+// thread runs the setup geometry of 4 consecutive primitives and derives the
+// set of ranks owning a tile row its bbox touches (ty % G == rank).  Per
+// destination the chunk's ids are compacted in primitive order (ballot ranks
+// within a wave, per-wave totals scanned in LDS) into that destination's
+// exchange block, and the chunk's count is stored in the block header.
+__global__ __launch_bounds__(kRouteThreads) void k_route(DrawParams P) {
+    __shared__ uint32_t s_tot[kRouteThreads / 64][kMaxShards];
+    const uint32_t G = P.shard_count, c = blockIdx.x, tid = threadIdx.x;
+    const uint32_t lane = tid & 63u, wave = tid >> 6;
+    const uint32_t p0 = P.route_lo + c * kRouteChunk + tid * 4u;
+    PrimIn in[4];
+#pragma unroll
+    for (int k = 0; k < 4; ++k) {
+        in[k].ok = p0 + k < P.route_hi;
+        if (in[k].ok) fetch_indices_gid(P, p0 + k, in[k]);
+    }
+#pragma unroll
+    for (int k = 0; k < 4; ++k) fetch_positions(P, in[k]);
+    uint32_t mask[4];
+    int ndropped = 0;
+#pragma unroll
+    for (int k = 0; k < 4; ++k) {
+        PrimGeom g;
+        mask[k] = 0u;
+        if (prim_geometry(P, in[k], g, ndropped)) {
+            const int ty0 = g.py0 >> kTileShift, ty1 = g.py1 >> kTileShift;
+            if ((uint32_t)(ty1 - ty0) + 1u >= G) {
+                mask[k] = G >= 32u ? 0xFFFFFFFFu : (1u << G) - 1u;
+            } else {
+                for (int ty = ty0; ty <= ty1; ++ty) mask[k] |= 1u << ((uint32_t)ty % G);
+            }
+        }
+    }
+    const unsigned long long below = (1ull << lane) - 1ull;
+    // per-wave totals of every destination
+    for (uint32_t d = 0; d < G; ++d) {
+        uint32_t n = 0;
+#pragma unroll
+        for (int k = 0; k < 4; ++k) n += (uint32_t)__popcll(__ballot((mask[k] >> d) & 1u));
+        if (lane == 0) s_tot[wave][d] = n;
+    }
+    __syncthreads();
+    if (tid < G) {  // exclusive scan over waves; the chunk's count into the header
+        uint32_t run = 0;
+        for (uint32_t w = 0; w < kRouteThreads / 64; ++w) {
+            const uint32_t n = s_tot[w][tid];
+            s_tot[w][tid] = run;
+            run += n;
+        }
+        P.route_out[(size_t)tid * P.list_block_words + c] = run;
+    }
+    __syncthreads();
+    for (uint32_t d = 0; d < G; ++d) {
+        uint32_t* ids = P.route_out + (size_t)d * P.list_block_words + P.list_chunks + (size_t)c * kRouteChunk;
+        uint32_t pos = s_tot[wave][d];  // thread-major order: lanes below hold earlier primitives
+#pragma unroll
+        for (int q = 0; q < 4; ++q) pos += (uint32_t)__popcll(__ballot((mask[q] >> d) & 1u) & below);
+#pragma unroll
+        for (int k = 0; k < 4; ++k) {
+            if ((mask[k] >> d) & 1u) ids[pos++] = p0 + (uint32_t)k;
+        }
+    }
 }
 
 // ------------------------------------------------------------ grid barrier
@@ -522,7 +639,7 @@ __global__ __launch_bounds__(kSetupThreads) void k_setup_bin(DrawParams P) {
             P.tile_offsets[nt] = total;
             volatile uint32_t* st = P.status;
             st[kStTotalPairs] = total;
-            if (total > P.bin_capacity) st[kStOverflow] = 1u;
+            if (total > P.bin_capacity) st[kStOverflow] += 1u;  // draws run in stream order
             if (total > st[kStMaxPairs]) st[kStMaxPairs] = total;
         }
     }
@@ -540,6 +657,8 @@ __global__ __launch_bounds__(kSetupThreads) void k_setup_bin(DrawParams P) {
             const uint32_t prim = (own_unit(P, w, G, j >> P.unit_shift) << P.unit_shift) + (j & (usz - 1u));
             if (prim >= P.prims) continue;
             const BBox bb = P.bbox_lds ? s_bbox[j] : P.bboxes[prim];
+            // overflowed draw: k_tile rasterizes by scanning every record's bbox
+            if (P.bbox_lds && total > P.bin_capacity) P.bboxes[prim] = bb;
             if (bb.bb0 == kEmptyBox) continue;
             const int tx0 = (int)(bb.bb0 & 0xFFFFu) >> kTileShift, tx1 = (int)(bb.bb1 & 0xFFFFu) >> kTileShift;
             const int ty0 = (int)(bb.bb0 >> 16) >> kTileShift, ty1 = (int)(bb.bb1 >> 16) >> kTileShift;
@@ -795,7 +914,7 @@ __device__ __forceinline__ void raster_lane(const DrawParams& P, const TriRecord
 template <bool IDX32>
 __device__ __forceinline__ void resolve_vids(const DrawParams& P, uint32_t prim, uint32_t v[3]) {
     if (IDX32) {
-        const uint32_t tri = (P.tris_per_instance == P.prims) ? prim : prim % P.tris_per_instance;
+        const uint32_t tri = tri_of(P, prim_gid(P, prim));
         const uint3 ix = *reinterpret_cast<const uint3*>(P.ib + (uint64_t)(P.first + tri * 3u) * 4);
         const uint32_t off = (uint32_t)P.vertex_offset;
         v[0] = ix.x + off; v[1] = ix.y + off; v[2] = ix.z + off;
@@ -886,6 +1005,7 @@ __global__ __launch_bounds__(NT, ZR_TILE_WGS * kTileThreads / NT) void k_tile(Dr
     __shared__ uint32_t s_sorted[kSortCap];
     __shared__ uint32_t s_bucket[kSortBuckets];
     __shared__ float s_srgb[256];
+    __shared__ uint32_t s_any;  // spill path: some primitive touching the tile (resolve's in-bounds fallback)
     const uint32_t t = (P.debug & kDebugReverseTiles) ? P.ntiles - 1u - blockIdx.x : blockIdx.x;
     const uint32_t oy = t / P.tiles_x, tx = t - oy * P.tiles_x;
     const uint32_t ty = oy * P.shard_count + P.shard_rank;
@@ -898,8 +1018,11 @@ __global__ __launch_bounds__(NT, ZR_TILE_WGS * kTileThreads / NT) void k_tile(Dr
     // before anything else: workgroups dispatched last would otherwise queue these
     // loads behind the record gathers of every tile that started earlier.
     const uint32_t begin = P.tile_offsets[t], end = P.tile_offsets[t + 1];
-    // entries past bin_capacity were never written (overflowed draw, replayed by the runtime)
-    const uint32_t cnt = begin < P.bin_capacity ? min(end - begin, P.bin_capacity - begin) : 0u;
+    // A draw with more pairs than the bin buffer holds (the runtime grows it for
+    // later draws) is rasterized exactly but slowly: every tile scans all records'
+    // bboxes (k_setup_bin stored them) instead of reading its list.
+    const bool spill = P.tile_offsets[P.ntiles] > P.bin_capacity;
+    const uint32_t cnt = spill ? 0u : end - begin;
     constexpr uint32_t kPerThread = kSortCap / NT;
     uint32_t ent[kPerThread];
     auto load_segment = [&](uint32_t seg) {
@@ -920,6 +1043,7 @@ __global__ __launch_bounds__(NT, ZR_TILE_WGS * kTileThreads / NT) void k_tile(Dr
         if (INITD) s_initd[i] = d;
     }
     if (threadIdx.x < 255) s_srgb[threadIdx.x] = c_srgbT[threadIdx.x];
+    if (threadIdx.x == 0) s_any = 0xFFFFFFFFu;
     __syncthreads();
 
     const uint32_t wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
@@ -1005,17 +1129,50 @@ __global__ __launch_bounds__(NT, ZR_TILE_WGS * kTileThreads / NT) void k_tile(Dr
             }
             __syncthreads();
         }
+        if (spill) {
+            for (uint32_t cb = wave * 64u; cb < P.prims; cb += NT) {
+                const uint32_t j = cb + (uint32_t)lane;
+                bool hit = false;
+                int4 q0 = make_int4(0, 0, 0, 0), q1 = q0;
+                if (j < P.prims) {
+                    const BBox bb = P.bboxes[j];
+                    hit = bb.bb0 != kEmptyBox && (int)(bb.bb0 & 0xFFFFu) < x0 + kTile && (int)(bb.bb1 & 0xFFFFu) >= x0 &&
+                          (int)(bb.bb0 >> 16) < y0 + kTile && (int)(bb.bb1 >> 16) >= y0;
+                }
+                if (hit) {
+                    const int4* rp = reinterpret_cast<const int4*>(P.records + j);
+                    q0 = rp[0];
+                    q1 = rp[1];
+                    s_any = j;
+                }
+                const bool large = compact_is_large(q0);
+                if (hit && !large) raster_lane<MODE, INITD>(P, decode_compact(P, q0, q1, true), j + 1u, x0, y0, s_key, s_initd);
+                unsigned long long big = __ballot(hit && large);
+                while (big) {
+                    const uint32_t i = (uint32_t)__builtin_ctzll(big);
+                    big &= big - 1ull;
+                    const uint32_t prim = (uint32_t)rl((int)j, i);
+                    raster_prim<MODE, INITD>(P, load_uniform_record(P.records_big + prim), prim + 1u, x0, y0, lane,
+                                             s_key, s_initd);
+                }
+            }
+        }
     }
     __syncthreads();
     if (stamp) ts[3] = __builtin_amdgcn_s_memrealtime();
 
     // Resolve: four pixels per thread in two batches of two (the index width is a
     // template parameter so the batch's gathers are issued back to back).
-    const uint32_t fallback = cnt ? (P.bins[begin] & kBinPrimMask) : 0u;  // any binned primitive: loads in bounds
+    uint32_t fallback = cnt ? (P.bins[begin] & kBinPrimMask) : 0u;  // any binned primitive: loads in bounds
+    uint32_t rcnt = cnt;
+    if (spill) {
+        rcnt = s_any != 0xFFFFFFFFu ? 1u : 0u;
+        fallback = rcnt ? s_any : 0u;
+    }
     if (P.index_size == 4)
-        resolve_pixels<PROG, MODE, true, NT>(P, x0, y0, cnt, fallback, s_key, s_srgb);
+        resolve_pixels<PROG, MODE, true, NT>(P, x0, y0, rcnt, fallback, s_key, s_srgb);
     else
-        resolve_pixels<PROG, MODE, false, NT>(P, x0, y0, cnt, fallback, s_key, s_srgb);
+        resolve_pixels<PROG, MODE, false, NT>(P, x0, y0, rcnt, fallback, s_key, s_srgb);
     if (stamp) {
         ts[4] = __builtin_amdgcn_s_memrealtime();
         uint32_t hw, xcc;
@@ -1102,6 +1259,10 @@ void launch_tile(const DrawParams& p, void* stream) {
     case kProgFlat: launch_tile_p<kProgFlat>(p, s, initd); break;
     default: launch_tile_p<kProgBlinn>(p, s, initd); break;
     }
+}
+
+void launch_route(const DrawParams& p, void* stream) {
+    hipLaunchKernelGGL(k_route, dim3(p.list_chunks), dim3(kRouteThreads), 0, (hipStream_t)stream, p);
 }
 
 void launch_clear(const DrawParams& p, void* stream) {

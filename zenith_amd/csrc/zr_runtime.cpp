@@ -140,6 +140,8 @@ struct Cmd {
     int32_t e = 0;
     zr_viewport vp{};
     zr_rect2d rect{};
+    zr_exchange_fn exchange = nullptr;  // C_SET_SHARD with a partitioned setup
+    void* exchange_user = nullptr;
 };
 
 struct zr_cmd_t {
@@ -148,6 +150,7 @@ struct zr_cmd_t {
     zr_result err = ZR_SUCCESS;
     std::string err_msg;
     bool in_rendering = false;
+    bool has_exchange = false;  // a partitioned shard: its collective is called per submit, never captured
     // Replay of an unchanged command list: its launches captured once into a HIP
     // graph (valid while the device's scratch generation is unchanged).
     hipGraphExec_t graph = nullptr;
@@ -180,6 +183,10 @@ struct ScratchSet {
     uint64_t counters_cap = 0;
     uint32_t* bins = nullptr;
     uint64_t bins_cap = 0;
+    uint32_t* xsend = nullptr;  // partitioned setup: exchange blocks (words)
+    uint64_t xsend_cap = 0;
+    uint32_t* xrecv = nullptr;
+    uint64_t xrecv_cap = 0;
     hipEvent_t setup_done = nullptr;  // k_setup_bin of the last draw that used this set
     hipEvent_t tile_done = nullptr;   // k_tile of the last draw that used this set
     bool tile_done_valid = false;
@@ -215,9 +222,10 @@ struct zr_device_t {
     std::string dbg_ts_path;
     uint32_t* status_host = nullptr;
     uint32_t* status_dev = nullptr;
-    // replay + stats
+    // command lists submitted since the last sync point (in flight) + stats
     std::vector<zr_cmd*> pending;
-    uint64_t replays = 0;
+    uint64_t overflowed_draws = 0;
+    hipStream_t own_stream = nullptr;  // `stream` unless zr_device_set_stream installed the caller's
     zr_draw_stats last{};
     uint64_t last_prims = 0;
     // profiling
@@ -375,27 +383,24 @@ void dump_stamps(zr_device* d) {
 zr_result device_sync(zr_device* d) {
     zr_result rc = set_device(d);
     if (rc) return rc;
-    for (int attempt = 0; attempt < 8; ++attempt) {
-        if ((rc = sync_streams(d))) return rc;
-        collect_timings(d);
-        volatile uint32_t* st = d->status_host;
-        d->last.bin_pairs = st[kStTotalPairs];
-        d->last.triangles_setup = st[kStTrianglesSetup];
-        d->last.triangles_dropped_clip = st[kStDroppedClip];
-        d->last.bin_capacity = std::min<uint64_t>(d->sets[0].bins_cap, d->sets[1].bins ? d->sets[1].bins_cap : ~0ull);
-        d->last.replays = d->replays;
-        if (st[kStBarrierTimeout]) {
-            st[kStBarrierTimeout] = 0;
-            d->pending.clear();
-            return fail(ZR_ERROR_DEVICE_LOST, "k_setup_bin grid barrier timed out (workgroups not co-resident)");
-        }
-        if (d->dbg_ts && !d->dbg_ts_path.empty()) dump_stamps(d);
-        if (!st[kStOverflow]) {
-            d->pending.clear();
-            return ZR_SUCCESS;
-        }
-        // A draw produced more (tile, primitive) pairs than the bin buffer holds:
-        // grow it and replay every submission since the last sync, in order.
+    if ((rc = sync_streams(d))) return rc;
+    collect_timings(d);
+    volatile uint32_t* st = d->status_host;
+    d->last.bin_pairs = st[kStTotalPairs];
+    d->last.triangles_setup = st[kStTrianglesSetup];
+    d->last.triangles_dropped_clip = st[kStDroppedClip];
+    d->overflowed_draws += st[kStOverflow];
+    d->last.overflowed_draws = d->overflowed_draws;
+    d->pending.clear();
+    if (st[kStBarrierTimeout]) {
+        st[kStBarrierTimeout] = 0;
+        return fail(ZR_ERROR_DEVICE_LOST, "k_setup_bin grid barrier timed out (workgroups not co-resident)");
+    }
+    if (d->dbg_ts && !d->dbg_ts_path.empty()) dump_stamps(d);
+    if (st[kStOverflow]) {
+        // Draws with more (tile, primitive) pairs than the bin buffer holds were
+        // rasterized exactly by k_tile's scan of all records (slow); size the
+        // buffer for the largest draw seen so later draws read tile lists again.
         const uint64_t need = (uint64_t)st[kStMaxPairs] * 5 / 4 + 4096;
         st[kStOverflow] = 0;
         for (ScratchSet& S : d->sets) {
@@ -408,16 +413,9 @@ zr_result device_sync(zr_device* d) {
             S.bins_cap = need;
         }
         d->scratch_gen++;
-        d->replays++;
-        std::vector<zr_cmd*> again;
-        again.swap(d->pending);
-        for (zr_cmd* c : again) {
-            rc = execute(d, c);
-            if (rc) return rc;
-            d->pending.push_back(c);
-        }
     }
-    return fail(ZR_ERROR_OUT_OF_DEVICE_MEMORY, "bin buffer overflow persisted after replays");
+    d->last.bin_capacity = std::min<uint64_t>(d->sets[0].bins_cap, d->sets[1].bins ? d->sets[1].bins_cap : ~0ull);
+    return ZR_SUCCESS;
 }
 
 // ------------------------------------------------------------ draw execution
@@ -441,6 +439,8 @@ struct ExecState {
     RenderingState rs;
     bool color_clear_pending = false, depth_clear_pending = false;
     uint32_t shard_rank = 0, shard_count = 1;
+    zr_exchange_fn exchange = nullptr;
+    void* exchange_user = nullptr;
 };
 
 int32_t choose_depth_mode(bool test, bool write, int32_t op) {
@@ -577,6 +577,25 @@ zr_result exec_draw(zr_device* d, ExecState& s, const Cmd& c, bool indexed) {
     }
     P.tris_per_instance = (uint32_t)tpi;
     P.prims = (uint32_t)prims;
+    P.draw_prims = (uint32_t)prims;
+    // Partitioned setup: this rank routes [lo, hi) of the draw's
+    // primitives; the setup pass then runs over the received blocks' positions.
+    const bool partitioned = s.exchange != nullptr;
+    uint64_t positions = prims;
+    if (partitioned) {
+        const uint64_t G = s.shard_count;
+        const uint64_t per_rank = (prims + G - 1) / G;
+        const uint64_t chunks = std::max<uint64_t>(1, (per_rank + kRouteChunk - 1) / kRouteChunk);
+        positions = G * chunks * kRouteChunk;
+        if (positions > kBinPrimMask)
+            return fail(ZR_ERROR_FEATURE_NOT_PRESENT, "partitioned draw: more than 2^26-1 block positions");
+        P.list_chunks = (uint32_t)chunks;
+        P.list_span = (uint32_t)(chunks * kRouteChunk);
+        P.list_block_words = (uint32_t)(chunks * (kRouteChunk + 1));
+        P.route_lo = (uint32_t)std::min<uint64_t>(prims, (uint64_t)s.shard_rank * P.list_span);
+        P.route_hi = (uint32_t)std::min<uint64_t>(prims, (uint64_t)P.route_lo + P.list_span);
+        P.prims = (uint32_t)positions;
+    }
     // viewport transform constants (Vulkan 1.3 §Controlling the Viewport)
     P.hw = s.vp.width * 0.5f;
     P.hh = s.vp.height * 0.5f;
@@ -633,12 +652,12 @@ zr_result exec_draw(zr_device* d, ExecState& s, const Cmd& c, bool indexed) {
         // 64 * batch * 2^k primitives, at most ~64 units per workgroup on average
         const uint64_t cus = (uint64_t)std::max(d->cu_count, 1);
         const uint64_t per_wg = (uint64_t)kSetupThreads * P.setup_batch;
-        P.setup_wgs = (uint32_t)std::max<uint64_t>(1, std::min<uint64_t>(cus, (prims + per_wg - 1) / per_wg));
+        P.setup_wgs = (uint32_t)std::max<uint64_t>(1, std::min<uint64_t>(cus, (positions + per_wg - 1) / per_wg));
         uint32_t shift = 6;
         while ((1u << shift) < 64u * P.setup_batch) ++shift;
-        while (((prims + (1ull << shift) - 1) >> shift) > 64ull * P.setup_wgs) ++shift;
+        while (((positions + (1ull << shift) - 1) >> shift) > 64ull * P.setup_wgs) ++shift;
         P.unit_shift = shift;
-        P.units = (uint32_t)std::max<uint64_t>(1, (prims + (1ull << shift) - 1) >> shift);
+        P.units = (uint32_t)std::max<uint64_t>(1, (positions + (1ull << shift) - 1) >> shift);
         // a workgroup's bboxes live in LDS when they fit beside the histograms
         const uint64_t own_max = ((uint64_t)P.units + P.setup_wgs - 1) / P.setup_wgs;
         const uint64_t entries = own_max << shift;
@@ -656,7 +675,7 @@ zr_result exec_draw(zr_device* d, ExecState& s, const Cmd& c, bool indexed) {
     }
     // Draws alternate between the two scratch sets when overlapping (not while
     // debugging or with graph replay, whose captures bake in set 0: one stream).
-    const bool overlap = d->overlap && !d->debug && !d->use_graphs;
+    const bool overlap = d->overlap && !d->debug && !d->use_graphs && !partitioned;
     ScratchSet& S = d->sets[overlap ? d->cur_set : 0];
     if (overlap) d->cur_set ^= 1u;
     if ((rc = ensure_scratch(d, S, P))) return rc;
@@ -667,6 +686,20 @@ zr_result exec_draw(zr_device* d, ExecState& s, const Cmd& c, bool indexed) {
     // setup may start once the previous reader of this scratch set (a k_tile two
     // draws back) is done; it reads only vertex/index buffers besides the set
     if (overlap && S.tile_done_valid) ZR_HIP(hipStreamWaitEvent(ss, S.tile_done, 0));
+    if (partitioned) {
+        const uint64_t words = (uint64_t)s.shard_count * P.list_block_words;
+        if ((rc = grow(d, S.xsend, S.xsend_cap, words, 4))) return rc;
+        if ((rc = grow(d, S.xrecv, S.xrecv_cap, words, 4))) return rc;
+        P.route_out = S.xsend;
+        timed_launch(d, "route", ss, [&] { launch_route(P, ss); });
+        ZR_HIP(hipGetLastError());
+        zr_result xr = ZR_SUCCESS;
+        timed_launch(d, "exchange", ss, [&] {
+            xr = s.exchange(s.exchange_user, (void*)ss, S.xsend, S.xrecv, (uint64_t)P.list_block_words * 4u);
+        });
+        if (xr != ZR_SUCCESS) return fail(xr, "tile-shard exchange callback failed: " + g_last_error);
+        P.list = S.xrecv;
+    }
     // debug early exits skip the self-reset at the end of k_setup_bin
     if (d->debug) {
         ZR_HIP(hipMemsetAsync(P.counters, 0, kCtWords * 4, ss));
@@ -723,7 +756,12 @@ zr_result execute(zr_device* d, zr_cmd* cmd) {
             break;
         case C_BIND_IB: s.ib = c.buffer; s.ib_offset = c.offset; s.index_type = c.e; break;
         case C_DRAW: rc = exec_draw(d, s, c, c.d != 0); break;
-        case C_SET_SHARD: s.shard_rank = c.a; s.shard_count = c.b; break;
+        case C_SET_SHARD:
+            s.shard_rank = c.a;
+            s.shard_count = c.b;
+            s.exchange = c.exchange;
+            s.exchange_user = c.exchange_user;
+            break;
         }
         if (rc) return rc;
     }
@@ -776,6 +814,7 @@ ZR_API zr_result zr_device_create(int32_t hip_device, zr_device** out) {
     }
     ZR_HIP(hipSetDevice(hip_device));
     ZR_HIP(hipStreamCreateWithFlags(&d->stream, hipStreamNonBlocking));
+    d->own_stream = d->stream;
     ZR_HIP(hipStreamCreateWithFlags(&d->setup_stream, hipStreamNonBlocking));
     for (uint32_t b : {1u, 2u, 4u})  // histograms + bbox array may exceed the 64 KB default
         ZR_HIP(hipFuncSetAttribute(setup_bin_kernel(b), hipFuncAttributeMaxDynamicSharedMemorySize, (int)kSetupLdsBudget));
@@ -801,16 +840,26 @@ ZR_API void zr_device_destroy(zr_device* d) {
     if (d->dbg_ts) (void)hipFree(d->dbg_ts);
     for (ScratchSet& S : d->sets) {
         for (void* p : {(void*)S.records, (void*)S.records_big, (void*)S.bboxes, (void*)S.tile_counts,
-                        (void*)S.tile_offsets, (void*)S.counters, (void*)S.bins})
+                        (void*)S.tile_offsets, (void*)S.counters, (void*)S.bins, (void*)S.xsend, (void*)S.xrecv})
             if (p) (void)hipFree(p);
         if (S.setup_done) (void)hipEventDestroy(S.setup_done);
         if (S.tile_done) (void)hipEventDestroy(S.tile_done);
     }
     (void)hipHostFree(d->status_host);
     (void)hipStreamDestroy(d->setup_stream);
-    (void)hipStreamDestroy(d->stream);
+    (void)hipStreamDestroy(d->own_stream);
     delete d;
 }
+
+ZR_API zr_result zr_device_set_stream(zr_device* d, void* hip_stream) {
+    if (!d) return fail(ZR_ERROR_VALIDATION_FAILED, "device is NULL");
+    zr_result rc = device_sync(d);
+    if (rc) return rc;
+    d->stream = hip_stream ? (hipStream_t)hip_stream : d->own_stream;
+    return ZR_SUCCESS;
+}
+
+ZR_API void* zr_device_stream(const zr_device* d) { return d ? (void*)d->stream : nullptr; }
 
 ZR_API zr_result zr_device_wait_idle(zr_device* d) {
     if (!d) return fail(ZR_ERROR_VALIDATION_FAILED, "device is NULL");
@@ -1205,6 +1254,7 @@ ZR_API zr_result zr_cmd_begin(zr_cmd* c) {
     c->in_rendering = false;
     c->drop_graph();
     c->eager_runs = 0;
+    c->has_exchange = false;
     return ZR_SUCCESS;
 }
 
@@ -1367,6 +1417,21 @@ ZR_API void zr_cmd_set_tile_shard(zr_cmd* c, uint32_t rank, uint32_t count) {
     c->cmds.push_back(k);
 }
 
+ZR_API void zr_cmd_set_tile_shard_exchange(zr_cmd* c, uint32_t rank, uint32_t count, zr_exchange_fn exchange,
+                                           void* user) {
+    if (!c) return;
+    if (count == 0 || rank >= count || count > kMaxShards) return latch(c, ZR_ERROR_VALIDATION_FAILED, "bad tile shard");
+    if (!exchange) return latch(c, ZR_ERROR_VALIDATION_FAILED, "tile shard exchange is NULL");
+    Cmd k;
+    k.type = C_SET_SHARD;
+    k.a = rank;
+    k.b = count;
+    k.exchange = exchange;
+    k.exchange_user = user;
+    c->cmds.push_back(k);
+    c->has_exchange = true;
+}
+
 // --------------------------------------------------------------- submission
 
 ZR_API zr_result zr_fence_create(zr_device* d, zr_fence** out) {
@@ -1395,7 +1460,7 @@ ZR_API void zr_fence_destroy(zr_fence* f) {
 // (sizing scratch); the second captures the same launches into a HIP graph, later
 // ones replay it (one launch per frame instead of one per kernel).
 static zr_result submit_graph_or_eager(zr_device* d, zr_cmd* c) {
-    const bool graphs = d->use_graphs && !d->profiling && !d->debug;
+    const bool graphs = d->use_graphs && !d->profiling && !d->debug && !c->has_exchange;
     if (!graphs || c->eager_runs == 0) {
         c->eager_runs++;
         return execute(d, c);
@@ -1437,7 +1502,7 @@ ZR_API zr_result zr_submit(zr_device* d, zr_cmd* c, zr_fence* f) {
     if (rc) return rc;
     rc = submit_graph_or_eager(d, c);
     if (rc) return rc;
-    d->pending.push_back(c);
+    if (std::find(d->pending.begin(), d->pending.end(), c) == d->pending.end()) d->pending.push_back(c);
     if (f) {
         ZR_HIP(hipEventRecord(f->ev, d->stream));
         f->submitted = true;

@@ -64,6 +64,16 @@ class RenderDevice:
         check(lib().zr_device_last_draw_stats(self.handle, C.byref(st)), "zr_device_last_draw_stats")
         return {f: getattr(st, f) for f, _ in st._fields_}
 
+    def set_stream(self, hip_stream: Optional[int]):
+        """Runs the device's work on the caller's HIP stream (e.g. torch's current
+        stream, so torch.distributed collectives order against it); None = own."""
+        check(lib().zr_device_set_stream(self.handle, C.c_void_p(hip_stream) if hip_stream else None),
+              "zr_device_set_stream")
+
+    @property
+    def stream(self) -> int:
+        return lib().zr_device_stream(self.handle) or 0
+
     def submit(self, encoder: "CommandEncoder", fence: Optional["Fence"] = None):
         check(lib().zr_submit(self.handle, encoder.handle, fence.handle if fence else None), "zr_submit")
 
@@ -498,9 +508,11 @@ class CommandEncoder:
         check(lib().zr_cmd_create(device.handle, C.byref(h)), "zr_cmd_create")
         self.handle = h
         self.device = device
+        self._keep = []
 
     def begin(self):
-        check(lib().zr_cmd_begin(self.handle), "zr_cmd_begin")
+        check(lib().zr_cmd_begin(self.handle), "zr_cmd_begin")  # waits for its in-flight submissions
+        self._keep = []
 
     def end(self):
         check(lib().zr_cmd_end(self.handle), "zr_cmd_end")
@@ -530,8 +542,16 @@ class CommandEncoder:
         lib().zr_cmd_draw_indexed(self.handle, index_count, instance_count, first_index, vertex_offset,
                                   first_instance)
 
-    def set_tile_shard(self, rank: int, count: int):
-        lib().zr_cmd_set_tile_shard(self.handle, rank, count)
+    def set_tile_shard(self, rank: int, count: int, exchange=None):
+        """Tile-row shard of the following render passes.  With ``exchange`` (a
+        :class:`zenith_amd.shard.Exchange`) primitive setup is partitioned across
+        the ranks too and routed through that all-to-all."""
+        if exchange is None:
+            lib().zr_cmd_set_tile_shard(self.handle, rank, count)
+        else:
+            cb = exchange.c_callback()
+            self._keep.append(cb)  # the callback must outlive every submission of this list
+            lib().zr_cmd_set_tile_shard_exchange(self.handle, rank, count, C.cast(cb, C.c_void_p), None)
 
     def destroy(self):
         lib().zr_cmd_destroy(self.handle)

@@ -46,3 +46,160 @@ class TileRowGather:
             torch.index_select(image, 0, self.rows[self.rank], out=self.send_buf)
             for req in dist.batch_isend_irecv([dist.P2POp(dist.isend, self.send_buf, 0)]):
                 req.wait()
+
+
+# ------------------------------------------------ partitioned setup exchange
+#
+# zr_cmd_set_tile_shard_exchange (include/zenith_raster.h): each
+# rank routes 1/G of a draw's primitives to the ranks owning the tile rows they
+# touch; the routing lists travel in one all-to-all per draw.  Block layout per
+# destination (zr_internal.h): [chunks] u32 counts, then [chunks][ROUTE_CHUNK]
+# u32 primitive ids, each chunk's ids in primitive order.
+
+ROUTE_CHUNK = 4096  # zr::kRouteChunk
+
+
+def route_geometry(n_prims: int, world: int):
+    """(chunks, span, block_words) of a G-way partitioned draw of n primitives."""
+    per_rank = -(-n_prims // world)
+    chunks = max(1, -(-per_rank // ROUTE_CHUNK))
+    return chunks, chunks * ROUTE_CHUNK, chunks * (ROUTE_CHUNK + 1)
+
+
+def route_blocks(row_lo, row_hi, rank: int, world: int) -> torch.Tensor:
+    """Host model of k_route for rank `rank`: row_lo/row_hi are each primitive's
+    first/last tile row (row_lo < 0: no sample).  Returns the send buffer,
+    [world][block_words] uint32 (as int64 for portability)."""
+    n = len(row_lo)
+    chunks, span, bw = route_geometry(n, world)
+    send = torch.zeros((world, bw), dtype=torch.int64)
+    lo, hi = min(n, rank * span), min(n, rank * span + span)
+    for c in range(chunks):
+        fill = [0] * world
+        for p in range(lo + c * ROUTE_CHUNK, min(hi, lo + (c + 1) * ROUTE_CHUNK)):
+            a, b = int(row_lo[p]), int(row_hi[p])
+            if a < 0:
+                continue
+            dests = range(world) if b - a + 1 >= world else sorted({t % world for t in range(a, b + 1)})
+            for d in dests:
+                send[d, chunks + c * ROUTE_CHUNK + fill[d]] = p
+                fill[d] += 1
+        for d in range(world):
+            send[d, c] = fill[d]
+    return send
+
+
+def received_primitives(recv: torch.Tensor, n_prims: int, world: int) -> list:
+    """Primitive ids a rank's received blocks hold, in block-position order
+    (= API order, the sequence the visibility keys use)."""
+    chunks, _, bw = route_geometry(n_prims, world)
+    recv = recv.reshape(world, bw)
+    out = []
+    for s in range(world):
+        for c in range(chunks):
+            k = int(recv[s, c])
+            out += recv[s, chunks + c * ROUTE_CHUNK: chunks + c * ROUTE_CHUNK + k].tolist()
+    return out
+
+
+class _DeviceBytes:
+    """A raw device pointer as a uint8 array (__cuda_array_interface__), so the
+    runtime's exchange blocks can be handed to torch without a copy."""
+
+    def __init__(self, ptr: int, nbytes: int):
+        self.__cuda_array_interface__ = {"shape": (nbytes,), "typestr": "|u1", "data": (ptr, False),
+                                         "version": 2, "strides": None}
+
+
+def device_bytes(ptr: int, nbytes: int, device) -> torch.Tensor:
+    return torch.as_tensor(_DeviceBytes(ptr, nbytes), device=device)
+
+
+class Exchange:
+    """An all-to-all the runtime calls once per partitioned draw (zr_exchange_fn).
+    Subclasses implement ``exchange(stream, send_ptr, recv_ptr, bytes_per_rank)``
+    and must order it on ``stream``."""
+
+    def __init__(self):
+        self._cb = None
+        self.calls = 0
+
+    def exchange(self, stream: int, send: int, recv: int, nbytes: int) -> None:
+        raise NotImplementedError
+
+    def c_callback(self):
+        if self._cb is None:
+            from . import zr
+
+            def call(user, stream, send, recv, nbytes):
+                try:
+                    self.exchange(stream or 0, send or 0, recv or 0, int(nbytes))
+                    self.calls += 1
+                    return zr.SUCCESS
+                except Exception as e:  # never unwind into the C runtime
+                    import traceback
+                    traceback.print_exc()
+                    self.error = e
+                    return zr.ERROR_UNKNOWN
+            self._cb = zr.EXCHANGE_FN(call)
+        return self._cb
+
+
+class RcclExchange(Exchange):
+    """The exchange over torch.distributed (RCCL over xGMI with the "nccl"
+    backend): one all_to_all_single per draw, ordered on the runtime's stream
+    without a host wait."""
+
+    def __init__(self, device, group=None):
+        super().__init__()
+        self.device = torch.device(device)
+        self.group = group
+        self.world = dist.get_world_size(group)
+        self._views = {}
+
+    def _view(self, ptr, nbytes):
+        key = (ptr, nbytes)
+        t = self._views.get(key)
+        if t is None:
+            t = self._views[key] = device_bytes(ptr, nbytes, self.device)
+        return t
+
+    def exchange(self, stream, send, recv, nbytes):
+        s = self._view(send, nbytes * self.world)
+        r = self._view(recv, nbytes * self.world)
+        cur = torch.cuda.current_stream(self.device)
+        if stream and stream != cur.cuda_stream:
+            with torch.cuda.stream(torch.cuda.ExternalStream(stream, device=self.device)):
+                dist.all_to_all_single(r, s, group=self.group)
+        else:
+            dist.all_to_all_single(r, s, group=self.group)
+
+
+class ThreadGroupExchange(Exchange):
+    """G ranks emulated by G threads of one process on one GPU (tests): each
+    rank's runtime calls its own instance from its submitting thread; the
+    instances meet at a barrier and copy blocks device-to-device."""
+
+    class Group:
+        def __init__(self, world: int, device):
+            import threading
+            self.world = world
+            self.device = torch.device(device)
+            self.barrier = threading.Barrier(world, timeout=120)
+            self.sends = [None] * world
+
+    def __init__(self, group: "ThreadGroupExchange.Group", rank: int):
+        super().__init__()
+        self.group, self.rank = group, rank
+
+    def exchange(self, stream, send, recv, nbytes):
+        g = self.group
+        torch.cuda.ExternalStream(stream, device=g.device).synchronize()  # k_route done
+        g.sends[self.rank] = send
+        g.barrier.wait()
+        r = device_bytes(recv, nbytes * g.world, g.device)
+        for s in range(g.world):
+            src = device_bytes(g.sends[s] + self.rank * nbytes, nbytes, g.device)
+            r[s * nbytes:(s + 1) * nbytes].copy_(src)
+        torch.cuda.synchronize(g.device)
+        g.barrier.wait()  # every rank copied before any send buffer is rewritten

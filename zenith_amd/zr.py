@@ -72,7 +72,7 @@ class zr_kernel_time(C.Structure):
 class zr_draw_stats(C.Structure):
     _fields_ = [("triangles_in", C.c_uint64), ("triangles_setup", C.c_uint64),
                 ("triangles_dropped_clip", C.c_uint64), ("bin_pairs", C.c_uint64),
-                ("bin_capacity", C.c_uint64), ("replays", C.c_uint64)]
+                ("bin_capacity", C.c_uint64), ("overflowed_draws", C.c_uint64)]
 
 
 class zr_buffer_desc(C.Structure):
@@ -158,6 +158,10 @@ class zr_rendering_info(C.Structure):
                 ("depth_attachment", C.POINTER(zr_rendering_attachment))]
 
 
+# zr_exchange_fn (include/zenith_raster.h): (user, hip_stream, send, recv, bytes_per_rank) -> zr_result
+EXCHANGE_FN = C.CFUNCTYPE(C.c_int32, C.c_void_p, C.c_void_p, C.c_void_p, C.c_void_p, C.c_uint64)
+
+
 # ------------------------------------------------------------------- loading
 _P = C.c_void_p
 _R = C.c_int32
@@ -206,6 +210,9 @@ _SIGS = {
     "zr_cmd_draw": (None, [_P, C.c_uint32, C.c_uint32, C.c_uint32, C.c_uint32]),
     "zr_cmd_draw_indexed": (None, [_P, C.c_uint32, C.c_uint32, C.c_uint32, C.c_int32, C.c_uint32]),
     "zr_cmd_set_tile_shard": (None, [_P, C.c_uint32, C.c_uint32]),
+    "zr_cmd_set_tile_shard_exchange": (None, [_P, C.c_uint32, C.c_uint32, _P, _P]),
+    "zr_device_set_stream": (_R, [_P, _P]),
+    "zr_device_stream": (_P, [_P]),
     "zr_fence_create": (_R, [_P, C.POINTER(_P)]),
     "zr_fence_destroy": (None, [_P]),
     "zr_submit": (_R, [_P, _P, _P]),
