@@ -41,22 +41,34 @@ def parse():
     p.add_argument("--cpu-seconds", type=float, default=10.0, help="CPU baseline sample length")
     p.add_argument("--no-cpu-baseline", action="store_true")
     p.add_argument("--emulate-shard", type=int, default=0, metavar="G",
-                   help="diagnostic (1 GPU): run only rank 0's share of a G-way tile-row shard, no gather")
+                   help="diagnostic (1 GPU): run only rank 0's share of a G-way tile-row shard, no gather "
+                        "(partitioned setup: rank 0's routed block stands in for every source's)")
+    p.add_argument("--setup", choices=["partitioned", "replicated"], default="partitioned",
+                   help="tile-row shards: route 1/G of the primitives per rank through an RCCL all-to-all "
+                        "(DESIGN.md §7), or set up every primitive on every rank")
+    p.add_argument("--force-dist", action="store_true",
+                   help="run the multi-GPU code path (RCCL process group, exchange, gather) even at 1 GPU")
     p.add_argument("--pmc", default=os.path.join(ROOT, "profiles", "r01_pmc_c2.json"),
                    help="rocprofv3 PMC summary for roofline.traffic (tools/pmc_summary.py)")
     return p.parse_args()
 
 
-def algorithmic_bytes(kernel, n_tris, b_in, pairs, pixels):
+def algorithmic_bytes(kernel, n_tris, b_in, pairs, pixels, n_route=0):
     """Per-launch algorithmic bytes of each pass.
 
     setup_bin: read index+vertex data once (b_in per triangle), write one 32-B
                record per triangle and one 4-B bin entry per (tile, triangle) pair.
+               With a partitioned setup n_tris is the rank's received triangles
+               (+ their 4-B ids).
+    route:     (partitioned setup) read indices + positions of the rank's range
+               (12 + 3 * 12 B per triangle).
     tile:      read each pair's bin entry + record once, write the colour + depth
                texel of every owned pixel (4 + 4 B).
     """
     if kernel == "setup_bin":
-        return n_tris * (b_in + RECORD_BYTES) + pairs * BIN_ENTRY_BYTES
+        return n_tris * (b_in + RECORD_BYTES + (4 if n_route else 0)) + pairs * BIN_ENTRY_BYTES
+    if kernel == "route":
+        return n_route * 48
     if kernel == "tile":
         return pairs * (BIN_ENTRY_BYTES + RECORD_BYTES) + pixels * 8
     return 0
@@ -80,6 +92,22 @@ def cpu_baseline(scene, seconds, max_frames=500):
                       f"after 1 warm-up; {dt:.2f} s wall on {threads} threads"}
 
 
+class MirrorExchange(shard.Exchange):
+    """--emulate-shard diagnostic (1 GPU, partitioned setup): rank 0's own routed
+    block stands in for every source's, so the per-rank list-mode setup and tile
+    pass see a workload of the real size (duplicate primitives, not the real frame)."""
+
+    def __init__(self, device, world):
+        super().__init__()
+        self.device, self.world = device, world
+
+    def exchange(self, stream, send, recv, nbytes):
+        with torch.cuda.stream(torch.cuda.ExternalStream(stream, device=self.device)):
+            src = shard.device_bytes(send, nbytes, self.device)
+            dst = shard.device_bytes(recv, nbytes * self.world, self.device).view(self.world, nbytes)
+            dst.copy_(src.unsqueeze(0).expand(self.world, nbytes))
+
+
 def main():
     a = parse()
     world = int(os.environ.get("WORLD_SIZE", "1"))
@@ -89,7 +117,11 @@ def main():
         raise SystemExit(f"--gpus {a.gpus} but WORLD_SIZE={world}: launch N>1 with torch.distributed.run")
     torch.cuda.set_device(local)
     cuda = torch.device("cuda", local)
-    if world > 1:
+    distributed = world > 1 or a.force_dist
+    if distributed:
+        if "MASTER_ADDR" not in os.environ:  # --force-dist without a launcher
+            os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=os.environ.get("MASTER_PORT", "29533"),
+                              RANK="0", WORLD_SIZE="1")
         dist.init_process_group("nccl", device_id=cuda)
 
     scene = scenes.config_scene(a.config)
@@ -101,23 +133,35 @@ def main():
     color = rhi.Texture(dev, rhi.TextureDesc.new_color("frame.color", W, H, scene.color_format), color_t.data_ptr())
     depth = rhi.Texture(dev, rhi.TextureDesc.new_depth("frame.depth", W, H), depth_t.data_ptr())
     r = renderer.SceneRenderer(dev, scene)
-    if a.emulate_shard and world > 1:
+    if a.emulate_shard and distributed:
         raise SystemExit("--emulate-shard is a 1-GPU diagnostic")
     shard_g = a.emulate_shard if a.emulate_shard > 1 else world
-    enc = r.record(color, depth, shard=(rank, shard_g) if shard_g > 1 else None)
-    gather = shard.TileRowGather(H, W * 4, rank, world, cuda) if world > 1 else None
+    exchange = None
+    if a.setup == "partitioned" and distributed:
+        exchange = shard.RcclExchange(cuda)
+    elif a.setup == "partitioned" and shard_g > 1:
+        exchange = MirrorExchange(cuda, shard_g)
+    if exchange is not None:
+        enc = r.record(color, depth, shard=(rank, shard_g, exchange))
+    else:
+        enc = r.record(color, depth, shard=(rank, shard_g) if shard_g > 1 else None)
+    gather = shard.TileRowGather(H, W * 4, rank, world, cuda) if distributed else None
+    # Multi-GPU: the runtime, the exchange and the gather share one stream (the
+    # runtime's), so a frame is enqueued without any host wait.
+    stream_ctx = torch.cuda.stream(torch.cuda.ExternalStream(dev.stream, device=cuda)) if distributed else None
+    if stream_ctx is not None:
+        stream_ctx.__enter__()
 
     def step():
         dev.submit(enc)
         if gather is not None:
-            dev.wait_idle()          # frame done on the raster stream before RCCL reads it
-            gather.gather(color_t)
+            gather.gather(color_t)  # ordered after the frame on the same stream
 
     for _ in range(a.warmup):
         step()
     dev.wait_idle()
     torch.cuda.synchronize()
-    if world > 1:
+    if distributed:
         dist.barrier()
     torch.cuda.synchronize()
     t0 = time.perf_counter()
@@ -125,11 +169,11 @@ def main():
         step()
     dev.wait_idle()
     torch.cuda.synchronize()
-    if world > 1:
+    if distributed:
         dist.barrier()
     t1 = time.perf_counter()
     elapsed = torch.tensor([t1 - t0], dtype=torch.float64, device=cuda)
-    if world > 1:
+    if distributed:
         dist.all_reduce(elapsed, op=dist.ReduceOp.MAX)
     elapsed = float(elapsed.item())
 
@@ -150,13 +194,19 @@ def main():
     pairs = stats["bin_pairs"]
     pixels = int(shard.owned_rows(H, rank, shard_g).numel()) * W
     b_in = scenes.config_bytes_per_triangle(a.config)
+    n_setup, n_route = N, 0
+    if exchange is not None:  # this rank's range and the triangles it received
+        _, span, _ = shard.route_geometry(N, shard_g)
+        n_route = max(0, min(N, (rank + 1) * span) - rank * span)
+        n_setup = stats["triangles_setup"]
     kernels = {}
     for name, (ms, n) in kt.items():
         avg_us = ms * 1e3 / max(n, 1)
-        by = algorithmic_bytes(name, N, b_in, pairs, pixels)
+        by = algorithmic_bytes(name, n_setup, b_in, pairs, pixels, n_route)
         kernels[name] = {"avg_us": round(avg_us, 2), "launches": n, "alg_bytes": by,
                          "gbps": round(by / (avg_us * 1e-6) / 1e9, 1) if by and avg_us > 0 else None}
-    dom = max(kt, key=lambda k: kt[k][0]) if kt else "tile"
+    launches = {k: v for k, v in kt.items() if k != "exchange"}  # "exchange": the all-to-all, not a kernel
+    dom = max(launches, key=lambda k: launches[k][0]) if launches else "tile"
     dk = kernels.get(dom, {})
     traffic = None
     if os.path.exists(a.pmc):
@@ -178,7 +228,9 @@ def main():
                                f"{'Blinn-Phong' if scene.program == scenes.PROGRAM_BLINN_PHONG else 'flat'} "
                                f"+ D32 LESS, B8G8R8A8_SRGB",
                    "triangles": N, "width": W, "height": H, "tile": shard.TILE,
-                   "parallelism": f"tile-rows x{world}" + (" + RCCL row gather" if world > 1 else "")},
+                   "parallelism": f"tile-rows x{world}" + (
+                       f", {a.setup} setup" + (" (RCCL all-to-all)" if exchange is not None else "")
+                       + " + RCCL row gather" if distributed else "")},
         "fps": round(1e3 / ms_per_step, 2),
         "ms_per_step_profiled": round((tp1 - tp0) / a.steps * 1e3, 4),
         "frame_alg_bytes": frame_bytes,
@@ -197,11 +249,14 @@ def main():
         out["cpu_baseline"] = None
     if rank == 0:
         print(json.dumps(out), flush=True)
+    if stream_ctx is not None:
+        dev.wait_idle()
+        stream_ctx.__exit__(None, None, None)
     enc.destroy()
     color.destroy()
     depth.destroy()
     dev.close()
-    if world > 1:
+    if distributed:
         dist.destroy_process_group()
 
 

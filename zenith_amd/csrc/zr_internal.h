@@ -84,15 +84,14 @@ struct alignas(8) BBox {
 constexpr uint32_t kMaxTilesPerPass = 16384;  // LDS histogram of the setup pass (64 KB)
 
 // Partitioned setup for tile-row shards.  Rank r routes the
-// primitives of its range [r * span, (r + 1) * span) in chunks of kRouteChunk
-// (one k_route workgroup each) to the ranks owning their tile rows.  Exchange
-// block for one destination = [chunks] u32 counts, then [chunks][kRouteChunk]
-// u32 primitive ids, each chunk's ids in primitive order.  After the all-to-all,
-// a receiver's blocks in source order, read chunk by chunk, list its primitives
-// in API order, so a block position is an order-preserving primitive sequence.
-constexpr uint32_t kRouteChunk = 4096;
-constexpr uint32_t kRouteChunkShift = 12;
-constexpr int kRouteThreads = 1024;  // 4 primitives per thread
+// primitives of its range [r * span, (r + 1) * span) to the ranks owning the tile
+// rows they touch, in chunks of kRouteChunk (one workgroup of k_route_count and
+// k_route_scatter each).  Exchange block for one destination = [1] u32 count,
+// then up to `span` u32 primitive ids in primitive order.  After the all-to-all a
+// receiver's blocks, in source order, list its primitives in API order, so the
+// dense position over the concatenated blocks is an order-preserving sequence.
+constexpr uint32_t kRouteChunk = 512;
+constexpr int kRouteThreads = 256;   // 2 primitives per thread
 constexpr uint32_t kMaxShards = 32;  // destination masks are u32
 
 // Timing-experiment switches (ZR_DEBUG env var); never set in production runs.
@@ -113,7 +112,17 @@ enum StatusWord : uint32_t {
 // Device-side counters (zeroed with the tile counts before each draw).
 // Device counters of k_setup_bin.  Zero between draws: the last workgroup to
 // finish (kCtExit) resets them, so a draw needs no memset launch.
-enum CounterWord : uint32_t { kCtSetup = 0, kCtDropped = 1, kCtBarrier = 2, kCtExit = 3, kCtWords = 4 };
+// The grid barrier is two-level (arrivals on 8 group counters, blockIdx % 8, then
+// one top counter; release through 8 group flags), each word on a 128-B line of
+// its own: 256 workgroups on one counter cost ~10 us after the last arrival.
+constexpr uint32_t kBarrierGroups = 8;
+enum CounterWord : uint32_t {
+    kCtSetup = 0, kCtDropped = 1, kCtExit = 3,
+    kCtGroup = 32,                            // + 32 * group: arrivals of the group
+    kCtTop = 32 * (1 + kBarrierGroups),       // groups complete
+    kCtRelease = 32 * (2 + kBarrierGroups),   // + 32 * group: barrier open
+    kCtWords = 32 * (2 + 2 * kBarrierGroups),
+};
 
 struct DrawParams {
     // vertex input (binding 0) and index buffer
@@ -159,22 +168,24 @@ struct DrawParams {
     // tiling / sharding
     uint32_t tiles_x, tiles_y, shard_rank, shard_count, owned_rows, ntiles;
     uint32_t tile_threads;    // k_tile workgroup size: 256 or 512 (tile_threads_for)
-    // partitioned setup (list mode).  In list mode `prims` counts
-    // block positions (sources * list_span), most of them empty.
+    // partitioned setup (list mode).  In list mode `prims` is the
+    // capacity of the received blocks (shard_count * span); the setup pass runs
+    // over the dense positions [0, sum of the blocks' counts).
     uint32_t draw_prims;      // primitives of the draw (instances * triangles per instance)
-    const uint32_t* list;     // received exchange blocks, or nullptr (setup over [0, prims))
-    uint32_t list_span;       // positions per source block: list_chunks * kRouteChunk
-    uint32_t list_chunks;
-    uint32_t list_block_words;// list_chunks * (kRouteChunk + 1)
-    uint32_t* route_out;      // k_route: this rank's send blocks ([shard_count][list_block_words])
-    uint32_t route_lo, route_hi; // k_route: this rank's primitive range
+    const uint32_t* list;     // received exchange blocks ([shard_count][list_block_words]), or nullptr
+    uint32_t list_block_words;// 1 + span
+    uint32_t* gids;           // list mode: the draw primitive of each setup record (resolve's index fetch)
+    uint32_t* route_out;      // k_route_*: this rank's send blocks ([shard_count][list_block_words])
+    uint32_t* route_masks;    // [span] destination mask of each primitive of the range
+    uint32_t* route_counts;   // [route_chunks][shard_count] ids per chunk and destination
+    uint32_t route_lo, route_hi, route_chunks;
     // scratch (binning without contended global atomics)
     TriCompact* records;      // [prims] compact records (every binned primitive)
     TriRecord* records_big;   // [prims] full records, written for large primitives only
     BBox* bboxes;             // [prims]; bb0 == kEmptyBox when culled / no owned tile
     uint32_t* tile_counts;    // [ntiles]
     uint32_t* tile_offsets;   // [ntiles] exclusive scan (list starts)
-    uint32_t* counters;       // [kCtWords]
+    uint32_t* counters;       // [kCtWords] (CounterWord)
     uint32_t* bins;           // [bin_capacity] primitive ids grouped by tile
     uint32_t bin_capacity;
     uint32_t setup_wgs;       // workgroups of k_setup_bin (<= CUs: all resident)
@@ -193,6 +204,8 @@ struct DrawParams {
 // primitives spread over more waves).  Measured on C2 shards (1 GPU, rank 0 of
 // G): G=4 tile pass 44 -> 39 us, G=8 40 -> 33 us; 16 waves per tile was slower
 // than 4 (61 / 43 us), so it is not built.
+// k_setup_bin LDS words besides the two tile arrays: misc (32) + list prefix (64).
+constexpr uint32_t kSetupMiscWords = 96;
 inline uint32_t tile_threads_for(uint32_t ntiles, uint32_t cus) {
     const uint32_t per_cu = ntiles / (cus ? cus : 1u);
     return per_cu >= 6u ? (uint32_t)kTileThreads : 512u;
@@ -204,6 +217,6 @@ size_t setup_bin_lds_bytes(uint32_t ntiles, uint32_t bbox_entries);
 const void* setup_bin_kernel(uint32_t batch);
 void launch_tile(const DrawParams& p, void* stream);
 void launch_clear(const DrawParams& p, void* stream);
-void launch_route(const DrawParams& p, void* stream);     // partitioned setup: route own range
+void launch_route(const DrawParams& p, void* stream);     // partitioned setup: route own range (2 kernels)
 
 }  // namespace zr

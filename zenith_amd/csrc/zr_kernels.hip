@@ -30,11 +30,11 @@ namespace zr {
 #ifndef ZR_TILE_WGS
 #define ZR_TILE_WGS 8        // k_tile workgroups per CU the register budget is sized for
 #endif
+#ifndef ZR_TILE_LPT
+#define ZR_TILE_LPT 1        // waves claim raster chunks largest-first from an LDS counter (0: static)
+#endif
 #ifndef ZR_EXP_EXTRA_VALU
 #define ZR_EXP_EXTRA_VALU 0  // experiment only: dummy VALU ops per lane-raster step
-#endif
-#ifndef ZR_TILE_PREFETCH
-#define ZR_TILE_PREFETCH 0   // request the next chunk's records before rasterizing this one
 #endif
 
 __constant__ float c_srgbT[255] = ZR_SRGB_THRESHOLDS_INIT;
@@ -59,22 +59,10 @@ __device__ __forceinline__ uint32_t tri_of(const DrawParams& P, uint32_t gid) {
     return (P.tris_per_instance == P.draw_prims) ? gid : gid % P.tris_per_instance;
 }
 
-// List mode (partitioned setup, zr_internal.h): the draw primitive at block
-// position `pos`, and whether that position holds one (chunks are partly filled).
-__device__ __forceinline__ bool list_entry(const DrawParams& P, uint32_t pos, uint32_t& gid) {
-    const uint32_t s = pos / P.list_span, jj = pos - s * P.list_span;
-    const uint32_t* blk = P.list + (size_t)s * P.list_block_words;
-    const uint32_t n = blk[jj >> kRouteChunkShift];
-    gid = blk[P.list_chunks + jj];
-    return (jj & (kRouteChunk - 1u)) < n;
-}
-
 // Draw primitive of a setup record index: the index itself, or in list mode the
-// primitive its (valid) block position holds.
+// primitive k_setup_bin recorded for that dense position.
 __device__ __forceinline__ uint32_t prim_gid(const DrawParams& P, uint32_t pos) {
-    if (!P.list) return pos;
-    const uint32_t s = pos / P.list_span;
-    return P.list[(size_t)s * P.list_block_words + P.list_chunks + (pos - s * P.list_span)];
+    return P.list ? P.gids[pos] : pos;
 }
 
 __device__ __forceinline__ void winner_vids(const DrawParams& P, uint32_t prim, uint32_t v[3]) {
@@ -244,16 +232,22 @@ __device__ __forceinline__ void fetch_indices_gid(const DrawParams& P, uint32_t 
     in.ok = ok;
 }
 
-// Record index `pos` of the setup pass: the draw primitive itself, or in list
-// mode the primitive its block position holds (none: in.ok = false).
-__device__ __forceinline__ void fetch_indices(const DrawParams& P, uint32_t pos, PrimIn& in) {
-    in.ok = pos < P.prims;
+// List mode: the draw primitive at dense position `pos` of the received blocks
+// (s_pre: exclusive prefix of the blocks' counts, G + 1 entries, in LDS).
+__device__ __forceinline__ uint32_t list_gid(const DrawParams& P, const uint32_t* s_pre, uint32_t pos) {
+    uint32_t src = 0;
+    while (src + 1u < P.shard_count && pos >= s_pre[src + 1u]) ++src;
+    return P.list[(size_t)src * P.list_block_words + 1u + (pos - s_pre[src])];
+}
+
+// Setup record `pos` (< n_pos): the draw primitive itself, or in list mode the
+// one at that dense position of the received blocks.
+__device__ __forceinline__ void fetch_indices(const DrawParams& P, uint32_t pos, uint32_t n_pos, const uint32_t* s_pre,
+                                              PrimIn& in, uint32_t& gid) {
+    in.ok = pos < n_pos;
+    gid = pos;
     if (!in.ok) return;
-    uint32_t gid = pos;
-    if (P.list && !list_entry(P, pos, gid)) {
-        in.ok = false;
-        return;
-    }
+    if (P.list) gid = list_gid(P, s_pre, pos);
     fetch_indices_gid(P, gid, in);
 }
 
@@ -332,10 +326,10 @@ __device__ __forceinline__ bool prim_geometry(const DrawParams& P, const PrimIn&
     return g.px0 <= g.px1 && g.py0 <= g.py1;
 }
 
-__device__ __forceinline__ void setup_finish(const DrawParams& P, uint32_t prim, const PrimIn& in, uint32_t* s_hist,
-                                             BBox* bbox_out,
+__device__ __forceinline__ void setup_finish(const DrawParams& P, uint32_t prim, uint32_t n_pos, uint32_t gid,
+                                             const PrimIn& in, uint32_t* s_hist, BBox* bbox_out,
                                              int& nvalid, int& ndropped) {
-    if (prim >= P.prims) return;
+    if (prim >= n_pos) return;
     BBox box{kEmptyBox, 0u};
     PrimGeom g;
     if (prim_geometry(P, in, g, ndropped)) {
@@ -365,6 +359,7 @@ __device__ __forceinline__ void setup_finish(const DrawParams& P, uint32_t prim,
             c.dz2 = g.z[2] - g.z[0];
             c.invA2s = (g.flags & kFlagSwapped) ? -invA2 : invA2;
             P.records[prim] = c;
+            if (P.list) P.gids[prim] = gid;
             box.bb0 = (uint32_t)g.px0 | ((uint32_t)g.py0 << 16);
             box.bb1 = (uint32_t)g.px1 | ((uint32_t)g.py1 << 16);
             if (!small) {
@@ -385,89 +380,136 @@ __device__ __forceinline__ void setup_finish(const DrawParams& P, uint32_t prim,
 
 // ----------------------------------------------------------------- k_route
 //
-// Partitioned setup, step 1 (tile-row shards): workgroup c routes
-// primitives [route_lo + c * kRouteChunk, ...) of this rank's range.  Each
-// thread runs the setup geometry of 4 consecutive primitives and derives the
-// set of ranks owning a tile row its bbox touches (ty % G == rank).  Per
-// destination the chunk's ids are compacted in primitive order (ballot ranks
-// within a wave, per-wave totals scanned in LDS) into that destination's
-// exchange block, and the chunk's count is stored in the block header.
-__global__ __launch_bounds__(kRouteThreads) void k_route(DrawParams P) {
-    __shared__ uint32_t s_tot[kRouteThreads / 64][kMaxShards];
-    const uint32_t G = P.shard_count, c = blockIdx.x, tid = threadIdx.x;
-    const uint32_t lane = tid & 63u, wave = tid >> 6;
-    const uint32_t p0 = P.route_lo + c * kRouteChunk + tid * 4u;
-    PrimIn in[4];
+// Partitioned setup, step 1 (tile-row shards).  Workgroup c of
+// both kernels owns primitives [route_lo + c * kRouteChunk, ...) of this rank's
+// range, thread t the primitives base + t and base + t + 256 (coalesced).
+//   k_route_count    setup geometry -> the set of ranks owning a tile row the
+//                    bbox touches (ty % G == rank) as a mask per primitive, and
+//                    the chunk's id count per destination
+//   k_route_scatter  prefix of the counts of earlier chunks, then the chunk's ids
+//                    in primitive order into each destination's block (ballot
+//                    ranks within a wave, per-wave offsets in LDS); the last
+//                    chunk stores the block totals.
+__device__ __forceinline__ uint32_t dest_mask(const DrawParams& P, const PrimGeom& g) {
+    const uint32_t G = P.shard_count;
+    const int ty0 = g.py0 >> kTileShift, ty1 = g.py1 >> kTileShift;
+    if ((uint32_t)(ty1 - ty0) + 1u >= G) return G >= 32u ? 0xFFFFFFFFu : (1u << G) - 1u;
+    uint32_t m = 0;
+    for (int ty = ty0; ty <= ty1; ++ty) m |= 1u << ((uint32_t)ty % G);
+    return m;
+}
+
+__global__ __launch_bounds__(kRouteThreads) void k_route_count(DrawParams P) {
+    __shared__ uint32_t s_cnt[kMaxShards];
+    const uint32_t G = P.shard_count, c = blockIdx.x, tid = threadIdx.x, lane = tid & 63u;
+    if (tid < kMaxShards) s_cnt[tid] = 0;
+    const uint32_t p0 = P.route_lo + c * kRouteChunk + tid;
+    PrimIn in[2];
 #pragma unroll
-    for (int k = 0; k < 4; ++k) {
-        in[k].ok = p0 + k < P.route_hi;
-        if (in[k].ok) fetch_indices_gid(P, p0 + k, in[k]);
+    for (int k = 0; k < 2; ++k) {
+        in[k].ok = p0 + k * kRouteThreads < P.route_hi;
+        if (in[k].ok) fetch_indices_gid(P, p0 + k * kRouteThreads, in[k]);
     }
 #pragma unroll
-    for (int k = 0; k < 4; ++k) fetch_positions(P, in[k]);
-    uint32_t mask[4];
+    for (int k = 0; k < 2; ++k) fetch_positions(P, in[k]);
+    uint32_t m[2];
     int ndropped = 0;
 #pragma unroll
-    for (int k = 0; k < 4; ++k) {
+    for (int k = 0; k < 2; ++k) {
         PrimGeom g;
-        mask[k] = 0u;
-        if (prim_geometry(P, in[k], g, ndropped)) {
-            const int ty0 = g.py0 >> kTileShift, ty1 = g.py1 >> kTileShift;
-            if ((uint32_t)(ty1 - ty0) + 1u >= G) {
-                mask[k] = G >= 32u ? 0xFFFFFFFFu : (1u << G) - 1u;
-            } else {
-                for (int ty = ty0; ty <= ty1; ++ty) mask[k] |= 1u << ((uint32_t)ty % G);
+        m[k] = prim_geometry(P, in[k], g, ndropped) ? dest_mask(P, g) : 0u;
+        if (p0 + k * kRouteThreads < P.route_hi) P.route_masks[p0 + k * kRouteThreads - P.route_lo] = m[k];
+    }
+    __syncthreads();
+    for (uint32_t d = 0; d < G; ++d) {
+        const uint32_t n = (uint32_t)(__popcll(__ballot((m[0] >> d) & 1u)) + __popcll(__ballot((m[1] >> d) & 1u)));
+        if (lane == 0 && n) atomicAdd(&s_cnt[d], n);
+    }
+    __syncthreads();
+    if (tid < G) P.route_counts[(size_t)c * G + tid] = s_cnt[tid];
+}
+
+__global__ __launch_bounds__(kRouteThreads) void k_route_scatter(DrawParams P) {
+    constexpr uint32_t kWaves = kRouteThreads / 64;
+    __shared__ uint32_t s_pre[kMaxShards];
+    __shared__ uint32_t s_off[2][kWaves][kMaxShards];
+    const uint32_t G = P.shard_count, c = blockIdx.x, tid = threadIdx.x;
+    const uint32_t lane = tid & 63u, wave = tid >> 6;
+    if (tid < kMaxShards) s_pre[tid] = 0;
+    const uint32_t p0 = P.route_lo + c * kRouteChunk + tid;
+    uint32_t m[2];
+#pragma unroll
+    for (int k = 0; k < 2; ++k) {
+        const uint32_t p = p0 + k * kRouteThreads;
+        m[k] = p < P.route_hi ? P.route_masks[p - P.route_lo] : 0u;
+    }
+    __syncthreads();
+    for (uint32_t i = tid; i < c * G; i += kRouteThreads) {  // ids of earlier chunks, per destination
+        const uint32_t n = P.route_counts[i];
+        if (n) atomicAdd(&s_pre[i % G], n);
+    }
+    for (uint32_t d = 0; d < G; ++d) {
+#pragma unroll
+        for (int k = 0; k < 2; ++k) {
+            const uint32_t n = (uint32_t)__popcll(__ballot((m[k] >> d) & 1u));
+            if (lane == 0) s_off[k][wave][d] = n;
+        }
+    }
+    __syncthreads();
+    if (tid < G) {  // primitive order: first half (k = 0) wave by wave, then the second half
+        uint32_t run = s_pre[tid];
+        for (int k = 0; k < 2; ++k)
+            for (uint32_t w = 0; w < kWaves; ++w) {
+                const uint32_t n = s_off[k][w][tid];
+                s_off[k][w][tid] = run;
+                run += n;
             }
-        }
+        if (c + 1u == P.route_chunks) P.route_out[(size_t)tid * P.list_block_words] = run;  // block total
     }
+    __syncthreads();
     const unsigned long long below = (1ull << lane) - 1ull;
-    // per-wave totals of every destination
     for (uint32_t d = 0; d < G; ++d) {
-        uint32_t n = 0;
+        uint32_t* ids = P.route_out + (size_t)d * P.list_block_words + 1u;
 #pragma unroll
-        for (int k = 0; k < 4; ++k) n += (uint32_t)__popcll(__ballot((mask[k] >> d) & 1u));
-        if (lane == 0) s_tot[wave][d] = n;
-    }
-    __syncthreads();
-    if (tid < G) {  // exclusive scan over waves; the chunk's count into the header
-        uint32_t run = 0;
-        for (uint32_t w = 0; w < kRouteThreads / 64; ++w) {
-            const uint32_t n = s_tot[w][tid];
-            s_tot[w][tid] = run;
-            run += n;
-        }
-        P.route_out[(size_t)tid * P.list_block_words + c] = run;
-    }
-    __syncthreads();
-    for (uint32_t d = 0; d < G; ++d) {
-        uint32_t* ids = P.route_out + (size_t)d * P.list_block_words + P.list_chunks + (size_t)c * kRouteChunk;
-        uint32_t pos = s_tot[wave][d];  // thread-major order: lanes below hold earlier primitives
-#pragma unroll
-        for (int q = 0; q < 4; ++q) pos += (uint32_t)__popcll(__ballot((mask[q] >> d) & 1u) & below);
-#pragma unroll
-        for (int k = 0; k < 4; ++k) {
-            if ((mask[k] >> d) & 1u) ids[pos++] = p0 + (uint32_t)k;
+        for (int k = 0; k < 2; ++k) {
+            const bool on = (m[k] >> d) & 1u;
+            const unsigned long long b = __ballot(on);
+            if (on) ids[s_off[k][wave][d] + (uint32_t)__popcll(b & below)] = p0 + k * kRouteThreads;
         }
     }
 }
 
 // ------------------------------------------------------------ grid barrier
 //
-// Monotonic-counter barrier for the persistent binning kernel (one workgroup per
-// CU, so every workgroup is resident).  Protocol per cdna_hip_programming.md §6
-// G16 / MI355X_MICROARCH.md "Valid forms": every storing wave drains its stores,
-// the workgroup meets, lane 0 releases at agent scope, arrives with a relaxed
-// agent atomic, polls relaxed with s_sleep (bounded), then acquires at agent
-// scope before the workgroup reads other workgroups' data.
-__device__ __forceinline__ void grid_barrier(uint32_t* counter, uint32_t target, uint32_t* status, bool drain) {
+// Grid barrier of the persistent binning kernel (one workgroup per CU, so every
+// workgroup is resident), XCD-hierarchical as MI355X_MICROARCH.md "barrier-xcd":
+// lane 0 of each workgroup arrives on its group's counter (blockIdx % 8: a group
+// label for workgroups that usually share an XCD; correctness never depends on
+// the placement), the last arrival of a group arrives on the top counter, the
+// last group opens the 8 group flags, and every workgroup polls its group's
+// flag.  Relaxed agent-scope atomics and sc1 polls: nothing handed across the
+// barrier is a plain store (tile counts are atomics, read back with sc1 loads;
+// every bbox phase 4 reads was stored by its own workgroup), so no release /
+// acquire fence -- a release would write back the XCD L2.
+// Bounded: a timeout sets a status word instead of hanging.
+__device__ __forceinline__ void grid_barrier(uint32_t* ctr, uint32_t nwg, uint32_t w, uint32_t* status, bool drain) {
     // every storing wave drains its stores, unless nothing after the barrier reads
     // what this workgroup stored before it (drain == false)
     if (drain) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     __syncthreads();
     if (threadIdx.x == 0) {
-        __hip_atomic_fetch_add(counter, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        const uint32_t g = w % kBarrierGroups;
+        const uint32_t groups = min(nwg, kBarrierGroups);
+        const uint32_t in_group = nwg / kBarrierGroups + (g < nwg % kBarrierGroups ? 1u : 0u);
+        const uint32_t prev = __hip_atomic_fetch_add(&ctr[kCtGroup + 32u * g], 1u, __ATOMIC_RELAXED,
+                                                     __HIP_MEMORY_SCOPE_AGENT);
+        if (prev + 1u == in_group &&
+            __hip_atomic_fetch_add(&ctr[kCtTop], 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) + 1u == groups) {
+            for (uint32_t k = 0; k < groups; ++k)
+                __hip_atomic_store(&ctr[kCtRelease + 32u * k], 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        }
         uint32_t spins = 0;
-        while (__hip_atomic_load(counter, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) < target) {
+        while (__hip_atomic_load(&ctr[kCtRelease + 32u * g], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == 0u) {
             __builtin_amdgcn_s_sleep(1);
             if (++spins > (1u << 24)) {  // never expected: report instead of hanging
                 ((volatile uint32_t*)status)[kStBarrierTimeout] = 1u;
@@ -553,29 +595,42 @@ __device__ __forceinline__ uint32_t block_exclusive_scan(uint32_t* a, uint32_t n
     } while (0)
 
 // i-th unit of primitives owned by workgroup w (static schedules).
-__device__ __forceinline__ uint32_t own_unit(const DrawParams& P, uint32_t w, uint32_t G, uint32_t i) {
+__device__ __forceinline__ uint32_t own_unit(const DrawParams& P, uint32_t units, uint32_t w, uint32_t G, uint32_t i) {
     if (P.setup_sched == 0) {
-        const uint32_t upw = (P.units + G - 1u) / G;
-        return i < upw ? w * upw + i : P.units;
+        const uint32_t upw = (units + G - 1u) / G;
+        return i < upw ? w * upw + i : units;
     }
     return w + i * G;
 }
 
 template <uint32_t KB>
 __global__ __launch_bounds__(kSetupThreads) void k_setup_bin(DrawParams P) {
-    extern __shared__ __attribute__((aligned(16))) uint32_t s_lds[];  // [2 * ntiles + 32] + bboxes
+    extern __shared__ __attribute__((aligned(16))) uint32_t s_lds[];  // [2 * ntiles + kSetupMiscWords] + bboxes
     const uint32_t nt = P.ntiles, G = gridDim.x, w = blockIdx.x, tid = threadIdx.x;
     uint32_t* s_hist = s_lds;            // histogram -> own offsets -> cursors
     uint32_t* s_base = s_lds + nt;       // tile totals -> tile bases
     uint32_t* s_misc = s_base + nt;      // [32]
+    uint32_t* s_pre = s_misc + 32;       // list mode: exclusive prefix of the received blocks' counts
     // this workgroup's primitives' tile bboxes, indexed like phase 4's flattened
     // (own unit, primitive in unit) space, when they fit (P.bbox_lds): then
     // nothing read after the grid barrier depends on phase 1's global stores
-    BBox* s_bbox = reinterpret_cast<BBox*>(s_misc + 32);
+    BBox* s_bbox = reinterpret_cast<BBox*>(s_misc + kSetupMiscWords);
     ZR_STAMP(0);
     for (uint32_t t = tid; t < nt; t += kSetupThreads) s_hist[t] = 0;
     if (tid < 32) s_misc[tid] = 0;
+    if (P.list && tid == 0) {
+        uint32_t run = 0;
+        for (uint32_t src = 0; src < P.shard_count; ++src) {
+            s_pre[src] = run;
+            run += P.list[(size_t)src * P.list_block_words];
+        }
+        s_pre[P.shard_count] = run;
+    }
     __syncthreads();
+    // setup records: the draw's primitives, or (list mode) the dense positions of
+    // the received blocks, in units of 2^unit_shift
+    const uint32_t n_pos = P.list ? min(s_pre[P.shard_count], P.prims) : P.prims;
+    const uint32_t units = P.list ? (n_pos + (1u << P.unit_shift) - 1u) >> P.unit_shift : P.units;
 
     // ---- phase 1
     int nvalid = 0, ndropped = 0;
@@ -583,22 +638,23 @@ __global__ __launch_bounds__(kSetupThreads) void k_setup_bin(DrawParams P) {
         const uint32_t lane = tid & 63u, wave = tid >> 6;
         const uint32_t rounds = (1u << P.unit_shift) / (64u * KB);
         for (uint32_t i = 0;; ++i) {
-            const uint32_t u = own_unit(P, w, G, wave + i * (kSetupThreads / 64u));
-            if (u >= P.units) break;
+            const uint32_t u = own_unit(P, units, w, G, wave + i * (kSetupThreads / 64u));
+            if (u >= units) break;
             const uint32_t jw = wave + i * (kSetupThreads / 64u);  // own-unit ordinal
             for (uint32_t r = 0; r < rounds; ++r) {
                 const uint32_t pb = (u << P.unit_shift) + r * 64u * KB + lane;
                 const uint32_t lb = (jw << P.unit_shift) + r * 64u * KB + lane;
                 PrimIn in[KB];
+                uint32_t gid[KB];
 #pragma unroll
-                for (uint32_t b = 0; b < KB; ++b) fetch_indices(P, min(pb + b * 64u, P.prims), in[b]);
+                for (uint32_t b = 0; b < KB; ++b) fetch_indices(P, pb + b * 64u, n_pos, s_pre, in[b], gid[b]);
 #pragma unroll
                 for (uint32_t b = 0; b < KB; ++b) fetch_positions(P, in[b]);
 #pragma unroll
                 for (uint32_t b = 0; b < KB; ++b) {
-                    const uint32_t prim = min(pb + b * 64u, P.prims);
+                    const uint32_t prim = min(pb + b * 64u, n_pos);
                     BBox* out = P.bbox_lds ? &s_bbox[lb + b * 64u] : &P.bboxes[min(prim, P.prims - 1u)];
-                    setup_finish(P, prim, in[b], s_hist, out, nvalid, ndropped);
+                    setup_finish(P, prim, n_pos, gid[b], in[b], s_hist, out, nvalid, ndropped);
                 }
             }
         }
@@ -625,7 +681,7 @@ __global__ __launch_bounds__(kSetupThreads) void k_setup_bin(DrawParams P) {
         if (s_misc[1]) atomicAdd(&P.counters[kCtDropped], s_misc[1]);
     }
     ZR_STAMP(2);
-    grid_barrier(&P.counters[kCtBarrier], G, P.status, !P.bbox_lds);
+    grid_barrier(P.counters, G, w, P.status, !P.bbox_lds);
     ZR_STAMP(3);
     if (P.debug & kDebugStopAfterScan) return;
 
@@ -637,6 +693,7 @@ __global__ __launch_bounds__(kSetupThreads) void k_setup_bin(DrawParams P) {
         for (uint32_t t = tid; t < nt; t += kSetupThreads) P.tile_offsets[t] = s_base[t];
         if (tid == 0) {
             P.tile_offsets[nt] = total;
+            P.tile_offsets[nt + 1] = n_pos;  // records k_tile's overflow scan covers
             volatile uint32_t* st = P.status;
             st[kStTotalPairs] = total;
             if (total > P.bin_capacity) st[kStOverflow] += 1u;  // draws run in stream order
@@ -652,10 +709,10 @@ __global__ __launch_bounds__(kSetupThreads) void k_setup_bin(DrawParams P) {
     {
         const uint32_t usz = 1u << P.unit_shift;
         uint32_t nown = 0;
-        while (own_unit(P, w, G, nown) < P.units) ++nown;
+        while (own_unit(P, units, w, G, nown) < units) ++nown;
         for (uint32_t j = tid; j < (nown << P.unit_shift); j += kSetupThreads) {
-            const uint32_t prim = (own_unit(P, w, G, j >> P.unit_shift) << P.unit_shift) + (j & (usz - 1u));
-            if (prim >= P.prims) continue;
+            const uint32_t prim = (own_unit(P, units, w, G, j >> P.unit_shift) << P.unit_shift) + (j & (usz - 1u));
+            if (prim >= n_pos) continue;
             const BBox bb = P.bbox_lds ? s_bbox[j] : P.bboxes[prim];
             // overflowed draw: k_tile rasterizes by scanning every record's bbox
             if (P.bbox_lds && total > P.bin_capacity) P.bboxes[prim] = bb;
@@ -696,7 +753,7 @@ __global__ __launch_bounds__(kSetupThreads) void k_setup_bin(DrawParams P) {
     __syncthreads();
     if (s_misc[2]) {
         for (uint32_t t = tid; t < nt; t += kSetupThreads) st_sc1(&P.tile_counts[t], 0u);
-        if (tid < kCtWords) st_sc1(&P.counters[tid], 0u);
+        for (uint32_t i = tid; i < kCtWords; i += kSetupThreads) st_sc1(&P.counters[i], 0u);
     }
     ZR_STAMP(6);
 }
@@ -1006,6 +1063,7 @@ __global__ __launch_bounds__(NT, ZR_TILE_WGS * kTileThreads / NT) void k_tile(Dr
     __shared__ uint32_t s_bucket[kSortBuckets];
     __shared__ float s_srgb[256];
     __shared__ uint32_t s_any;  // spill path: some primitive touching the tile (resolve's in-bounds fallback)
+    __shared__ uint32_t s_claim;  // next 64-entry chunk of the segment to rasterize
     const uint32_t t = (P.debug & kDebugReverseTiles) ? P.ntiles - 1u - blockIdx.x : blockIdx.x;
     const uint32_t oy = t / P.tiles_x, tx = t - oy * P.tiles_x;
     const uint32_t ty = oy * P.shard_count + P.shard_rank;
@@ -1059,6 +1117,7 @@ __global__ __launch_bounds__(NT, ZR_TILE_WGS * kTileThreads / NT) void k_tile(Dr
             const uint32_t n = min(kSortCap, cnt - seg);
             if (seg) load_segment(seg);
             if (threadIdx.x < kSortBuckets) s_bucket[threadIdx.x] = 0u;
+            if (threadIdx.x == 0) s_claim = 0u;
             __syncthreads();
             uint32_t pr[kPerThread], bk[kPerThread], sl[kPerThread];
 #pragma unroll
@@ -1090,26 +1149,30 @@ __global__ __launch_bounds__(NT, ZR_TILE_WGS * kTileThreads / NT) void k_tile(Dr
             }
             __syncthreads();
             if (stamp && seg == 0) ts[2] = __builtin_amdgcn_s_memrealtime();
-            // One lane per entry loads its 64-B record.  With ZR_TILE_PREFETCH the
-            // next chunk's records are requested before the current chunk is
-            // rasterized (the gather hides behind the raster loop).
-            uint32_t nprim = 0;
-            int4 n0 = make_int4(0, 0, 0, 0), n1 = n0, n2 = n0, n3 = n0;
-            auto fetch = [&](uint32_t cbx) {
-                const uint32_t j = cbx + (uint32_t)lane;
-                if (j < n) {
-                    nprim = s_sorted[j];
-                    const int4* rp = reinterpret_cast<const int4*>(P.records + nprim);
-                    n0 = rp[0]; n1 = rp[1];  // 32-B compact record
+            // Waves claim 64-entry chunks from an LDS counter, largest bboxes first
+            // (the sort put them last): longest-processing-time-first balances the
+            // waves of a tile.  One lane per entry loads its 32-B compact record.
+            // With no more chunks than waves each wave takes one statically (measured
+            // faster there: C1 78 vs 85 us, C3 299 vs 304 us; LPT: C2 80 vs 82 us).
+            const uint32_t nch = (n + 63u) / 64u;
+            const bool lpt = ZR_TILE_LPT && nch > NT / 64u;
+            for (uint32_t it = 0;; ++it) {
+                uint32_t claim = wave + it * (NT / 64u);  // static: wave w takes chunks w, w + waves, ...
+                if (lpt) {
+                    if (lane == 0) claim = atomicAdd(&s_claim, 1u);
+                    claim = (uint32_t)__builtin_amdgcn_readfirstlane((int)claim);
                 }
-            };
-            if (ZR_TILE_PREFETCH) fetch(wave * 64u);
-            for (uint32_t cb = wave * 64u; cb < n; cb += NT) {
-                if (!ZR_TILE_PREFETCH) fetch(cb);
+                if (claim >= nch) break;
+                const uint32_t cb = (lpt ? nch - 1u - claim : claim) * 64u;
                 const uint32_t j = cb + (uint32_t)lane;
-                const uint32_t my_prim = nprim;
-                const int4 q0 = n0, q1 = n1;
-                if (ZR_TILE_PREFETCH) fetch(cb + NT);
+                uint32_t my_prim = 0;
+                int4 q0 = make_int4(0, 0, 0, 0), q1 = q0;
+                if (j < n) {
+                    my_prim = s_sorted[j];
+                    const int4* rp = reinterpret_cast<const int4*>(P.records + my_prim);
+                    q0 = rp[0];
+                    q1 = rp[1];
+                }
                 const bool valid = j < n && !(P.debug & kDebugLoadOnly);
                 if (P.debug & kDebugLoadOnly) asm volatile("" ::"v"(q0.x), "v"(q1.x), "v"(my_prim));
                 const bool large = compact_is_large(q0);
@@ -1130,11 +1193,12 @@ __global__ __launch_bounds__(NT, ZR_TILE_WGS * kTileThreads / NT) void k_tile(Dr
             __syncthreads();
         }
         if (spill) {
-            for (uint32_t cb = wave * 64u; cb < P.prims; cb += NT) {
+            const uint32_t n_rec = P.tile_offsets[P.ntiles + 1];  // setup records of the draw
+            for (uint32_t cb = wave * 64u; cb < n_rec; cb += NT) {
                 const uint32_t j = cb + (uint32_t)lane;
                 bool hit = false;
                 int4 q0 = make_int4(0, 0, 0, 0), q1 = q0;
-                if (j < P.prims) {
+                if (j < n_rec) {
                     const BBox bb = P.bboxes[j];
                     hit = bb.bb0 != kEmptyBox && (int)(bb.bb0 & 0xFFFFu) < x0 + kTile && (int)(bb.bb1 & 0xFFFFu) >= x0 &&
                           (int)(bb.bb0 >> 16) < y0 + kTile && (int)(bb.bb1 >> 16) >= y0;
@@ -1202,7 +1266,7 @@ __global__ __launch_bounds__(kTileThreads) void k_clear(DrawParams P) {
 static inline uint32_t blocks_for(uint32_t n, uint32_t per) { return (n + per - 1) / per; }
 
 size_t setup_bin_lds_bytes(uint32_t ntiles, uint32_t bbox_entries) {
-    return (2 * (size_t)ntiles + 32) * sizeof(uint32_t) + (size_t)bbox_entries * sizeof(BBox);
+    return (2 * (size_t)ntiles + kSetupMiscWords) * sizeof(uint32_t) + (size_t)bbox_entries * sizeof(BBox);
 }
 
 const void* setup_bin_kernel(uint32_t batch) {
@@ -1262,7 +1326,8 @@ void launch_tile(const DrawParams& p, void* stream) {
 }
 
 void launch_route(const DrawParams& p, void* stream) {
-    hipLaunchKernelGGL(k_route, dim3(p.list_chunks), dim3(kRouteThreads), 0, (hipStream_t)stream, p);
+    hipLaunchKernelGGL(k_route_count, dim3(p.route_chunks), dim3(kRouteThreads), 0, (hipStream_t)stream, p);
+    hipLaunchKernelGGL(k_route_scatter, dim3(p.route_chunks), dim3(kRouteThreads), 0, (hipStream_t)stream, p);
 }
 
 void launch_clear(const DrawParams& p, void* stream) {

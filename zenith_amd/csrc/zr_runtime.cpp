@@ -187,6 +187,12 @@ struct ScratchSet {
     uint64_t xsend_cap = 0;
     uint32_t* xrecv = nullptr;
     uint64_t xrecv_cap = 0;
+    uint32_t* gids = nullptr;   // draw primitive per setup record (list mode)
+    uint64_t gids_cap = 0;
+    uint32_t* rmasks = nullptr; // route: destination mask per primitive of the range
+    uint64_t rmasks_cap = 0;
+    uint32_t* rcounts = nullptr;// route: ids per chunk and destination
+    uint64_t rcounts_cap = 0;
     hipEvent_t setup_done = nullptr;  // k_setup_bin of the last draw that used this set
     hipEvent_t tile_done = nullptr;   // k_tile of the last draw that used this set
     bool tile_done_valid = false;
@@ -508,7 +514,7 @@ zr_result ensure_scratch(zr_device* d, ScratchSet& S, DrawParams& P) {
         if ((rc = grow(d, S.tile_counts, S.tiles_cap, P.ntiles + 1, 4))) return rc;
         if (S.tiles_cap != cap) ZR_HIP(hipMemset(S.tile_counts, 0, S.tiles_cap * 4));
     }
-    if ((rc = grow(d, S.tile_offsets, S.tiles_cap2, P.ntiles + 1, 4))) return rc;
+    if ((rc = grow(d, S.tile_offsets, S.tiles_cap2, P.ntiles + 2, 4))) return rc;
     if (!S.counters) {  // zeroed once; k_setup_bin leaves them zero after every draw
         if ((rc = grow(d, S.counters, S.counters_cap, kCtWords, 4))) return rc;
         ZR_HIP(hipMemset(S.counters, 0, S.counters_cap * 4));
@@ -579,21 +585,22 @@ zr_result exec_draw(zr_device* d, ExecState& s, const Cmd& c, bool indexed) {
     P.prims = (uint32_t)prims;
     P.draw_prims = (uint32_t)prims;
     // Partitioned setup: this rank routes [lo, hi) of the draw's
-    // primitives; the setup pass then runs over the received blocks' positions.
+    // primitives; the setup pass then runs over the received blocks' dense
+    // positions (at most shard_count * span of them).
     const bool partitioned = s.exchange != nullptr;
     uint64_t positions = prims;
+    uint64_t span = 0;
     if (partitioned) {
         const uint64_t G = s.shard_count;
         const uint64_t per_rank = (prims + G - 1) / G;
-        const uint64_t chunks = std::max<uint64_t>(1, (per_rank + kRouteChunk - 1) / kRouteChunk);
-        positions = G * chunks * kRouteChunk;
+        span = std::max<uint64_t>(1, (per_rank + kRouteChunk - 1) / kRouteChunk) * kRouteChunk;
+        positions = G * span;
         if (positions > kBinPrimMask)
             return fail(ZR_ERROR_FEATURE_NOT_PRESENT, "partitioned draw: more than 2^26-1 block positions");
-        P.list_chunks = (uint32_t)chunks;
-        P.list_span = (uint32_t)(chunks * kRouteChunk);
-        P.list_block_words = (uint32_t)(chunks * (kRouteChunk + 1));
-        P.route_lo = (uint32_t)std::min<uint64_t>(prims, (uint64_t)s.shard_rank * P.list_span);
-        P.route_hi = (uint32_t)std::min<uint64_t>(prims, (uint64_t)P.route_lo + P.list_span);
+        P.list_block_words = (uint32_t)(span + 1);
+        P.route_chunks = (uint32_t)(span / kRouteChunk);
+        P.route_lo = (uint32_t)std::min<uint64_t>(prims, (uint64_t)s.shard_rank * span);
+        P.route_hi = (uint32_t)std::min<uint64_t>(prims, (uint64_t)P.route_lo + span);
         P.prims = (uint32_t)positions;
     }
     // viewport transform constants (Vulkan 1.3 §Controlling the Viewport)
@@ -675,7 +682,10 @@ zr_result exec_draw(zr_device* d, ExecState& s, const Cmd& c, bool indexed) {
     }
     // Draws alternate between the two scratch sets when overlapping (not while
     // debugging or with graph replay, whose captures bake in set 0: one stream).
-    const bool overlap = d->overlap && !d->debug && !d->use_graphs && !partitioned;
+    // Partitioned draws always use both scratch sets and streams: the route and the
+    // exchange of draw i+1 run on setup_stream while draw i's setup + tile pass
+    // run on the main stream.
+    const bool overlap = (d->overlap && !d->debug && !d->use_graphs) || partitioned;
     ScratchSet& S = d->sets[overlap ? d->cur_set : 0];
     if (overlap) d->cur_set ^= 1u;
     if ((rc = ensure_scratch(d, S, P))) return rc;
@@ -683,14 +693,25 @@ zr_result exec_draw(zr_device* d, ExecState& s, const Cmd& c, bool indexed) {
     d->last.triangles_in = prims;
 
     const hipStream_t ss = overlap ? d->setup_stream : d->stream;
-    // setup may start once the previous reader of this scratch set (a k_tile two
-    // draws back) is done; it reads only vertex/index buffers besides the set
+    // the first pass on ss may start once the previous reader of this scratch set
+    // (the k_tile two draws back) is done
     if (overlap && S.tile_done_valid) ZR_HIP(hipStreamWaitEvent(ss, S.tile_done, 0));
+    // debug early exits skip the self-reset at the end of k_setup_bin
+    if (d->debug) {
+        ZR_HIP(hipMemsetAsync(P.counters, 0, kCtWords * 4, d->stream));
+        ZR_HIP(hipMemsetAsync(P.tile_counts, 0, (size_t)P.ntiles * 4, d->stream));
+    }
     if (partitioned) {
         const uint64_t words = (uint64_t)s.shard_count * P.list_block_words;
         if ((rc = grow(d, S.xsend, S.xsend_cap, words, 4))) return rc;
         if ((rc = grow(d, S.xrecv, S.xrecv_cap, words, 4))) return rc;
+        if ((rc = grow(d, S.gids, S.gids_cap, positions, 4))) return rc;
+        if ((rc = grow(d, S.rmasks, S.rmasks_cap, span, 4))) return rc;
+        if ((rc = grow(d, S.rcounts, S.rcounts_cap, (uint64_t)P.route_chunks * s.shard_count, 4))) return rc;
         P.route_out = S.xsend;
+        P.route_masks = S.rmasks;
+        P.route_counts = S.rcounts;
+        P.gids = S.gids;
         timed_launch(d, "route", ss, [&] { launch_route(P, ss); });
         ZR_HIP(hipGetLastError());
         zr_result xr = ZR_SUCCESS;
@@ -699,16 +720,15 @@ zr_result exec_draw(zr_device* d, ExecState& s, const Cmd& c, bool indexed) {
         });
         if (xr != ZR_SUCCESS) return fail(xr, "tile-shard exchange callback failed: " + g_last_error);
         P.list = S.xrecv;
-    }
-    // debug early exits skip the self-reset at the end of k_setup_bin
-    if (d->debug) {
-        ZR_HIP(hipMemsetAsync(P.counters, 0, kCtWords * 4, ss));
-        ZR_HIP(hipMemsetAsync(P.tile_counts, 0, (size_t)P.ntiles * 4, ss));
-    }
-    timed_launch(d, "setup_bin", ss, [&] { launch_setup_bin(P, ss); });
-    if (overlap) {
         ZR_HIP(hipEventRecord(S.setup_done, ss));
         ZR_HIP(hipStreamWaitEvent(d->stream, S.setup_done, 0));
+        timed_launch(d, "setup_bin", d->stream, [&] { launch_setup_bin(P, d->stream); });
+    } else {
+        timed_launch(d, "setup_bin", ss, [&] { launch_setup_bin(P, ss); });
+        if (overlap) {
+            ZR_HIP(hipEventRecord(S.setup_done, ss));
+            ZR_HIP(hipStreamWaitEvent(d->stream, S.setup_done, 0));
+        }
     }
     timed_launch(d, "tile", d->stream, [&] { launch_tile(P, d->stream); });
     if (overlap) {
@@ -840,7 +860,8 @@ ZR_API void zr_device_destroy(zr_device* d) {
     if (d->dbg_ts) (void)hipFree(d->dbg_ts);
     for (ScratchSet& S : d->sets) {
         for (void* p : {(void*)S.records, (void*)S.records_big, (void*)S.bboxes, (void*)S.tile_counts,
-                        (void*)S.tile_offsets, (void*)S.counters, (void*)S.bins, (void*)S.xsend, (void*)S.xrecv})
+                        (void*)S.tile_offsets, (void*)S.counters, (void*)S.bins, (void*)S.xsend, (void*)S.xrecv,
+                        (void*)S.gids, (void*)S.rmasks, (void*)S.rcounts})
             if (p) (void)hipFree(p);
         if (S.setup_done) (void)hipEventDestroy(S.setup_done);
         if (S.tile_done) (void)hipEventDestroy(S.tile_done);
