@@ -46,6 +46,9 @@ def parse():
     p.add_argument("--setup", choices=["partitioned", "replicated"], default="partitioned",
                    help="tile-row shards: route 1/G of the primitives per rank through an RCCL all-to-all "
                         "(DESIGN.md §7), or set up every primitive on every rank")
+    p.add_argument("--comm", choices=["runtime", "torch"], default="runtime",
+                   help="multi-GPU collectives: the runtime's own RCCL communicators (exchange + row gather "
+                        "enqueued from C++), or torch.distributed's (Python callbacks)")
     p.add_argument("--force-dist", action="store_true",
                    help="run the multi-GPU code path (RCCL process group, exchange, gather) even at 1 GPU")
     p.add_argument("--pmc", default=os.path.join(ROOT, "profiles", "r01_pmc_c2.json"),
@@ -110,6 +113,11 @@ class MirrorExchange(shard.Exchange):
 
 def main():
     a = parse()
+    # The JSON line is the only thing on stdout: libraries that print to fd 1
+    # (RCCL's version banner) are sent to stderr.
+    json_out = os.fdopen(os.dup(1), "w")
+    os.dup2(2, 1)
+    sys.stdout = sys.stderr
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
@@ -127,35 +135,69 @@ def main():
     scene = scenes.config_scene(a.config)
     W, H, N = scene.width, scene.height, scene.triangles
     dev = rhi.RenderDevice(local)
-    color_t = torch.zeros((H, W * 4), dtype=torch.uint8, device=cuda)
+    # Multi-GPU frames ping-pong between two colour targets: frame f+1 renders
+    # while frame f's rows are gathered on a stream of their own.
+    nbuf = 2 if distributed else 1
+    color_ts = [torch.zeros((H, W * 4), dtype=torch.uint8, device=cuda) for _ in range(nbuf)]
+    color_t = color_ts[0]
     depth_t = torch.zeros((H, W), dtype=torch.float32, device=cuda)
     torch.cuda.synchronize()
-    color = rhi.Texture(dev, rhi.TextureDesc.new_color("frame.color", W, H, scene.color_format), color_t.data_ptr())
+    colors = [rhi.Texture(dev, rhi.TextureDesc.new_color(f"frame.color{i}", W, H, scene.color_format), t.data_ptr())
+              for i, t in enumerate(color_ts)]
+    color = colors[0]
     depth = rhi.Texture(dev, rhi.TextureDesc.new_depth("frame.depth", W, H), depth_t.data_ptr())
     r = renderer.SceneRenderer(dev, scene)
     if a.emulate_shard and distributed:
         raise SystemExit("--emulate-shard is a 1-GPU diagnostic")
     shard_g = a.emulate_shard if a.emulate_shard > 1 else world
     exchange = None
-    if a.setup == "partitioned" and distributed:
-        exchange = shard.RcclExchange(cuda)
+    runtime_comm = distributed and a.comm == "runtime"
+    if runtime_comm:
+        shard.init_runtime_rccl(dev, rank, world)
+    if a.setup == "partitioned" and runtime_comm:
+        exchange = "rccl"
+    elif a.setup == "partitioned" and distributed:
+        # its own communicator (and so its own RCCL stream): the exchange of frame
+        # f+1 must not queue behind the row gather of frame f
+        exchange = shard.RcclExchange(cuda, group=dist.new_group(list(range(world))))
     elif a.setup == "partitioned" and shard_g > 1:
         exchange = MirrorExchange(cuda, shard_g)
-    if exchange is not None:
-        enc = r.record(color, depth, shard=(rank, shard_g, exchange))
-    else:
-        enc = r.record(color, depth, shard=(rank, shard_g) if shard_g > 1 else None)
-    gather = shard.TileRowGather(H, W * 4, rank, world, cuda) if distributed else None
-    # Multi-GPU: the runtime, the exchange and the gather share one stream (the
-    # runtime's), so a frame is enqueued without any host wait.
-    stream_ctx = torch.cuda.stream(torch.cuda.ExternalStream(dev.stream, device=cuda)) if distributed else None
+    sh = (rank, shard_g, exchange) if exchange is not None else ((rank, shard_g) if shard_g > 1 else None)
+    encs = [r.record(c, depth, shard=sh, encoder=rhi.CommandEncoder(dev)) for c in colors]
+    enc = encs[0]
+    gather = shard.TileRowGather(H, W * 4, rank, world, cuda) if distributed and not runtime_comm else None
+    # Multi-GPU: torch's current stream is the runtime's main stream, so frames,
+    # exchanges and gathers are ordered by streams and events, never a host wait.
+    main_stream = torch.cuda.ExternalStream(dev.stream, device=cuda)
+    stream_ctx = torch.cuda.stream(main_stream) if distributed else None
     if stream_ctx is not None:
         stream_ctx.__enter__()
+    gstream = torch.cuda.Stream(cuda) if gather is not None else None
+    gdone = [None] * nbuf
+    frame = [0]
+
+    host_t = [0.0, 0.0]  # host seconds in submit / gather (diagnostic)
 
     def step():
-        dev.submit(enc)
+        b = frame[0] % nbuf
+        frame[0] += 1
+        if gdone[b] is not None:
+            main_stream.wait_event(gdone[b])  # the gather of frame f-2 read this target
+        h0 = time.perf_counter()
+        dev.submit(encs[b])
+        h1 = time.perf_counter()
+        host_t[0] += h1 - h0
+        if runtime_comm:
+            dev.gather_tile_rows(colors[b], 0)  # RCCL on the runtime's gather stream
+            host_t[1] += time.perf_counter() - h1
         if gather is not None:
-            gather.gather(color_t)  # ordered after the frame on the same stream
+            ev = torch.cuda.Event()
+            ev.record(main_stream)
+            gstream.wait_event(ev)
+            with torch.cuda.stream(gstream):
+                gather.gather(color_ts[b])
+            gdone[b] = torch.cuda.Event()
+            gdone[b].record(gstream)
 
     for _ in range(a.warmup):
         step()
@@ -164,9 +206,11 @@ def main():
     if distributed:
         dist.barrier()
     torch.cuda.synchronize()
+    host_t[0] = host_t[1] = 0.0
     t0 = time.perf_counter()
     for _ in range(a.steps):
         step()
+    t_enq = time.perf_counter()  # host enqueue time of the K frames (diagnostic: host-bound if ~ wall)
     dev.wait_idle()
     torch.cuda.synchronize()
     if distributed:
@@ -230,9 +274,12 @@ def main():
                    "triangles": N, "width": W, "height": H, "tile": shard.TILE,
                    "parallelism": f"tile-rows x{world}" + (
                        f", {a.setup} setup" + (" (RCCL all-to-all)" if exchange is not None else "")
-                       + " + RCCL row gather" if distributed else "")},
+                       + f" + RCCL row gather ({a.comm} communicators)" if distributed else "")},
         "fps": round(1e3 / ms_per_step, 2),
         "ms_per_step_profiled": round((tp1 - tp0) / a.steps * 1e3, 4),
+        "host_enqueue_ms_per_step": round((t_enq - t0) / a.steps * 1e3, 4),
+        "host_submit_ms_per_step": round(host_t[0] / a.steps * 1e3, 4),
+        "host_gather_ms_per_step": round(host_t[1] / a.steps * 1e3, 4),
         "frame_alg_bytes": frame_bytes,
         "frame_gbps": round(frame_bytes / (ms_per_step * 1e-3) / 1e9, 1),
         "roofline": {"bound": "hbm", "kernel": dom, "achieved": achieved, "peak": HBM_PEAK_GBPS, "unit": "GB/s",
@@ -248,12 +295,14 @@ def main():
     elif rank == 0:
         out["cpu_baseline"] = None
     if rank == 0:
-        print(json.dumps(out), flush=True)
+        print(json.dumps(out), file=json_out, flush=True)
     if stream_ctx is not None:
         dev.wait_idle()
         stream_ctx.__exit__(None, None, None)
-    enc.destroy()
-    color.destroy()
+    for e in encs:
+        e.destroy()
+    for c in colors:
+        c.destroy()
     depth.destroy()
     dev.close()
     if distributed:

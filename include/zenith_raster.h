@@ -339,6 +339,25 @@ typedef zr_result (*zr_exchange_fn)(void *user, void *hip_stream, const void *se
 ZR_API void zr_cmd_set_tile_shard_exchange(zr_cmd *cmd, uint32_t rank, uint32_t count, zr_exchange_fn exchange,
                                            void *user);
 
+/* Multi-GPU over RCCL inside the runtime (no reference counterpart).
+ * One process per GPU.  Rank 0 makes two ids (zr_rccl_get_unique_id), the caller
+ * distributes them (any side channel), and every rank calls zr_device_init_rccl
+ * (collective, blocking).  Then:
+ *   zr_cmd_set_tile_shard_exchange(cmd, rank, nranks, zr_rccl_exchange_fn(), dev)
+ *     partitions setup with the built-in all-to-all (grouped send/recv);
+ *   zr_device_gather_tile_rows(dev, tex, root) sends this rank's tile rows of
+ *     `tex` into the root's `tex` (the root receives all others) on a stream of
+ *     its own after the work enqueued so far; the next render pass writing `tex`
+ *     waits for it.  Collective: every rank calls it for its frame, in order.
+ * RCCL is loaded at run time (the process's copy if one is loaded, else
+ * librccl.so); ZR_ERROR_INITIALIZATION_FAILED when unavailable. */
+#define ZR_RCCL_ID_BYTES 128
+ZR_API zr_result zr_rccl_get_unique_id(void *out);
+ZR_API zr_result zr_device_init_rccl(zr_device *dev, const void *exchange_id, const void *gather_id, int32_t nranks,
+                                     int32_t rank);
+ZR_API zr_exchange_fn zr_rccl_exchange_fn(void);
+ZR_API zr_result zr_device_gather_tile_rows(zr_device *dev, zr_texture *tex, int32_t root);
+
 /* -------------------------------------------------------------- submission */
 
 ZR_API zr_result zr_fence_create(zr_device *dev, zr_fence **out);

@@ -397,3 +397,28 @@ def test_partitioned_rccl_exchange():
         dev.close()
     finally:
         dist.destroy_process_group()
+
+
+def test_runtime_rccl_world1():
+    """The runtime's own RCCL communicators (zr_device_init_rccl) at world size 1:
+    partitioned setup through zr_rccl_exchange_fn, and the tile-row gather (no
+    peers: nothing moves) ordered before the next pass on the same target."""
+    dev = rhi.RenderDevice(0)
+    try:
+        shard.init_runtime_rccl(dev, 0, 1)
+        s = scenes.soup_scene(76, 5000, 256, 192, 10.0, scenes.PROGRAM_BLINN_PHONG)
+        color = rhi.Texture(dev, rhi.TextureDesc.new_color("rt", s.width, s.height, s.color_format))
+        depth = rhi.Texture(dev, rhi.TextureDesc.new_depth("ds", s.width, s.height))
+        r = renderer.SceneRenderer(dev, s)
+        enc = r.record(color, depth, shard=(0, 1, "rccl"))
+        oc, od = oracle.render(s)
+        for _ in range(3):
+            dev.submit(enc)
+            dev.gather_tile_rows(color, 0)
+        dev.wait_idle()
+        assert np.array_equal(color.read(), oc) and np.array_equal(depth.read().view(np.uint32), od.view(np.uint32))
+        enc.destroy()
+        color.destroy()
+        depth.destroy()
+    finally:
+        dev.close()

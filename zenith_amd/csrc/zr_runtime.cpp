@@ -17,6 +17,7 @@
 
 #include "zenith_raster.h"
 #include "zr_internal.h"
+#include "zr_rccl.h"
 #include "zr_shading.h"
 
 using namespace zr;
@@ -102,6 +103,10 @@ struct zr_texture_t {
     uint32_t bpp;
     bool external;
     std::string name;
+    // zr_device_gather_tile_rows: the gather that last read this texture (the
+    // next render pass writing it waits for it on the device stream)
+    hipEvent_t gather_done = nullptr;
+    bool gather_pending = false;
 };
 
 struct zr_pipeline_t {
@@ -232,6 +237,14 @@ struct zr_device_t {
     std::vector<zr_cmd*> pending;
     uint64_t overflowed_draws = 0;
     hipStream_t own_stream = nullptr;  // `stream` unless zr_device_set_stream installed the caller's
+    // multi-GPU (zr_device_init_rccl): one communicator for the partitioned-setup
+    // exchange (setup stream), one for the tile-row gather (gather stream), so an
+    // exchange never queues behind the previous frame's gather
+    void* comm_x = nullptr;
+    void* comm_g = nullptr;
+    int comm_rank = 0, comm_size = 1;
+    hipStream_t gather_stream = nullptr;
+    hipEvent_t frame_done = nullptr;
     zr_draw_stats last{};
     uint64_t last_prims = 0;
     // profiling
@@ -295,6 +308,7 @@ void timed_launch(zr_device* d, const char* name, hipStream_t stream, F&& fn) {
 zr_result sync_streams(zr_device* d) {
     ZR_HIP(hipStreamSynchronize(d->setup_stream));
     ZR_HIP(hipStreamSynchronize(d->stream));
+    if (d->gather_stream) ZR_HIP(hipStreamSynchronize(d->gather_stream));
     return ZR_SUCCESS;
 }
 
@@ -763,6 +777,12 @@ zr_result execute(zr_device* d, zr_cmd* cmd) {
         case C_BEGIN_RENDERING:
             s.rendering = true;
             s.rs = c.rendering;
+            for (const zr_texture* t : {s.rs.has_color ? s.rs.color.texture : nullptr,
+                                        s.rs.has_depth ? s.rs.depth.texture : nullptr}) {
+                if (!t || !t->gather_pending) continue;
+                if (d->capturing) return ZR_NOT_READY;  // a gather is not part of the graph: run eagerly
+                ZR_HIP(hipStreamWaitEvent(d->stream, t->gather_done, 0));
+            }
             s.color_clear_pending = s.rs.has_color && s.rs.color.load_op == ZR_ATTACHMENT_LOAD_OP_CLEAR;
             s.depth_clear_pending = s.rs.has_depth && s.rs.depth.load_op == ZR_ATTACHMENT_LOAD_OP_CLEAR;
             break;
@@ -867,6 +887,10 @@ ZR_API void zr_device_destroy(zr_device* d) {
         if (S.tile_done) (void)hipEventDestroy(S.tile_done);
     }
     (void)hipHostFree(d->status_host);
+    rccl_comm_destroy(d->comm_x);
+    rccl_comm_destroy(d->comm_g);
+    if (d->gather_stream) (void)hipStreamDestroy(d->gather_stream);
+    if (d->frame_done) (void)hipEventDestroy(d->frame_done);
     (void)hipStreamDestroy(d->setup_stream);
     (void)hipStreamDestroy(d->own_stream);
     delete d;
@@ -1030,6 +1054,7 @@ ZR_API void zr_texture_destroy(zr_texture* t) {
     if (!t) return;
     device_sync(t->dev);
     if (!t->external) (void)hipFree(t->ptr);
+    if (t->gather_done) (void)hipEventDestroy(t->gather_done);
     delete t;
 }
 
@@ -1451,6 +1476,94 @@ ZR_API void zr_cmd_set_tile_shard_exchange(zr_cmd* c, uint32_t rank, uint32_t co
     k.exchange_user = user;
     c->cmds.push_back(k);
     c->has_exchange = true;
+}
+
+// ------------------------------------------------------------ multi-GPU (RCCL)
+
+namespace {
+
+// The built-in zr_exchange_fn: one grouped send + receive per rank over the
+// device's exchange communicator, enqueued on the stream the runtime passes.
+zr_result rccl_exchange(void* user, void* stream, const void* send, void* recv, uint64_t bytes_per_rank) {
+    zr_device* d = (zr_device*)user;
+    if (!d || !d->comm_x) return fail(ZR_ERROR_INITIALIZATION_FAILED, "zr_rccl_exchange_fn: device has no RCCL communicator");
+    std::string err;
+    const hipStream_t s = (hipStream_t)stream;
+    if (rccl_has_all_to_all()) {
+        if (!rccl_all_to_all(send, recv, bytes_per_rank, d->comm_x, s, err)) return fail(ZR_ERROR_DEVICE_LOST, err);
+        return ZR_SUCCESS;
+    }
+    bool ok = rccl_group_start(err);
+    for (int p = 0; ok && p < d->comm_size; ++p) {
+        ok = rccl_send((const uint8_t*)send + (uint64_t)p * bytes_per_rank, bytes_per_rank, p, d->comm_x, s, err) &&
+             rccl_recv((uint8_t*)recv + (uint64_t)p * bytes_per_rank, bytes_per_rank, p, d->comm_x, s, err);
+    }
+    if (!rccl_group_end(err) || !ok) return fail(ZR_ERROR_DEVICE_LOST, err);
+    return ZR_SUCCESS;
+}
+
+}  // namespace
+
+ZR_API zr_result zr_rccl_get_unique_id(void* out) {
+    if (!out) return fail(ZR_ERROR_VALIDATION_FAILED, "out is NULL");
+    std::string err;
+    if (!rccl_unique_id(out, err)) return fail(ZR_ERROR_INITIALIZATION_FAILED, err);
+    return ZR_SUCCESS;
+}
+
+ZR_API zr_result zr_device_init_rccl(zr_device* d, const void* exchange_id, const void* gather_id, int32_t nranks,
+                                     int32_t rank) {
+    if (!d || !exchange_id || !gather_id) return fail(ZR_ERROR_VALIDATION_FAILED, "NULL argument");
+    if (nranks < 1 || nranks > (int32_t)kMaxShards || rank < 0 || rank >= nranks)
+        return fail(ZR_ERROR_VALIDATION_FAILED, "bad rank / rank count");
+    if (d->comm_x) return fail(ZR_ERROR_VALIDATION_FAILED, "device already has RCCL communicators");
+    zr_result rc = set_device(d);
+    if (rc) return rc;
+    std::string err;
+    if (!rccl_comm_init(&d->comm_x, exchange_id, nranks, rank, err) ||
+        !rccl_comm_init(&d->comm_g, gather_id, nranks, rank, err)) {
+        rccl_comm_destroy(d->comm_x);
+        d->comm_x = nullptr;
+        return fail(ZR_ERROR_INITIALIZATION_FAILED, err);
+    }
+    d->comm_rank = rank;
+    d->comm_size = nranks;
+    ZR_HIP(hipStreamCreateWithFlags(&d->gather_stream, hipStreamNonBlocking));
+    ZR_HIP(hipEventCreateWithFlags(&d->frame_done, hipEventDisableTiming));
+    return ZR_SUCCESS;
+}
+
+ZR_API zr_exchange_fn zr_rccl_exchange_fn(void) { return &rccl_exchange; }
+
+ZR_API zr_result zr_device_gather_tile_rows(zr_device* d, zr_texture* t, int32_t root) {
+    if (!d || !t) return fail(ZR_ERROR_VALIDATION_FAILED, "NULL argument");
+    if (!d->comm_g) return fail(ZR_ERROR_INITIALIZATION_FAILED, "device has no RCCL communicator (zr_device_init_rccl)");
+    if (root < 0 || root >= d->comm_size) return fail(ZR_ERROR_VALIDATION_FAILED, "bad root rank");
+    zr_result rc = set_device(d);
+    if (rc) return rc;
+    if (!t->gather_done) ZR_HIP(hipEventCreateWithFlags(&t->gather_done, hipEventDisableTiming));
+    // after everything enqueued so far on the device stream (the frame)
+    ZR_HIP(hipEventRecord(d->frame_done, d->stream));
+    ZR_HIP(hipStreamWaitEvent(d->gather_stream, d->frame_done, 0));
+    const uint64_t row_bytes = (uint64_t)t->width * t->bpp;
+    const uint32_t tiles_y = (t->height + kTile - 1) / kTile;
+    const int G = d->comm_size, me = d->comm_rank;
+    std::string err;
+    bool ok = rccl_group_start(err);
+    // every tile row is a contiguous span of the linear image: sent from its owner
+    // straight into place on the root, no packing
+    for (uint32_t ty = 0; ok && ty < tiles_y; ++ty) {
+        const int owner = (int)(ty % (uint32_t)G);
+        if (owner == root) continue;
+        uint8_t* p = (uint8_t*)t->ptr + (uint64_t)ty * kTile * row_bytes;
+        const uint64_t bytes = (uint64_t)std::min<uint32_t>(kTile, t->height - ty * kTile) * row_bytes;
+        if (me == root) ok = rccl_recv(p, bytes, owner, d->comm_g, d->gather_stream, err);
+        else if (me == owner) ok = rccl_send(p, bytes, root, d->comm_g, d->gather_stream, err);
+    }
+    if (!rccl_group_end(err) || !ok) return fail(ZR_ERROR_DEVICE_LOST, err);
+    ZR_HIP(hipEventRecord(t->gather_done, d->gather_stream));
+    t->gather_pending = true;
+    return ZR_SUCCESS;
 }
 
 // --------------------------------------------------------------- submission

@@ -131,7 +131,9 @@ class SceneRenderer:
         self.encoder = rhi.CommandEncoder(device)
 
     def record(self, color: rhi.Texture, depth: Optional[rhi.Texture], shard: Optional[tuple] = None,
-               viewport=None, scissor=None) -> rhi.CommandEncoder:
+               viewport=None, scissor=None, encoder: Optional[rhi.CommandEncoder] = None) -> rhi.CommandEncoder:
+        """Records the scene's node into ``encoder`` (default: the renderer's own)."""
+        encoder = encoder or self.encoder
         s = self.scene
         W, H = s.width, s.height
 
@@ -159,8 +161,8 @@ class SceneRenderer:
                 enc.draw(s.draw_count, s.instance_count, s.first, 0)
             ctx.end_rendering()
 
-        rhi.execute_graphic_node(self.device, self.encoder, self.pipeline, [color], depth, job)
-        return self.encoder
+        rhi.execute_graphic_node(self.device, encoder, self.pipeline, [color], depth, job)
+        return encoder
 
 
 def render_scene(device: rhi.RenderDevice, scene: Scene, shard: Optional[tuple] = None, viewport=None,

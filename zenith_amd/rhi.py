@@ -74,6 +74,16 @@ class RenderDevice:
     def stream(self) -> int:
         return lib().zr_device_stream(self.handle) or 0
 
+    def init_rccl(self, exchange_id: bytes, gather_id: bytes, nranks: int, rank: int):
+        """Joins the runtime's RCCL communicators (collective over all ranks; the ids
+        come from rank 0's :func:`zenith_amd.zr` ``zr_rccl_get_unique_id``)."""
+        check(lib().zr_device_init_rccl(self.handle, exchange_id, gather_id, nranks, rank), "zr_device_init_rccl")
+
+    def gather_tile_rows(self, texture: "Texture", root: int = 0):
+        """Sends this rank's tile rows of ``texture`` into the root's (RCCL, on the
+        runtime's gather stream; the next pass writing ``texture`` waits for it)."""
+        check(lib().zr_device_gather_tile_rows(self.handle, texture.handle, root), "zr_device_gather_tile_rows")
+
     def submit(self, encoder: "CommandEncoder", fence: Optional["Fence"] = None):
         check(lib().zr_submit(self.handle, encoder.handle, fence.handle if fence else None), "zr_submit")
 
@@ -548,6 +558,9 @@ class CommandEncoder:
         the ranks too and routed through that all-to-all."""
         if exchange is None:
             lib().zr_cmd_set_tile_shard(self.handle, rank, count)
+        elif exchange == "rccl":  # the runtime's own all-to-all (RenderDevice.init_rccl)
+            lib().zr_cmd_set_tile_shard_exchange(self.handle, rank, count, lib().zr_rccl_exchange_fn(),
+                                                 self.device.handle)
         else:
             cb = exchange.c_callback()
             self._keep.append(cb)  # the callback must outlive every submission of this list

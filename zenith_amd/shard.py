@@ -23,8 +23,8 @@ def owned_rows(height: int, rank: int, world: int, tile: int = TILE, device=None
 class TileRowGather:
     """Pre-plans the row index lists and receive buffers for one image shape."""
 
-    def __init__(self, height: int, row_bytes: int, rank: int, world: int, device, tile: int = TILE):
-        self.rank, self.world = rank, world
+    def __init__(self, height: int, row_bytes: int, rank: int, world: int, device, tile: int = TILE, group=None):
+        self.rank, self.world, self.group = rank, world, group
         self.rows = [owned_rows(height, r, world, tile, device) for r in range(world)]
         self.send_buf = torch.empty((len(self.rows[rank]), row_bytes), dtype=torch.uint8, device=device)
         self.recv_bufs = None
@@ -36,15 +36,16 @@ class TileRowGather:
         """image: [H, row_bytes] uint8, fully valid on rank 0 afterwards."""
         if self.world == 1:
             return
+        peer = (lambda r: dist.get_global_rank(self.group, r)) if self.group is not None else (lambda r: r)
         if self.rank == 0:
-            ops = [dist.P2POp(dist.irecv, self.recv_bufs[r], r) for r in range(1, self.world)]
+            ops = [dist.P2POp(dist.irecv, self.recv_bufs[r], peer(r), group=self.group) for r in range(1, self.world)]
             for req in dist.batch_isend_irecv(ops):
                 req.wait()
             for r in range(1, self.world):
                 image.index_copy_(0, self.rows[r], self.recv_bufs[r])
         else:
             torch.index_select(image, 0, self.rows[self.rank], out=self.send_buf)
-            for req in dist.batch_isend_irecv([dist.P2POp(dist.isend, self.send_buf, 0)]):
+            for req in dist.batch_isend_irecv([dist.P2POp(dist.isend, self.send_buf, peer(0), group=self.group)]):
                 req.wait()
 
 
@@ -203,3 +204,22 @@ class ThreadGroupExchange(Exchange):
             r[s * nbytes:(s + 1) * nbytes].copy_(src)
         torch.cuda.synchronize(g.device)
         g.barrier.wait()  # every rank copied before any send buffer is rewritten
+
+
+def init_runtime_rccl(device, rank: int, world: int, group=None) -> None:
+    """Gives ``device`` (rhi.RenderDevice) the runtime's own RCCL communicators:
+    rank 0 makes the two ids, torch.distributed carries them to every rank, and
+    every rank joins (zr_device_init_rccl).  After this, tile-row shards can use
+    exchange="rccl" and RenderDevice.gather_tile_rows."""
+    import ctypes as C
+    from . import zr
+    ids = [None]
+    if rank == 0:
+        a = C.create_string_buffer(zr.RCCL_ID_BYTES)
+        b = C.create_string_buffer(zr.RCCL_ID_BYTES)
+        zr.check(zr.lib().zr_rccl_get_unique_id(a), "zr_rccl_get_unique_id")
+        zr.check(zr.lib().zr_rccl_get_unique_id(b), "zr_rccl_get_unique_id")
+        ids = [(a.raw, b.raw)]
+    if world > 1:
+        dist.broadcast_object_list(ids, src=0, group=group)
+    device.init_rccl(ids[0][0], ids[0][1], world, rank)

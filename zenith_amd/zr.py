@@ -160,6 +160,7 @@ class zr_rendering_info(C.Structure):
 
 # zr_exchange_fn (include/zenith_raster.h): (user, hip_stream, send, recv, bytes_per_rank) -> zr_result
 EXCHANGE_FN = C.CFUNCTYPE(C.c_int32, C.c_void_p, C.c_void_p, C.c_void_p, C.c_void_p, C.c_uint64)
+RCCL_ID_BYTES = 128
 
 
 # ------------------------------------------------------------------- loading
@@ -213,6 +214,10 @@ _SIGS = {
     "zr_cmd_set_tile_shard_exchange": (None, [_P, C.c_uint32, C.c_uint32, _P, _P]),
     "zr_device_set_stream": (_R, [_P, _P]),
     "zr_device_stream": (_P, [_P]),
+    "zr_rccl_get_unique_id": (_R, [_P]),
+    "zr_device_init_rccl": (_R, [_P, _P, _P, C.c_int32, C.c_int32]),
+    "zr_rccl_exchange_fn": (_P, []),
+    "zr_device_gather_tile_rows": (_R, [_P, _P, C.c_int32]),
     "zr_fence_create": (_R, [_P, C.POINTER(_P)]),
     "zr_fence_destroy": (None, [_P]),
     "zr_submit": (_R, [_P, _P, _P]),
