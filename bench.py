@@ -43,9 +43,10 @@ def parse():
     p.add_argument("--emulate-shard", type=int, default=0, metavar="G",
                    help="diagnostic (1 GPU): run only rank 0's share of a G-way tile-row shard, no gather "
                         "(partitioned setup: rank 0's routed block stands in for every source's)")
-    p.add_argument("--setup", choices=["partitioned", "replicated"], default="partitioned",
-                   help="tile-row shards: route 1/G of the primitives per rank through an RCCL all-to-all "
-                        "(DESIGN.md §7), or set up every primitive on every rank")
+    p.add_argument("--setup", choices=["partitioned", "replicated"], default="replicated",
+                   help="tile-row shards: set up every primitive on every rank (binning only its own rows), "
+                        "or route 1/G of the primitives per rank through an RCCL all-to-all (DESIGN.md §7; "
+                        "1-GPU emulation: equal at G=8, slower at G=2/4, before the all-to-all's own cost)")
     p.add_argument("--comm", choices=["runtime", "torch"], default="runtime",
                    help="multi-GPU collectives: the runtime's own RCCL communicators (exchange + row gather "
                         "enqueued from C++), or torch.distributed's (Python callbacks)")

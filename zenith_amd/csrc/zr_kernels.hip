@@ -33,6 +33,9 @@ namespace zr {
 #ifndef ZR_TILE_LPT
 #define ZR_TILE_LPT 1        // waves claim raster chunks largest-first from an LDS counter (0: static)
 #endif
+#ifndef ZR_TILE_SUBLANE
+#define ZR_TILE_SUBLANE 1    // sparse segments: k lanes per entry split its bbox rows (0: one lane per entry)
+#endif
 #ifndef ZR_EXP_EXTRA_VALU
 #define ZR_EXP_EXTRA_VALU 0  // experiment only: dummy VALU ops per lane-raster step
 #endif
@@ -912,17 +915,20 @@ __device__ __forceinline__ void raster_prim(const DrawParams& P, const TriRecord
 // Lane-parallel path for small primitives (kFlagSmall): each lane walks its own
 // primitive's bbox ∩ tile in row order, stepping the three edge functions
 // incrementally in int32 (exact: |w| <= 2^29 inside a small primitive's bbox).
+// With k = 2^ksh lanes per primitive (sparse tiles), lane `sub` of the
+// primitive's group takes the bbox rows sub, sub + k, ...
 template <int MODE, bool INITD>
 __device__ __forceinline__ void raster_lane(const DrawParams& P, const TriRecord& r, uint32_t seq, int x0, int y0,
-                                            unsigned long long* s_key, const float* s_initd) {
+                                            unsigned long long* s_key, const float* s_initd, int sub, int ksh) {
+    const int k = 1 << ksh;
     const int X0 = r.X0, Y0 = r.Y0, X1 = r.X1, Y1 = r.Y1, X2 = r.X2, Y2 = r.Y2;
     const float z0 = r.z0, dz1 = r.dz1, dz2 = r.dz2, invA2 = r.invA2;
     const uint32_t bb0 = r.bb0, bb1 = r.bb1, flags = r.flags;
     const int bx0 = max((int)(bb0 & 0xFFFFu), x0), by0 = max((int)(bb0 >> 16), y0);
     const int bx1 = min((int)(bb1 & 0xFFFFu), x0 + kTile - 1), by1 = min((int)(bb1 >> 16), y0 + kTile - 1);
     const int bw = bx1 - bx0 + 1, bh = by1 - by0 + 1;
-    if (bw <= 0 || bh <= 0) return;
-    const int Sx = bx0 * 256 + 128, Sy = by0 * 256 + 128;
+    if (bw <= 0 || bh <= sub) return;
+    const int Sx = bx0 * 256 + 128, Sy = (by0 + sub) * 256 + 128;
     const int dx0 = X2 - X1, dy0 = Y2 - Y1, dx1 = X0 - X2, dy1 = Y0 - Y2, dx2 = X1 - X0, dy2 = Y1 - Y0;
     int r0 = dx0 * (Sy - Y1) - dy0 * (Sx - X1);
     int r1 = dx1 * (Sy - Y2) - dy1 * (Sx - X2);
@@ -936,12 +942,12 @@ __device__ __forceinline__ void raster_lane(const DrawParams& P, const TriRecord
     // values, so coverage is one sign test; depth adds it back.  Fragment depth is
     // never -0 here: setup canonicalised the vertex depths to +0 (the oracle's
     // per-fragment -0 -> +0 rule therefore gives the same bits).
-    const int n = bw * bh;
-    const int j0 = sy0 - (bw - 1) * sx0, j1 = sy1 - (bw - 1) * sx1, j2 = sy2 - (bw - 1) * sx2;
+    const int n = bw * ((bh - sub + k - 1) >> ksh);
+    const int j0 = k * sy0 - (bw - 1) * sx0, j1 = k * sy1 - (bw - 1) * sx1, j2 = k * sy2 - (bw - 1) * sx2;
     int w0 = r0 - b0, w1 = r1 - b1, w2 = r2 - b2;
     int ex = 0;
-    uint32_t la = (uint32_t)(((by0 - y0) * kTile + (bx0 - x0)) * 8);  // byte offset of the key
-    const uint32_t lj = (uint32_t)((kTile - bw + 1) * 8);
+    uint32_t la = (uint32_t)(((by0 + sub - y0) * kTile + (bx0 - x0)) * 8);  // byte offset of the key
+    const uint32_t lj = (uint32_t)((k * kTile - bw + 1) * 8);
     for (int k = 0; k < n; ++k) {
         if ((w0 | w1 | w2) >= 0) {
             const float fb1 = (float)(w1 + b1) * invA2, fb2 = (float)(w2 + b2) * invA2;
@@ -1152,9 +1158,14 @@ __global__ __launch_bounds__(NT, ZR_TILE_WGS * kTileThreads / NT) void k_tile(Dr
             // Waves claim 64-entry chunks from an LDS counter, largest bboxes first
             // (the sort put them last): longest-processing-time-first balances the
             // waves of a tile.  One lane per entry loads its 32-B compact record.
-            // With no more chunks than waves each wave takes one statically (measured
-            // faster there: C1 78 vs 85 us, C3 299 vs 304 us; LPT: C2 80 vs 82 us).
-            const uint32_t nch = (n + 63u) / 64u;
+            // A sparse segment (fewer entries than lanes) gives each entry k lanes,
+            // which split its bbox rows.  With no more chunks than waves each wave
+            // takes one statically (measured faster there: C1 78 vs 85 us, C3 299
+            // vs 304 us; LPT: C2 80 vs 82 us).
+            const uint32_t kl = ZR_TILE_SUBLANE ? min(8u, max(1u, (uint32_t)NT / max(n, 1u))) : 1u;
+            const uint32_t ksh = 31u - __clz(kl);  // lanes per entry: 1, 2, 4 or 8
+            const uint32_t per = 64u >> ksh;       // entries per chunk
+            const uint32_t nch = (n + per - 1u) / per;
             const bool lpt = ZR_TILE_LPT && nch > NT / 64u;
             for (uint32_t it = 0;; ++it) {
                 uint32_t claim = wave + it * (NT / 64u);  // static: wave w takes chunks w, w + waves, ...
@@ -1163,8 +1174,9 @@ __global__ __launch_bounds__(NT, ZR_TILE_WGS * kTileThreads / NT) void k_tile(Dr
                     claim = (uint32_t)__builtin_amdgcn_readfirstlane((int)claim);
                 }
                 if (claim >= nch) break;
-                const uint32_t cb = (lpt ? nch - 1u - claim : claim) * 64u;
-                const uint32_t j = cb + (uint32_t)lane;
+                const uint32_t cb = (lpt ? nch - 1u - claim : claim) * per;
+                const uint32_t j = cb + ((uint32_t)lane >> ksh);
+                const int sub = lane & ((1 << ksh) - 1);
                 uint32_t my_prim = 0;
                 int4 q0 = make_int4(0, 0, 0, 0), q1 = q0;
                 if (j < n) {
@@ -1178,10 +1190,10 @@ __global__ __launch_bounds__(NT, ZR_TILE_WGS * kTileThreads / NT) void k_tile(Dr
                 const bool large = compact_is_large(q0);
                 if (valid && !large) {
                     const TriRecord r = decode_compact(P, q0, q1, true);
-                    raster_lane<MODE, INITD>(P, r, my_prim + 1u, x0, y0, s_key, s_initd);
+                    raster_lane<MODE, INITD>(P, r, my_prim + 1u, x0, y0, s_key, s_initd, sub, (int)ksh);
                 }
                 // large primitives: the whole wave sweeps one primitive at a time (full record)
-                unsigned long long big = __ballot(valid && large);
+                unsigned long long big = __ballot(valid && large && sub == 0);
                 while (big) {
                     const uint32_t i = (uint32_t)__builtin_ctzll(big);
                     big &= big - 1ull;
@@ -1210,7 +1222,8 @@ __global__ __launch_bounds__(NT, ZR_TILE_WGS * kTileThreads / NT) void k_tile(Dr
                     s_any = j;
                 }
                 const bool large = compact_is_large(q0);
-                if (hit && !large) raster_lane<MODE, INITD>(P, decode_compact(P, q0, q1, true), j + 1u, x0, y0, s_key, s_initd);
+                if (hit && !large)
+                    raster_lane<MODE, INITD>(P, decode_compact(P, q0, q1, true), j + 1u, x0, y0, s_key, s_initd, 0, 0);
                 unsigned long long big = __ballot(hit && large);
                 while (big) {
                     const uint32_t i = (uint32_t)__builtin_ctzll(big);
