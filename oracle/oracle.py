@@ -24,7 +24,7 @@ class _Target(C.Structure):
 
 class _VertexInput(C.Structure):
     _fields_ = [("vertex_data", C.c_void_p), ("vertex_bytes", C.c_uint64), ("stride", C.c_uint32),
-                ("attr_count", C.c_uint32), ("attr_offset", C.c_uint32 * 4),
+                ("attr_count", C.c_uint32), ("attr_offset", C.c_uint32 * 4), ("attr_size", C.c_uint32 * 4),
                 ("index_data", C.c_void_p), ("index_bytes", C.c_uint64), ("index_type", C.c_int32)]
 
 
@@ -34,7 +34,7 @@ class _DrawState(C.Structure):
                 ("cull_mode", C.c_uint32), ("front_face", C.c_int32),
                 ("depth_test", C.c_uint32), ("depth_write", C.c_uint32), ("depth_op", C.c_int32),
                 ("color_write_mask", C.c_uint32), ("tile_size", C.c_uint32),
-                ("shard_rank", C.c_uint32), ("shard_count", C.c_uint32)]
+                ("shard_rank", C.c_uint32), ("shard_count", C.c_uint32), ("view_proj", C.c_float * 16)]
 
 
 class _DrawCmd(C.Structure):
@@ -132,9 +132,11 @@ def render(scene, tile_size: int = 32, shard=(0, 1), nthreads: int = 1, with_sta
                 1 if scene.depth else 0, tile_size, shard[0], shard[1])
     vb = np.ascontiguousarray(scene.vertices, dtype=np.float32)
     ib = None if scene.indices is None else np.ascontiguousarray(scene.indices)
-    nat = vb.shape[1] // 3
-    offs = (C.c_uint32 * 4)(*[12 * a for a in range(nat)], *([0] * (4 - nat)))
-    vi = _VertexInput(vb.ctypes.data, vb.nbytes, vb.shape[1] * 4, nat, offs,
+    layout = scene.layout
+    nat = len(layout)
+    offs = (C.c_uint32 * 4)(*[4 * sum(layout[:a]) for a in range(nat)], *([0] * (4 - nat)))
+    sizes = (C.c_uint32 * 4)(*[4 * n for n in layout], *([0] * (4 - nat)))
+    vi = _VertexInput(vb.ctypes.data, vb.nbytes, vb.shape[1] * 4, nat, offs, sizes,
                       ib.ctypes.data if ib is not None else None, ib.nbytes if ib is not None else 0,
                       scene.index_type)
     vp = viewport or (0.0, 0.0, float(W), float(H), 0.0, 1.0)
@@ -142,7 +144,7 @@ def render(scene, tile_size: int = 32, shard=(0, 1), nthreads: int = 1, with_sta
     st = _DrawState(scene.program, scene.time, (C.c_float * 6)(*vp), (C.c_int32 * 4)(*sc), ra_c,
                     scene.cull_mode, scene.front_face, 1 if scene.depth_test else 0,
                     1 if scene.depth_write else 0, scene.depth_op, scene.write_mask, tile_size,
-                    shard[0], shard[1])
+                    shard[0], shard[1], (C.c_float * 16)(*(scene.view_proj or (0.0,) * 16)))
     cmd = _DrawCmd(scene.draw_count, scene.instance_count, scene.first, scene.vertex_offset, 0,
                    1 if ib is not None else 0)
     stats = Stats()

@@ -156,9 +156,12 @@ void zro_clear(const zro_target *t, const int32_t ra[4], const float cc[4], int 
 
 /* ------------------------------------------------------------ shader stages */
 
-/* Vertex stage of every built-in program: SV_Position = float4(position, 1)
- * (triangle.slang:21-22).  Varyings are the remaining float3 inputs. */
-static int program_attr_count(int32_t p) { return p == ZRO_PROGRAM_BLINN_PHONG ? 3 : 2; }
+/* Vertex stages: SV_Position = float4(position, 1) (triangle.slang:21-22) for the
+ * triangle / flat / Blinn-Phong programs; mul(View.view_proj, float4(position, 1))
+ * for mesh.slang.  Varyings are the remaining inputs. */
+static int program_attr_count(int32_t p) {
+    return (p == ZRO_PROGRAM_BLINN_PHONG || p == ZRO_PROGRAM_MESH) ? 3 : 2;
+}
 
 typedef struct tri_setup {
     int32_t X[3], Y[3];
@@ -166,66 +169,44 @@ typedef struct tri_setup {
     float invA2;
     int32_t bias[3];
     int32_t px0, py0, px1, py1;
-    uint32_t vid[3];
+    uint32_t vid[3];     /* record order (after the orientation swap)                  */
+    uint32_t ovid[3];    /* mesh: the primitive's vertex ids in API order               */
+    float clip[3][4];    /* mesh: the primitive's clip-space vertices in API order      */
     int32_t valid;
 } tri_setup;
 
-static const float *fetch3(const zro_vertex_input *vi, uint32_t vid, uint32_t loc) {
+static const float *fetchv(const zro_vertex_input *vi, uint32_t vid, uint32_t loc) {
+    const uint32_t size = vi->attr_size[loc] ? vi->attr_size[loc] : 12u;
     const uint64_t off = (uint64_t)vid * vi->stride + vi->attr_offset[loc];
-    if (off + 12 > vi->vertex_bytes) return NULL;
+    if (off + size > vi->vertex_bytes) return NULL;
     return (const float *)(vi->vertex_data + off);
 }
 
-/* Primitive assembly + vertex stage + viewport + snap + facing/cull + bbox.
- * Returns 1 if the triangle may produce fragments. */
-static int setup_triangle(const zro_target *t, const zro_draw_state *s, const zro_vertex_input *vi,
-                          const zro_draw_cmd *cmd, uint32_t tri, tri_setup *o, int *dropped_clip) {
-    *dropped_clip = 0;
-    o->valid = 0;
-    const int nattr = program_attr_count(s->program);
-    if (vi->attr_count < (uint32_t)nattr) return 0;
-    for (int k = 0; k < 3; ++k) {
-        const uint64_t e = (uint64_t)cmd->first + (uint64_t)tri * 3u + (uint64_t)k;
-        int64_t v;
-        if (cmd->indexed) {
-            const uint32_t isz = vi->index_type == 0 ? 2u : 4u;
-            if ((e + 1) * isz > vi->index_bytes) return 0;
-            const uint32_t ix = isz == 2 ? ((const uint16_t *)vi->index_data)[e]
-                                         : ((const uint32_t *)vi->index_data)[e];
-            v = (int64_t)ix + (int64_t)cmd->vertex_offset;
-        } else {
-            v = (int64_t)e;
-        }
-        if (v < 0 || v > 0xFFFFFFFFll) return 0;
-        o->vid[k] = (uint32_t)v;
-        for (int a = 0; a < nattr; ++a)
-            if (!fetch3(vi, o->vid[k], (uint32_t)a)) return 0;
-    }
-    /* viewport transform, Vulkan 1.3 §Controlling the Viewport */
-    const float hw = s->viewport[2] * 0.5f, hh = s->viewport[3] * 0.5f;
-    const float cx = s->viewport[0] + hw, cy = s->viewport[1] + hh;
-    const float dr = s->viewport[5] - s->viewport[4], dmin = s->viewport[4];
-    for (int k = 0; k < 3; ++k) {
-        const float *pos = fetch3(vi, o->vid[k], 0);
-        const float x = pos[0], y = pos[1], z = pos[2], w = 1.0f; /* vsmain */
-        if (!(w > 0.0f)) { *dropped_clip = 1; return 0; }
-        const float xd = x / w, yd = y / w, zd = z / w;
-        const float xf = fmaf(xd, hw, cx), yf = fmaf(yd, hh, cy);
-        if (!(fabsf(xf) < 4194304.0f && fabsf(yf) < 4194304.0f)) { *dropped_clip = 1; return 0; }
-        o->X[k] = zro_snap(xf);
-        o->Y[k] = zro_snap(yf);
-        o->z[k] = fmaf(zd, dr, dmin);
-        o->invw[k] = 1.0f / w;
-    }
-    int64_t A2 = (int64_t)(o->X[1] - o->X[0]) * (o->Y[2] - o->Y[0]) -
-                 (int64_t)(o->X[2] - o->X[0]) * (o->Y[1] - o->Y[0]);
+/* scissor ∩ render area ∩ attachment, inclusive */
+static void clip_rect(const zro_target *t, const zro_draw_state *s, int32_t r[4]) {
+    int32_t cx0 = s->scissor[0], cy0 = s->scissor[1];
+    int32_t cx1 = s->scissor[0] + s->scissor[2] - 1, cy1 = s->scissor[1] + s->scissor[3] - 1;
+    if (s->render_area[0] > cx0) cx0 = s->render_area[0];
+    if (s->render_area[1] > cy0) cy0 = s->render_area[1];
+    if (s->render_area[0] + s->render_area[2] - 1 < cx1) cx1 = s->render_area[0] + s->render_area[2] - 1;
+    if (s->render_area[1] + s->render_area[3] - 1 < cy1) cy1 = s->render_area[1] + s->render_area[3] - 1;
+    if (cx0 < 0) cx0 = 0;
+    if (cy0 < 0) cy0 = 0;
+    if (cx1 > (int32_t)t->width - 1) cx1 = (int32_t)t->width - 1;
+    if (cy1 > (int32_t)t->height - 1) cy1 = (int32_t)t->height - 1;
+    r[0] = cx0; r[1] = cy0; r[2] = cx1; r[3] = cy1;
+}
+
+static int64_t area2(const int32_t X[3], const int32_t Y[3]) {
+    return (int64_t)(X[1] - X[0]) * (Y[2] - Y[0]) - (int64_t)(X[2] - X[0]) * (Y[1] - Y[0]);
+}
+
+/* Orientation (A2 > 0, v0 keeps its slot), top-left biases and clipped pixel bbox
+ * of one snapped triangle whose facing was already tested.  1 if it can cover. */
+static int finish_tri(const zro_target *t, const zro_draw_state *s, tri_setup *o) {
+    int64_t A2 = area2(o->X, o->Y);
     if (A2 == 0) return 0;
-    /* Vulkan facing: a = -1/2 sum(x_i y_{i+1} - x_{i+1} y_i) = -A2/2; a > 0 is CCW. */
-    const int ccw = A2 < 0;
-    const int front = (s->front_face == 0) ? ccw : !ccw;
-    if ((s->cull_mode & 1u) && front) return 0;
-    if ((s->cull_mode & 2u) && !front) return 0;
-    if (A2 < 0) { /* orient to A2 > 0; v0 (provoking) keeps its slot */
+    if (A2 < 0) {
         int32_t ti; float tf; uint32_t tu;
         ti = o->X[1]; o->X[1] = o->X[2]; o->X[2] = ti;
         ti = o->Y[1]; o->Y[1] = o->Y[2]; o->Y[2] = ti;
@@ -249,28 +230,156 @@ static int setup_triangle(const zro_target *t, const zro_draw_state *s, const zr
         if (o->Y[k] < minY) minY = o->Y[k];
         if (o->Y[k] > maxY) maxY = o->Y[k];
     }
-    /* pixel centres (p + 1/2) inside the fixed-point bbox */
+    /* pixel centres (p + 1/2) inside the fixed-point bbox, within the clip rect */
+    int32_t cr[4];
+    clip_rect(t, s, cr);
     int32_t px0 = (minX - 128 + 255) >> 8, px1 = (maxX - 128) >> 8;
     int32_t py0 = (minY - 128 + 255) >> 8, py1 = (maxY - 128) >> 8;
-    /* scissor ∩ render area ∩ attachment */
-    int32_t cx0 = s->scissor[0], cy0 = s->scissor[1];
-    int32_t cx1 = s->scissor[0] + s->scissor[2] - 1, cy1 = s->scissor[1] + s->scissor[3] - 1;
-    if (s->render_area[0] > cx0) cx0 = s->render_area[0];
-    if (s->render_area[1] > cy0) cy0 = s->render_area[1];
-    if (s->render_area[0] + s->render_area[2] - 1 < cx1) cx1 = s->render_area[0] + s->render_area[2] - 1;
-    if (s->render_area[1] + s->render_area[3] - 1 < cy1) cy1 = s->render_area[1] + s->render_area[3] - 1;
-    if (cx0 < 0) cx0 = 0;
-    if (cy0 < 0) cy0 = 0;
-    if (cx1 > (int32_t)t->width - 1) cx1 = (int32_t)t->width - 1;
-    if (cy1 > (int32_t)t->height - 1) cy1 = (int32_t)t->height - 1;
-    if (px0 < cx0) px0 = cx0;
-    if (py0 < cy0) py0 = cy0;
-    if (px1 > cx1) px1 = cx1;
-    if (py1 > cy1) py1 = cy1;
+    if (px0 < cr[0]) px0 = cr[0];
+    if (py0 < cr[1]) py0 = cr[1];
+    if (px1 > cr[2]) px1 = cr[2];
+    if (py1 > cr[3]) py1 = cr[3];
     if (px0 > px1 || py0 > py1) return 0;
     o->px0 = px0; o->py0 = py0; o->px1 = px1; o->py1 = py1;
     o->valid = 1;
     return 1;
+}
+
+/* Vertex ids of draw primitive `tri` (API order); 0 if an index is out of range. */
+static int fetch_ids(const zro_vertex_input *vi, const zro_draw_cmd *cmd, uint32_t tri, int nattr, uint32_t vid[3]) {
+    for (int k = 0; k < 3; ++k) {
+        const uint64_t e = (uint64_t)cmd->first + (uint64_t)tri * 3u + (uint64_t)k;
+        int64_t v;
+        if (cmd->indexed) {
+            const uint32_t isz = vi->index_type == 0 ? 2u : 4u;
+            if ((e + 1) * isz > vi->index_bytes) return 0;
+            const uint32_t ix = isz == 2 ? ((const uint16_t *)vi->index_data)[e]
+                                         : ((const uint32_t *)vi->index_data)[e];
+            v = (int64_t)ix + (int64_t)cmd->vertex_offset;
+        } else {
+            v = (int64_t)e;
+        }
+        if (v < 0 || v > 0xFFFFFFFFll) return 0;
+        vid[k] = (uint32_t)v;
+        for (int a = 0; a < nattr; ++a)
+            if (!fetchv(vi, vid[k], (uint32_t)a)) return 0;
+    }
+    return 1;
+}
+
+/* mesh.slang vsmain: clip = view_proj * (p, 1), column-major M[c*4 + r]; per row
+ * t = M0r*x, t = fma(M1r, y, t), t = fma(M2r, z, t), c_r = t + M3r. */
+static void transform(const float *M, const float *p, float c[4]) {
+    for (int r = 0; r < 4; ++r) {
+        float t = M[r] * p[0];
+        t = fmaf(M[4 + r], p[1], t);
+        t = fmaf(M[8 + r], p[2], t);
+        c[r] = t + M[12 + r];
+    }
+}
+
+/* Sutherland-Hodgman against the Vulkan depth planes z >= 0, then z <= w (x and y
+ * use the guard band), vertex order kept from v0; new vertex a + t (b - a),
+ * t = da / (da - db).  Returns the polygon size (0, 3, 4 or 5). */
+static int clip_polygon(const float in[3][4], float out[5][4]) {
+    float a_[5][4], b_[5][4];
+    int n = 3;
+    memcpy(a_, in, sizeof(float) * 12);
+    for (int plane = 0; plane < 2; ++plane) {
+        const float(*src)[4] = plane == 0 ? (const float(*)[4])a_ : (const float(*)[4])b_;
+        float(*dst)[4] = plane == 0 ? b_ : a_;
+        int m = 0;
+        for (int i = 0; i < n; ++i) {
+            const float *a = src[i], *b = src[(i + 1) % n];
+            const float da = plane == 0 ? a[2] : a[3] - a[2];
+            const float db = plane == 0 ? b[2] : b[3] - b[2];
+            if (da >= 0.0f) { memcpy(dst[m], a, sizeof(float) * 4); ++m; }
+            if ((da >= 0.0f) != (db >= 0.0f)) {
+                const float tt = da / (da - db);
+                for (int k = 0; k < 4; ++k) dst[m][k] = fmaf(tt, b[k] - a[k], a[k]);
+                ++m;
+            }
+        }
+        n = m;
+        if (n == 0) return 0;
+    }
+    memcpy(out, a_, sizeof(float) * 4 * (size_t)n);
+    return n;
+}
+
+/* Primitive assembly + vertex stage + clip + viewport + snap + facing/cull +
+ * bbox.  Fills up to 3 triangles (the mesh program's clipped fan; one otherwise)
+ * and returns how many may produce fragments. */
+static int setup_prim(const zro_target *t, const zro_draw_state *s, const zro_vertex_input *vi,
+                      const zro_draw_cmd *cmd, uint32_t tri, tri_setup o[3], int *dropped_clip) {
+    *dropped_clip = 0;
+    o[0].valid = o[1].valid = o[2].valid = 0;
+    const int nattr = program_attr_count(s->program);
+    if (vi->attr_count < (uint32_t)nattr) return 0;
+    uint32_t vid[3];
+    if (!fetch_ids(vi, cmd, tri, nattr, vid)) return 0;
+    /* viewport transform, Vulkan 1.3 §Controlling the Viewport */
+    const float hw = s->viewport[2] * 0.5f, hh = s->viewport[3] * 0.5f;
+    const float cx = s->viewport[0] + hw, cy = s->viewport[1] + hh;
+    const float dr = s->viewport[5] - s->viewport[4], dmin = s->viewport[4];
+    float poly[5][4];
+    int n = 3;
+    float clip[3][4];
+    for (int k = 0; k < 3; ++k) {
+        const float *pos = fetchv(vi, vid[k], 0);
+        if (s->program == ZRO_PROGRAM_MESH) {
+            transform(s->view_proj, pos, clip[k]);
+        } else {
+            clip[k][0] = pos[0]; clip[k][1] = pos[1]; clip[k][2] = pos[2]; clip[k][3] = 1.0f;
+        }
+    }
+    if (s->program == ZRO_PROGRAM_MESH) {
+        n = clip_polygon((const float(*)[4])clip, poly);
+        if (n == 0) { *dropped_clip = 1; return 0; }
+    } else {
+        memcpy(poly, clip, sizeof clip);
+    }
+    int32_t X[5], Y[5];
+    float Z[5], IW[5];
+    for (int k = 0; k < n; ++k) {
+        const float x = poly[k][0], y = poly[k][1], z = poly[k][2], w = poly[k][3];
+        if (!(w > 0.0f)) { *dropped_clip = 1; return 0; }
+        const float xd = x / w, yd = y / w, zd = z / w;
+        const float xf = fmaf(xd, hw, cx), yf = fmaf(yd, hh, cy);
+        if (!(fabsf(xf) < 4194304.0f && fabsf(yf) < 4194304.0f)) { *dropped_clip = 1; return 0; }
+        X[k] = zro_snap(xf);
+        Y[k] = zro_snap(yf);
+        Z[k] = fmaf(zd, dr, dmin) + 0.0f; /* -0 -> +0 */
+        IW[k] = 1.0f / w;
+    }
+    /* Vulkan facing of the (clipped) polygon: a = -1/2 sum(x_i y_{i+1} - x_{i+1} y_i),
+     * summed over its fan as -A2/2 each; a > 0 is CCW. */
+    int64_t Asum = 0;
+    for (int k = 1; k + 1 < n; ++k) {
+        const int32_t fx[3] = {X[0], X[k], X[k + 1]}, fy[3] = {Y[0], Y[k], Y[k + 1]};
+        Asum += area2(fx, fy);
+    }
+    if (Asum == 0) return 0;
+    const int ccw = Asum < 0;
+    const int front = (s->front_face == 0) ? ccw : !ccw;
+    if ((s->cull_mode & 1u) && front) return 0;
+    if ((s->cull_mode & 2u) && !front) return 0;
+    int nvalid = 0;
+    for (int k = 1; k + 1 < n; ++k) {
+        tri_setup *f = &o[k - 1];
+        const int idx[3] = {0, k, k + 1};
+        for (int j = 0; j < 3; ++j) {
+            f->X[j] = X[idx[j]];
+            f->Y[j] = Y[idx[j]];
+            f->z[j] = Z[idx[j]];
+            f->invw[j] = IW[idx[j]];
+            f->vid[j] = vid[j];     /* unclipped (n == 3): the primitive's own vertices */
+            f->ovid[j] = vid[j];
+            for (int c = 0; c < 4; ++c) f->clip[j][c] = clip[j][c];
+        }
+        nvalid += finish_tri(t, s, f);
+    }
+    return nvalid;
 }
 
 static int depth_pass(int32_t op, float z, float d) {
@@ -295,36 +404,10 @@ static void interp3(const float *f0, const float *f1, const float *f2, const flo
     for (int i = 0; i < 3; ++i) out[i] = ((pw[0] * f0[i] + pw[1] * f1[i]) + pw[2] * f2[i]) * inv;
 }
 
-/* Fragment stage for each built-in program. */
-static void shade(const zro_draw_state *s, const zro_vertex_input *vi, const tri_setup *o,
-                  int64_t w0, int64_t w1, int64_t w2, float out[4]) {
-    const float b0 = (float)w0 * o->invA2, b1 = (float)w1 * o->invA2, b2 = (float)w2 * o->invA2;
-    const float pw[3] = {b0 * o->invw[0], b1 * o->invw[1], b2 * o->invw[2]};
-    const float inv = 1.0f / ((pw[0] + pw[1]) + pw[2]);
-    out[3] = 1.0f;
-    if (s->program == ZRO_PROGRAM_FLAT_COLOR) {
-        /* flat_color.slang: nointerpolation colour from the provoking (first) vertex */
-        const float *c = fetch3(vi, o->vid[0], 1);
-        out[0] = c[0]; out[1] = c[1]; out[2] = c[2];
-        return;
-    }
-    if (s->program == ZRO_PROGRAM_TRIANGLE) {
-        /* triangle.slang:34-38: animated = c * (0.5 + 0.5*sin(Time.time*3 + c*6.28)) */
-        float c[3];
-        interp3(fetch3(vi, o->vid[0], 1), fetch3(vi, o->vid[1], 1), fetch3(vi, o->vid[2], 1), pw, inv, c);
-        const float t3 = s->time * 3.0f;
-        for (int i = 0; i < 3; ++i) {
-            const float arg = t3 + c[i] * 6.28f;
-            out[i] = c[i] * (0.5f + 0.5f * zro_sinf(arg));
-        }
-        return;
-    }
-    /* blinn_phong.slang: kd = colour, ks = 0.5, n = 32, ambient 0.05 */
+/* blinn_phong.slang / mesh.slang lighting: ks = 0.5, n = 32, ambient 0.05 */
+static void blinn_phong(const float n[3], const float kd[3], float out[4]) {
     static const float L[3] = {0x1.3651a0p-2f, 0x1.02995cp-1f, 0x1.9dc22cp-1f}; /* norm(.3,.5,.8) */
     static const float H[3] = {0x1.465e8ap-3f, 0x1.0ff974p-2f, 0x1.e6d20ap-1f}; /* norm(L+V)     */
-    float n[3], kd[3];
-    interp3(fetch3(vi, o->vid[0], 1), fetch3(vi, o->vid[1], 1), fetch3(vi, o->vid[2], 1), pw, inv, n);
-    interp3(fetch3(vi, o->vid[0], 2), fetch3(vi, o->vid[1], 2), fetch3(vi, o->vid[2], 2), pw, inv, kd);
     const float len2 = dot3(n, n);
     const float rl = len2 > 0.0f ? 1.0f / sqrtf(len2) : 0.0f;
     const float N[3] = {n[0] * rl, n[1] * rl, n[2] * rl};
@@ -335,6 +418,71 @@ static void shade(const zro_draw_state *s, const zro_vertex_input *vi, const tri
     sp = sp * sp; sp = sp * sp; sp = sp * sp; sp = sp * sp;
     const float amb = 0.05f + ndl;
     for (int i = 0; i < 3; ++i) out[i] = kd[i] * amb + 0.5f * sp;
+    out[3] = 1.0f;
+}
+
+/* Fragment stage for each built-in program. */
+static void shade(const zro_draw_state *s, const zro_vertex_input *vi, const tri_setup *o,
+                  int64_t w0, int64_t w1, int64_t w2, int32_t pxl, int32_t pyl, float out[4]) {
+    const float b0 = (float)w0 * o->invA2, b1 = (float)w1 * o->invA2, b2 = (float)w2 * o->invA2;
+    const float pw[3] = {b0 * o->invw[0], b1 * o->invw[1], b2 * o->invw[2]};
+    const float inv = 1.0f / ((pw[0] + pw[1]) + pw[2]);
+    out[3] = 1.0f;
+    if (s->program == ZRO_PROGRAM_FLAT_COLOR) {
+        /* flat_color.slang: nointerpolation colour from the provoking (first) vertex */
+        const float *c = fetchv(vi, o->vid[0], 1);
+        out[0] = c[0]; out[1] = c[1]; out[2] = c[2];
+        return;
+    }
+    if (s->program == ZRO_PROGRAM_TRIANGLE) {
+        /* triangle.slang:34-38: animated = c * (0.5 + 0.5*sin(Time.time*3 + c*6.28)) */
+        float c[3];
+        interp3(fetchv(vi, o->vid[0], 1), fetchv(vi, o->vid[1], 1), fetchv(vi, o->vid[2], 1), pw, inv, c);
+        const float t3 = s->time * 3.0f;
+        for (int i = 0; i < 3; ++i) {
+            const float arg = t3 + c[i] * 6.28f;
+            out[i] = c[i] * (0.5f + 0.5f * zro_sinf(arg));
+        }
+        return;
+    }
+    if (s->program == ZRO_PROGRAM_MESH) {
+        /* mesh.slang: perspective-correct barycentrics of the primitive (not of
+         * its clipped fan triangle) from its homogeneous screen vertices
+         * h_i = (x_i*hw + w_i*cx, y_i*hh + w_i*cy, w_i): b_i = E_i / sum E, with
+         * E_i = p . (h_j x h_k) at the pixel centre p = (px + .5, py + .5, 1). */
+        const float hw = s->viewport[2] * 0.5f, hh = s->viewport[3] * 0.5f;
+        const float cx = s->viewport[0] + hw, cy = s->viewport[1] + hh;
+        float hX[3], hY[3], hW[3];
+        for (int k = 0; k < 3; ++k) {
+            hX[k] = fmaf(o->clip[k][0], hw, o->clip[k][3] * cx);
+            hY[k] = fmaf(o->clip[k][1], hh, o->clip[k][3] * cy);
+            hW[k] = o->clip[k][3];
+        }
+        const float fx = (float)pxl + 0.5f, fy = (float)pyl + 0.5f;
+        float E[3];
+        for (int i = 0; i < 3; ++i) {
+            const int j = (i + 1) % 3, k = (i + 2) % 3;
+            const float c0 = hY[j] * hW[k] - hW[j] * hY[k];
+            const float c1 = hW[j] * hX[k] - hX[j] * hW[k];
+            const float c2 = hX[j] * hY[k] - hY[j] * hX[k];
+            E[i] = fmaf(c0, fx, fmaf(c1, fy, c2));
+        }
+        const float einv = 1.0f / ((E[0] + E[1]) + E[2]);
+        const float bb[3] = {E[0] * einv, E[1] * einv, E[2] * einv};
+        float nrm[3], uv[2];
+        const float *n0 = fetchv(vi, o->ovid[0], 1), *n1 = fetchv(vi, o->ovid[1], 1), *n2 = fetchv(vi, o->ovid[2], 1);
+        const float *u0 = fetchv(vi, o->ovid[0], 2), *u1 = fetchv(vi, o->ovid[1], 2), *u2 = fetchv(vi, o->ovid[2], 2);
+        for (int i = 0; i < 3; ++i) nrm[i] = (bb[0] * n0[i] + bb[1] * n1[i]) + bb[2] * n2[i];
+        for (int i = 0; i < 2; ++i) uv[i] = (bb[0] * u0[i] + bb[1] * u1[i]) + bb[2] * u2[i];
+        const float kdm[3] = {fmaf(uv[0], 0.3f, 0.35f), fmaf(uv[1], 0.3f, 0.35f), 0.7f};
+        blinn_phong(nrm, kdm, out);
+        return;
+    }
+    /* blinn_phong.slang: kd = colour */
+    float n[3], kd[3];
+    interp3(fetchv(vi, o->vid[0], 1), fetchv(vi, o->vid[1], 1), fetchv(vi, o->vid[2], 1), pw, inv, n);
+    interp3(fetchv(vi, o->vid[0], 2), fetchv(vi, o->vid[1], 2), fetchv(vi, o->vid[2], 2), pw, inv, kd);
+    blinn_phong(n, kd, out);
 }
 
 /* Rasterize one set-up triangle over rows [ry0, ry1] (inclusive), in order. */
@@ -370,7 +518,7 @@ static void raster_rows(const zro_target *t, const zro_draw_state *s, const zro_
             if (st) st->fragments_passed++;
             if (t->color) {
                 float c[4];
-                shade(s, vi, o, w0, w1, w2, c);
+                shade(s, vi, o, w0, w1, w2, px, py, c);
                 store_color(t, (uint32_t)px, (uint32_t)py, c, s->color_write_mask);
             }
         }
@@ -390,7 +538,7 @@ int zro_draw(const zro_target *t, const zro_draw_state *s, const zro_vertex_inpu
     memset(&st, 0, sizeof st);
     st.triangles_in = total;
     if (total == 0) { if (stats) *stats = st; return 0; }
-    tri_setup *buf = (tri_setup *)malloc(sizeof(tri_setup) * (total < CHUNK ? total : CHUNK));
+    tri_setup *buf = (tri_setup *)malloc(sizeof(tri_setup) * 3 * (total < CHUNK ? total : CHUNK));
     if (!buf) return -1;
     const int32_t band = (int32_t)s->tile_size;
     const int32_t nbands = (int32_t)((t->height + (uint32_t)band - 1) / (uint32_t)band);
@@ -402,7 +550,7 @@ int zro_draw(const zro_target *t, const zro_draw_state *s, const zro_vertex_inpu
         for (int64_t i = 0; i < n; ++i) {
             const uint32_t tri = (uint32_t)((c0 + (uint64_t)i) % per_inst);
             int dc = 0;
-            ns += (uint64_t)setup_triangle(t, s, vi, cmd, tri, &buf[i], &dc);
+            ns += setup_prim(t, s, vi, cmd, tri, &buf[3 * i], &dc) > 0 ? 1u : 0u;
             nd += (uint64_t)dc;
         }
         st.triangles_setup += ns;
@@ -414,7 +562,7 @@ int zro_draw(const zro_target *t, const zro_draw_state *s, const zro_vertex_inpu
             memset(&ls, 0, sizeof ls);
             const int32_t ry0 = b * band, ry1 = b * band + band - 1;
             if (!row_owned((uint32_t)ry0, s->tile_size, s->shard_rank, s->shard_count)) continue;
-            for (int64_t i = 0; i < n; ++i) {
+            for (int64_t i = 0; i < 3 * n; ++i) { /* in API order; a primitive's fan triangles do not overlap */
                 const tri_setup *o = &buf[i];
                 if (!o->valid || o->py1 < ry0 || o->py0 > ry1) continue;
                 raster_rows(t, s, vi, o, ry0, ry1, &ls);

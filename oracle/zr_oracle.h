@@ -36,6 +36,8 @@ enum {
     ZRO_PROGRAM_TRIANGLE = 0,    /* content/shaders/triangle.slang vsmain/psmain      */
     ZRO_PROGRAM_FLAT_COLOR = 1,  /* content/shaders/flat_color.slang (this repo)      */
     ZRO_PROGRAM_BLINN_PHONG = 2, /* content/shaders/blinn_phong.slang (this repo)     */
+    ZRO_PROGRAM_MESH = 3,        /* content/shaders/mesh.slang: View.view_proj camera,  */
+                                 /* near/far clip, perspective-correct (this repo)      */
 };
 
 typedef struct zro_target {
@@ -49,8 +51,9 @@ typedef struct zro_vertex_input {
     const uint8_t *vertex_data;
     uint64_t vertex_bytes;
     uint32_t stride;
-    uint32_t attr_count;       /* locations 0..attr_count-1, all R32G32B32_SFLOAT    */
+    uint32_t attr_count;       /* locations 0..attr_count-1, 32-bit float vectors    */
     uint32_t attr_offset[4];
+    uint32_t attr_size[4];     /* bytes: 12 (R32G32B32_SFLOAT) or 8 (R32G32_SFLOAT)   */
     const uint8_t *index_data; /* NULL for non-indexed draws                         */
     uint64_t index_bytes;
     int32_t index_type;        /* VkIndexType: 0 = UINT16, 1 = UINT32                */
@@ -69,6 +72,7 @@ typedef struct zro_draw_state {
     uint32_t color_write_mask; /* VkColorComponentFlags                              */
     uint32_t tile_size;        /* screen-tile edge (rows are sharded in tile rows)    */
     uint32_t shard_rank, shard_count; /* tile row r is drawn iff r % count == rank  */
+    float view_proj[16];       /* mesh program: View.view_proj, column-major (glam)   */
 } zro_draw_state;
 
 typedef struct zro_draw_cmd {

@@ -35,6 +35,10 @@ def golden_scenes():
         "soup_flat_256x192": scenes.soup_scene(21, 1000, 256, 192, 12.0, scenes.PROGRAM_FLAT_COLOR),
         "soup_blinn_256x192": scenes.soup_scene(22, 1000, 256, 192, 8.0, scenes.PROGRAM_BLINN_PHONG),
         "ties_64x64": tie,
+        # mesh.slang through a camera: near-plane crossings, behind-camera and
+        # off-screen primitives, and the cerberus asset
+        "mesh_soup_160x120": scenes.mesh_soup_scene(31, 600, 160, 120),
+        "cerberus_320x240": scenes.cerberus_scene(320, 240),
     }
 
 
@@ -76,7 +80,21 @@ def render_bytes(scene):
     return blobs
 
 
+def bake_cerberus():
+    """tests/golden/cerberus.mesh.npz: /root/reference/content/mesh/cerberus/scene.gltf
+    baked as zenith-asset's gltf_loader does (zenith_amd.assets).  Only where the
+    reference is mounted; the GPU box and later rounds use the committed file."""
+    from zenith_amd import assets
+    src = "/root/reference/content/mesh/cerberus/scene.gltf"
+    if not os.path.exists(src):
+        return
+    v, i = assets.load_gltf_meshes(src)[0]
+    np.savez_compressed(os.path.join(HERE, "cerberus.mesh.npz"), vertices=v, indices=i)
+
+
 def main():
+    if "--mesh" in sys.argv:
+        bake_cerberus()
     manifest = {}
     for name, scene in golden_scenes().items():
         blobs = render_bytes(scene)

@@ -422,3 +422,38 @@ def test_runtime_rccl_world1():
         depth.destroy()
     finally:
         dev.close()
+
+
+# ------------------------------------------------ mesh program (camera, clip)
+@pytest.mark.parametrize("seed,n", [(31, 600), (32, 3000), (33, 20000)])
+def test_mesh_soup(device, seed, n):
+    """mesh.slang through a reverse-Z camera: near-plane crossings (clipped fans),
+    primitives behind the camera and beyond the view edges; bit-exact."""
+    assert_parity(device, scenes.mesh_soup_scene(seed, n, 320, 240))
+
+
+@pytest.mark.parametrize("op,write", [(scenes.OP_GEQUAL, True), (scenes.OP_ALWAYS, True), (scenes.OP_GREATER, False)])
+def test_mesh_depth_modes(device, op, write):
+    """Last-wins modes resolve depth from the winning fan triangle's record."""
+    s = scenes.mesh_soup_scene(34, 2000, 256, 192)
+    s.depth_op, s.depth_write = op, write
+    assert_parity(device, s)
+
+
+def test_mesh_cerberus(device):
+    """The reference's cerberus asset (33,543 triangles) through the camera."""
+    assert_parity(device, scenes.cerberus_scene(640, 480))
+    assert_parity(device, scenes.cerberus_scene(1920, 1080))
+
+
+def test_mesh_shards_and_spill(monkeypatch, device):
+    s = scenes.mesh_soup_scene(35, 3000, 320, 240)
+    for r in range(3):
+        assert_parity(device, s, shard=(r, 3))
+    monkeypatch.setenv("ZR_BIN_CAPACITY", "256")
+    dev = rhi.RenderDevice(0)
+    try:
+        assert_parity(dev, s)
+        assert dev.last_draw_stats()["overflowed_draws"] == 1
+    finally:
+        dev.close()

@@ -18,7 +18,14 @@ constexpr int kSetupThreads = 1024;  // setup / bin workgroups (one LDS histogra
 constexpr uint32_t kSetupLdsBudget = 160u * 1024u;     // one k_setup_bin workgroup per CU owns the LDS
 constexpr uint32_t kSetupBboxLdsBytes = 96u * 1024u;  // cap on the per-workgroup bbox array in LDS
 
-enum Program : int32_t { kProgTriangle = 0, kProgFlat = 1, kProgBlinn = 2, kProgCount = 3 };
+enum Program : int32_t { kProgTriangle = 0, kProgFlat = 1, kProgBlinn = 2, kProgMesh = 3, kProgCount = 4 };
+
+// The mesh program (camera + clipping) cuts a primitive against
+// the depth planes into a fan of up to 3 triangles.  Fan k > 0 of primitive p
+// has setup record prims + 2p + k - 1 (records are sized 3 * prims); every fan
+// triangle of p carries the visibility sequence 4p + k + 1 (API order; fans of
+// one primitive never overlap).
+constexpr uint32_t kMeshFans = 3;
 
 // Visibility-key schemes: the per-pixel 64-bit atomicMin key
 // reproduces in-order Vulkan depth-test semantics independent of fragment order.
@@ -133,6 +140,7 @@ struct DrawParams {
     uint32_t stride;
     uint32_t nattr;
     uint32_t attr_offset[4];
+    uint32_t attr_size[4];    // bytes of each input: 12 (R32G32B32_SFLOAT) or 8 (R32G32_SFLOAT)
     uint32_t index_size;      // 0 = non-indexed draw, 2 or 4
     uint32_t first;           // first_index / first_vertex
     int32_t vertex_offset;
@@ -165,6 +173,7 @@ struct DrawParams {
     // shading
     int32_t program;
     const float* time_ptr;    // Time.time uniform (device) or nullptr
+    const float* view_proj;   // mesh program: View.view_proj, 16 floats column-major (device)
     // tiling / sharding
     uint32_t tiles_x, tiles_y, shard_rank, shard_count, owned_rows, ntiles;
     uint32_t tile_threads;    // k_tile workgroup size: 256 or 512 (tile_threads_for)
@@ -214,7 +223,7 @@ inline uint32_t tile_threads_for(uint32_t ntiles, uint32_t cus) {
 // Launchers (zr_kernels.hip).  All enqueue on `stream`; no host synchronisation.
 void launch_setup_bin(const DrawParams& p, void* stream);  // persistent: setup + scan + scatter
 size_t setup_bin_lds_bytes(uint32_t ntiles, uint32_t bbox_entries);
-const void* setup_bin_kernel(uint32_t batch);
+const void* setup_bin_kernel(uint32_t batch, bool mesh);
 void launch_tile(const DrawParams& p, void* stream);
 void launch_clear(const DrawParams& p, void* stream);
 void launch_route(const DrawParams& p, void* stream);     // partitioned setup: route own range (2 kernels)

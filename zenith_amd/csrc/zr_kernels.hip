@@ -260,7 +260,7 @@ __device__ __forceinline__ void fetch_positions(const DrawParams& P, PrimIn& in)
 #pragma unroll
     for (int k = 0; k < 3; ++k)
         for (uint32_t a = 0; a < P.nattr; ++a)
-            ok = ok && ((uint64_t)in.vid[k] * P.stride + P.attr_offset[a] + 12 <= P.vb_bytes);
+            ok = ok && ((uint64_t)in.vid[k] * P.stride + P.attr_offset[a] + P.attr_size[a] <= P.vb_bytes);
     in.ok = ok;
     if (!ok) return;
 #pragma unroll
@@ -281,26 +281,12 @@ struct PrimGeom {
     int32_t px0, py0, px1, py1;
 };
 
-__device__ __forceinline__ bool prim_geometry(const DrawParams& P, const PrimIn& in, PrimGeom& g, int& ndropped) {
-    if (!in.ok) return false;
-    g.rv[0] = in.vid[0]; g.rv[1] = in.vid[1]; g.rv[2] = in.vid[2];
-#pragma unroll
-    for (int k = 0; k < 3; ++k) {
-        const float x = in.p[k].x, y = in.p[k].y, zc = in.p[k].z, w = 1.0f;  // vsmain (triangle.slang:22)
-        if (!(w > 0.0f)) { ++ndropped; return false; }
-        const float xd = x / w, yd = y / w, zd = zc / w;
-        const float xf = fmaf(xd, P.hw, P.cx), yf = fmaf(yd, P.hh, P.cy);
-        if (!(fabsf(xf) < 4194304.0f && fabsf(yf) < 4194304.0f)) { ++ndropped; return false; }
-        g.X[k] = (int32_t)rintf(xf * 256.0f);
-        g.Y[k] = (int32_t)rintf(yf * 256.0f);
-        g.z[k] = fmaf(zd, P.dr, P.dmin) + 0.0f;  // -0 -> +0 (k_tile relies on it)
-    }
+// Orientation to A2 > 0 (v1/v2 swapped, v0 kept: kFlagSwapped), top-left biases,
+// the small flag and the clipped pixel bbox of a snapped triangle whose facing
+// was already tested.  False when no pixel centre of the clip rect is inside the bbox.
+__device__ __forceinline__ bool orient_and_bound(const DrawParams& P, PrimGeom& g, long long A2) {
     int32_t* X = g.X;
     int32_t* Y = g.Y;
-    long long A2 = (long long)(X[1] - X[0]) * (Y[2] - Y[0]) - (long long)(X[2] - X[0]) * (Y[1] - Y[0]);
-    const bool ccw = A2 < 0;  // Vulkan: a = -A2/2 > 0 is counter-clockwise
-    const bool front = (P.front_face == 0) ? ccw : !ccw;
-    if (A2 == 0 || ((P.cull_mode & 1u) && front) || ((P.cull_mode & 2u) && !front)) return false;
     uint32_t flags = 0;
     if (A2 < 0) {
         int32_t t = X[1]; X[1] = X[2]; X[2] = t;
@@ -329,6 +315,213 @@ __device__ __forceinline__ bool prim_geometry(const DrawParams& P, const PrimIn&
     return g.px0 <= g.px1 && g.py0 <= g.py1;
 }
 
+__device__ __forceinline__ bool prim_geometry(const DrawParams& P, const PrimIn& in, PrimGeom& g, int& ndropped) {
+    if (!in.ok) return false;
+    g.rv[0] = in.vid[0]; g.rv[1] = in.vid[1]; g.rv[2] = in.vid[2];
+#pragma unroll
+    for (int k = 0; k < 3; ++k) {
+        const float x = in.p[k].x, y = in.p[k].y, zc = in.p[k].z, w = 1.0f;  // vsmain (triangle.slang:22)
+        if (!(w > 0.0f)) { ++ndropped; return false; }
+        const float xd = x / w, yd = y / w, zd = zc / w;
+        const float xf = fmaf(xd, P.hw, P.cx), yf = fmaf(yd, P.hh, P.cy);
+        if (!(fabsf(xf) < 4194304.0f && fabsf(yf) < 4194304.0f)) { ++ndropped; return false; }
+        g.X[k] = (int32_t)rintf(xf * 256.0f);
+        g.Y[k] = (int32_t)rintf(yf * 256.0f);
+        g.z[k] = fmaf(zd, P.dr, P.dmin) + 0.0f;  // -0 -> +0 (k_tile relies on it)
+    }
+    long long A2 = (long long)(g.X[1] - g.X[0]) * (g.Y[2] - g.Y[0]) - (long long)(g.X[2] - g.X[0]) * (g.Y[1] - g.Y[0]);
+    const bool ccw = A2 < 0;  // Vulkan: a = -A2/2 > 0 is counter-clockwise
+    const bool front = (P.front_face == 0) ? ccw : !ccw;
+    if (A2 == 0 || ((P.cull_mode & 1u) && front) || ((P.cull_mode & 2u) && !front)) return false;
+    return orient_and_bound(P, g, A2);
+}
+
+// mesh.slang vsmain: clip = view_proj * (p, 1), column-major M[c * 4 + r], per row
+// t = M0r x; t = fma(M1r, y, t); t = fma(M2r, z, t); c_r = t + M3r (zr_oracle.c).
+__device__ __forceinline__ void mesh_transform(const float* M, const float3 p, float c[4]) {
+#pragma unroll
+    for (int r = 0; r < 4; ++r) {
+        float t = M[r] * p.x;
+        t = fmaf(M[4 + r], p.y, t);
+        t = fmaf(M[8 + r], p.z, t);
+        c[r] = t + M[12 + r];
+    }
+}
+
+// Sutherland-Hodgman against the Vulkan depth planes z >= 0, then z <= w (x / y
+// use the guard band), vertex order kept from v0: new vertex a + t (b - a),
+// t = da / (da - db).  Returns the polygon size (0, 3, 4 or 5).  Only primitives
+// crossing a plane get here (mesh_geometry's fast path takes the rest).
+__device__ __noinline__ int clip_polygon(const float (*in)[4], float (*out)[4]) {
+    float a_[5][4], b_[5][4];
+    int n = 3;
+    for (int i = 0; i < 3; ++i)
+        for (int k = 0; k < 4; ++k) a_[i][k] = in[i][k];
+    for (int plane = 0; plane < 2; ++plane) {
+        float (*src)[4] = plane == 0 ? a_ : b_;
+        float (*dst)[4] = plane == 0 ? b_ : a_;
+        int m = 0;
+        for (int i = 0; i < n; ++i) {
+            const float* a = src[i];
+            const float* b = src[(i + 1) % n];
+            const float da = plane == 0 ? a[2] : a[3] - a[2];
+            const float db = plane == 0 ? b[2] : b[3] - b[2];
+            if (da >= 0.0f) {
+                for (int k = 0; k < 4; ++k) dst[m][k] = a[k];
+                ++m;
+            }
+            if ((da >= 0.0f) != (db >= 0.0f)) {
+                const float tt = da / (da - db);
+                for (int k = 0; k < 4; ++k) dst[m][k] = fmaf(tt, b[k] - a[k], a[k]);
+                ++m;
+            }
+        }
+        n = m;
+        if (n == 0) return 0;
+    }
+    for (int i = 0; i < n; ++i)
+        for (int k = 0; k < 4; ++k) out[i][k] = a_[i][k];
+    return n;
+}
+
+// The mesh program's setup geometry: vertex stage, clip, viewport, snap, facing
+// of the clipped polygon (sum of its fan's A2), cull, then each fan triangle
+// (p0, pk, pk+1) oriented and bounded on its own.  valid bit k: fan k may cover.
+struct MeshFans {
+    PrimGeom f[kMeshFans];
+    uint32_t valid;
+};
+
+__device__ __forceinline__ bool mesh_geometry(const DrawParams& P, const PrimIn& in, MeshFans& m, int& ndropped) {
+    m.valid = 0;
+    if (!in.ok) return false;
+    float c[3][4];
+#pragma unroll
+    for (int k = 0; k < 3; ++k) mesh_transform(P.view_proj, in.p[k], c[k]);
+    bool inside = true;
+#pragma unroll
+    for (int k = 0; k < 3; ++k) inside = inside && c[k][2] >= 0.0f && c[k][3] - c[k][2] >= 0.0f;
+    float poly[5][4];
+    int n = 3;
+    if (inside) {
+#pragma unroll
+        for (int k = 0; k < 3; ++k)
+#pragma unroll
+            for (int j = 0; j < 4; ++j) poly[k][j] = c[k][j];
+    } else {
+        n = clip_polygon(c, poly);
+        if (n == 0) {
+            ++ndropped;
+            return false;
+        }
+    }
+    int32_t X[5], Y[5];
+    float Z[5];
+    for (int k = 0; k < n; ++k) {
+        const float x = poly[k][0], y = poly[k][1], z = poly[k][2], w = poly[k][3];
+        if (!(w > 0.0f)) { ++ndropped; return false; }
+        const float xd = x / w, yd = y / w, zd = z / w;
+        const float xf = fmaf(xd, P.hw, P.cx), yf = fmaf(yd, P.hh, P.cy);
+        if (!(fabsf(xf) < 4194304.0f && fabsf(yf) < 4194304.0f)) { ++ndropped; return false; }
+        X[k] = (int32_t)rintf(xf * 256.0f);
+        Y[k] = (int32_t)rintf(yf * 256.0f);
+        Z[k] = fmaf(zd, P.dr, P.dmin) + 0.0f;  // -0 -> +0
+    }
+    long long Asum = 0;
+    for (int k = 1; k + 1 < n; ++k)
+        Asum += (long long)(X[k] - X[0]) * (Y[k + 1] - Y[0]) - (long long)(X[k + 1] - X[0]) * (Y[k] - Y[0]);
+    const bool ccw = Asum < 0;
+    const bool front = (P.front_face == 0) ? ccw : !ccw;
+    if (Asum == 0 || ((P.cull_mode & 1u) && front) || ((P.cull_mode & 2u) && !front)) return false;
+    for (int k = 1; k + 1 < n; ++k) {
+        PrimGeom& g = m.f[k - 1];
+        g.X[0] = X[0]; g.X[1] = X[k]; g.X[2] = X[k + 1];
+        g.Y[0] = Y[0]; g.Y[1] = Y[k]; g.Y[2] = Y[k + 1];
+        g.z[0] = Z[0]; g.z[1] = Z[k]; g.z[2] = Z[k + 1];
+        g.rv[0] = in.vid[0]; g.rv[1] = in.vid[1]; g.rv[2] = in.vid[2];
+        const long long A2 = (long long)(g.X[1] - g.X[0]) * (g.Y[2] - g.Y[0]) -
+                             (long long)(g.X[2] - g.X[0]) * (g.Y[1] - g.Y[0]);
+        if (A2 != 0 && orient_and_bound(P, g, A2)) m.valid |= 1u << (k - 1);
+    }
+    return m.valid != 0;
+}
+
+// Counts the owned (tile, primitive) pairs of a set-up triangle in the LDS
+// histogram; returns how many there are.
+__device__ __forceinline__ uint32_t count_owned(const DrawParams& P, const PrimGeom& g, uint32_t* s_hist) {
+    const int tx0 = g.px0 >> kTileShift, tx1 = g.px1 >> kTileShift;
+    const int ty0 = g.py0 >> kTileShift, ty1 = g.py1 >> kTileShift;
+    uint32_t owned = 0;
+    for (int ty = ty0; ty <= ty1; ++ty) {
+        if ((uint32_t)ty % P.shard_count != P.shard_rank) continue;
+        const uint32_t row = ((uint32_t)ty / P.shard_count) * P.tiles_x;
+        for (int tx = tx0; tx <= tx1; ++tx) atomicAdd(&s_hist[row + tx], 1u);
+        owned += (uint32_t)(tx1 - tx0 + 1);
+    }
+    return owned;
+}
+
+// Stores setup record `rec` (compact, plus the full record for a large
+// triangle) and returns its tile bbox.
+__device__ __forceinline__ BBox write_record(const DrawParams& P, uint32_t rec, const PrimGeom& g) {
+    const int32_t* X = g.X;
+    const int32_t* Y = g.Y;
+    const float invA2 = 1.0f / (float)g.A2;
+    const bool small = (g.flags & kFlagSmall) != 0u;
+    TriCompact c;
+    c.X0 = X[0]; c.Y0 = Y[0];
+    c.dx1 = small ? (int16_t)(X[1] - X[0]) : kCompactLarge;
+    c.dy1 = small ? (int16_t)(Y[1] - Y[0]) : (int16_t)0;
+    c.dx2 = small ? (int16_t)(X[2] - X[0]) : (int16_t)0;
+    c.dy2 = small ? (int16_t)(Y[2] - Y[0]) : (int16_t)0;
+    c.z0 = g.z[0];
+    c.dz1 = g.z[1] - g.z[0];
+    c.dz2 = g.z[2] - g.z[0];
+    c.invA2s = (g.flags & kFlagSwapped) ? -invA2 : invA2;
+    P.records[rec] = c;
+    BBox box;
+    box.bb0 = (uint32_t)g.px0 | ((uint32_t)g.py0 << 16);
+    box.bb1 = (uint32_t)g.px1 | ((uint32_t)g.py1 << 16);
+    if (!small) {
+        TriRecord r;
+        r.X0 = X[0]; r.Y0 = Y[0]; r.X1 = X[1]; r.Y1 = Y[1]; r.X2 = X[2]; r.Y2 = Y[2];
+        r.z0 = c.z0; r.dz1 = c.dz1; r.dz2 = c.dz2;
+        r.invA2 = invA2;
+        r.v0 = g.rv[0]; r.v1 = g.rv[1]; r.v2 = g.rv[2];
+        r.bb0 = box.bb0;
+        r.bb1 = box.bb1;
+        r.flags = g.flags;
+        P.records_big[rec] = r;
+    }
+    return box;
+}
+
+// Setup record index of fan k of mesh primitive p (zr_internal.h kMeshFans).
+__device__ __forceinline__ uint32_t mesh_record(const DrawParams& P, uint32_t p, uint32_t k) {
+    return k ? P.prims + 2u * p + k - 1u : p;
+}
+
+// The mesh program's setup of primitive `prim`: fan 0's bbox to *bbox_out, fans
+// 1 and 2's to their global slots (empty when absent).
+__device__ __forceinline__ void setup_finish_mesh(const DrawParams& P, uint32_t prim, uint32_t n_pos, const PrimIn& in,
+                                                  uint32_t* s_hist, BBox* bbox_out, int& nvalid, int& ndropped) {
+    if (prim >= n_pos) return;
+    BBox box[kMeshFans];
+#pragma unroll
+    for (uint32_t k = 0; k < kMeshFans; ++k) box[k] = BBox{kEmptyBox, 0u};
+    MeshFans m;
+    if (mesh_geometry(P, in, m, ndropped)) {
+        ++nvalid;
+        for (uint32_t k = 0; k < kMeshFans; ++k) {
+            if (!((m.valid >> k) & 1u)) continue;
+            if (count_owned(P, m.f[k], s_hist)) box[k] = write_record(P, mesh_record(P, prim, k), m.f[k]);
+        }
+    }
+    *bbox_out = box[0];
+    P.bboxes[mesh_record(P, prim, 1)] = box[1];
+    P.bboxes[mesh_record(P, prim, 2)] = box[2];
+}
+
 __device__ __forceinline__ void setup_finish(const DrawParams& P, uint32_t prim, uint32_t n_pos, uint32_t gid,
                                              const PrimIn& in, uint32_t* s_hist, BBox* bbox_out,
                                              int& nvalid, int& ndropped) {
@@ -337,45 +530,9 @@ __device__ __forceinline__ void setup_finish(const DrawParams& P, uint32_t prim,
     PrimGeom g;
     if (prim_geometry(P, in, g, ndropped)) {
         ++nvalid;
-        const int tx0 = g.px0 >> kTileShift, tx1 = g.px1 >> kTileShift;
-        const int ty0 = g.py0 >> kTileShift, ty1 = g.py1 >> kTileShift;
-        uint32_t owned = 0;
-        for (int ty = ty0; ty <= ty1; ++ty) {
-            if ((uint32_t)ty % P.shard_count != P.shard_rank) continue;
-            const uint32_t row = ((uint32_t)ty / P.shard_count) * P.tiles_x;
-            for (int tx = tx0; tx <= tx1; ++tx) atomicAdd(&s_hist[row + tx], 1u);
-            owned += (uint32_t)(tx1 - tx0 + 1);
-        }
-        if (owned) {
-            const int32_t* X = g.X;
-            const int32_t* Y = g.Y;
-            const float invA2 = 1.0f / (float)g.A2;
-            const bool small = (g.flags & kFlagSmall) != 0u;
-            TriCompact c;
-            c.X0 = X[0]; c.Y0 = Y[0];
-            c.dx1 = small ? (int16_t)(X[1] - X[0]) : kCompactLarge;
-            c.dy1 = small ? (int16_t)(Y[1] - Y[0]) : (int16_t)0;
-            c.dx2 = small ? (int16_t)(X[2] - X[0]) : (int16_t)0;
-            c.dy2 = small ? (int16_t)(Y[2] - Y[0]) : (int16_t)0;
-            c.z0 = g.z[0];
-            c.dz1 = g.z[1] - g.z[0];
-            c.dz2 = g.z[2] - g.z[0];
-            c.invA2s = (g.flags & kFlagSwapped) ? -invA2 : invA2;
-            P.records[prim] = c;
+        if (count_owned(P, g, s_hist)) {
+            box = write_record(P, prim, g);
             if (P.list) P.gids[prim] = gid;
-            box.bb0 = (uint32_t)g.px0 | ((uint32_t)g.py0 << 16);
-            box.bb1 = (uint32_t)g.px1 | ((uint32_t)g.py1 << 16);
-            if (!small) {
-                TriRecord r;
-                r.X0 = X[0]; r.Y0 = Y[0]; r.X1 = X[1]; r.Y1 = Y[1]; r.X2 = X[2]; r.Y2 = Y[2];
-                r.z0 = c.z0; r.dz1 = c.dz1; r.dz2 = c.dz2;
-                r.invA2 = invA2;
-                r.v0 = g.rv[0]; r.v1 = g.rv[1]; r.v2 = g.rv[2];
-                r.bb0 = box.bb0;
-                r.bb1 = box.bb1;
-                r.flags = g.flags;
-                P.records_big[prim] = r;
-            }
         }
     }
     *bbox_out = box;
@@ -606,7 +763,7 @@ __device__ __forceinline__ uint32_t own_unit(const DrawParams& P, uint32_t units
     return w + i * G;
 }
 
-template <uint32_t KB>
+template <uint32_t KB, bool MESH>
 __global__ __launch_bounds__(kSetupThreads) void k_setup_bin(DrawParams P) {
     extern __shared__ __attribute__((aligned(16))) uint32_t s_lds[];  // [2 * ntiles + kSetupMiscWords] + bboxes
     const uint32_t nt = P.ntiles, G = gridDim.x, w = blockIdx.x, tid = threadIdx.x;
@@ -657,7 +814,10 @@ __global__ __launch_bounds__(kSetupThreads) void k_setup_bin(DrawParams P) {
                 for (uint32_t b = 0; b < KB; ++b) {
                     const uint32_t prim = min(pb + b * 64u, n_pos);
                     BBox* out = P.bbox_lds ? &s_bbox[lb + b * 64u] : &P.bboxes[min(prim, P.prims - 1u)];
-                    setup_finish(P, prim, n_pos, gid[b], in[b], s_hist, out, nvalid, ndropped);
+                    if (MESH)
+                        setup_finish_mesh(P, prim, n_pos, in[b], s_hist, out, nvalid, ndropped);
+                    else
+                        setup_finish(P, prim, n_pos, gid[b], in[b], s_hist, out, nvalid, ndropped);
                 }
             }
         }
@@ -696,7 +856,7 @@ __global__ __launch_bounds__(kSetupThreads) void k_setup_bin(DrawParams P) {
         for (uint32_t t = tid; t < nt; t += kSetupThreads) P.tile_offsets[t] = s_base[t];
         if (tid == 0) {
             P.tile_offsets[nt] = total;
-            P.tile_offsets[nt + 1] = n_pos;  // records k_tile's overflow scan covers
+            P.tile_offsets[nt + 1] = MESH ? kMeshFans * n_pos : n_pos;  // records k_tile's overflow scan covers
             volatile uint32_t* st = P.status;
             st[kStTotalPairs] = total;
             if (total > P.bin_capacity) st[kStOverflow] += 1u;  // draws run in stream order
@@ -711,15 +871,9 @@ __global__ __launch_bounds__(kSetupThreads) void k_setup_bin(DrawParams P) {
     // (own unit, primitive in unit) so every thread has work
     {
         const uint32_t usz = 1u << P.unit_shift;
-        uint32_t nown = 0;
-        while (own_unit(P, units, w, G, nown) < units) ++nown;
-        for (uint32_t j = tid; j < (nown << P.unit_shift); j += kSetupThreads) {
-            const uint32_t prim = (own_unit(P, units, w, G, j >> P.unit_shift) << P.unit_shift) + (j & (usz - 1u));
-            if (prim >= n_pos) continue;
-            const BBox bb = P.bbox_lds ? s_bbox[j] : P.bboxes[prim];
-            // overflowed draw: k_tile rasterizes by scanning every record's bbox
-            if (P.bbox_lds && total > P.bin_capacity) P.bboxes[prim] = bb;
-            if (bb.bb0 == kEmptyBox) continue;
+        // appends (tile, record) pairs of one setup record to its owned tiles' lists
+        auto scatter = [&](uint32_t rec, const BBox bb) {
+            if (bb.bb0 == kEmptyBox) return;
             const int tx0 = (int)(bb.bb0 & 0xFFFFu) >> kTileShift, tx1 = (int)(bb.bb1 & 0xFFFFu) >> kTileShift;
             const int ty0 = (int)(bb.bb0 >> 16) >> kTileShift, ty1 = (int)(bb.bb1 >> 16) >> kTileShift;
             for (int ty = ty0; ty <= ty1; ++ty) {
@@ -733,8 +887,22 @@ __global__ __launch_bounds__(kSetupThreads) void k_setup_bin(DrawParams P) {
                     const uint32_t area = (uint32_t)((cx1 - cx0 + 1) * (cy1 - cy0 + 1));
                     const uint32_t bucket = min((area - 1u) >> 2, kSortBuckets - 1u);
                     const uint32_t pos = atomicAdd(&s_hist[r + tx], 1u);
-                    if (pos < P.bin_capacity) P.bins[pos] = prim | (bucket << kBinPrimBits);
+                    if (pos < P.bin_capacity) P.bins[pos] = rec | (bucket << kBinPrimBits);
                 }
+            }
+        };
+        uint32_t nown = 0;
+        while (own_unit(P, units, w, G, nown) < units) ++nown;
+        for (uint32_t j = tid; j < (nown << P.unit_shift); j += kSetupThreads) {
+            const uint32_t prim = (own_unit(P, units, w, G, j >> P.unit_shift) << P.unit_shift) + (j & (usz - 1u));
+            if (prim >= n_pos) continue;
+            const BBox bb = P.bbox_lds ? s_bbox[j] : P.bboxes[prim];
+            // overflowed draw: k_tile rasterizes by scanning every record's bbox
+            if (P.bbox_lds && total > P.bin_capacity) P.bboxes[prim] = bb;
+            scatter(prim, bb);
+            if (MESH) {  // fans 1 and 2 (bboxes stored by this workgroup in phase 1)
+                scatter(mesh_record(P, prim, 1), P.bboxes[mesh_record(P, prim, 1)]);
+                scatter(mesh_record(P, prim, 2), P.bboxes[mesh_record(P, prim, 2)]);
             }
         }
     }
@@ -973,6 +1141,72 @@ __device__ __forceinline__ void raster_lane(const DrawParams& P, const TriRecord
     }
 }
 
+// Visibility sequence of setup record e (API order): e + 1, or for the mesh
+// program 4p + k + 1 for fan k of primitive p (zr_internal.h kMeshFans).
+template <int PROG>
+__device__ __forceinline__ uint32_t entry_seq(const DrawParams& P, uint32_t e) {
+    if (PROG != kProgMesh) return e + 1u;
+    if (e < P.prims) return 4u * e + 1u;
+    const uint32_t q = e - P.prims;
+    return 4u * (q >> 1) + (q & 1u) + 2u;
+}
+// ... and back: the setup record and the draw primitive of sequence s + 1.
+template <int PROG>
+__device__ __forceinline__ uint32_t seq_record(const DrawParams& P, uint32_t s) {
+    if (PROG != kProgMesh) return s;
+    const uint32_t p = s >> 2, k = s & 3u;
+    return k ? P.prims + 2u * p + k - 1u : p;
+}
+template <int PROG>
+__device__ __forceinline__ uint32_t seq_prim(uint32_t s) { return PROG == kProgMesh ? s >> 2 : s; }
+template <int PROG>
+__device__ __forceinline__ uint32_t record_prim(const DrawParams& P, uint32_t e) {
+    return (PROG == kProgMesh && e >= P.prims) ? (e - P.prims) >> 1 : e;
+}
+
+// mesh.slang psmain: perspective-correct barycentrics of the primitive (not of
+// its clipped fan triangle) from its homogeneous screen vertices
+// h_i = (x_i hw + w_i cx, y_i hh + w_i cy, w_i): b_i = E_i / sum E with
+// E_i = p . (h_j x h_k) at the pixel centre; then normal and uv interpolated and
+// lit like blinn_phong.slang with kd = (0.35 + 0.3 u, 0.35 + 0.3 v, 0.7)
+// (zr_oracle.c shade, same operation order).
+__device__ __forceinline__ void shade_mesh(const DrawParams& P, const uint32_t vid[3], int px, int py, float out[4]) {
+    float hX[3], hY[3], hW[3];
+#pragma unroll
+    for (int k = 0; k < 3; ++k) {
+        const float3 p = *reinterpret_cast<const float3*>(attr_ptr(P, vid[k], 0));
+        float c[4];
+        mesh_transform(P.view_proj, p, c);
+        hX[k] = fmaf(c[0], P.hw, c[3] * P.cx);
+        hY[k] = fmaf(c[1], P.hh, c[3] * P.cy);
+        hW[k] = c[3];
+    }
+    const float fx = (float)px + 0.5f, fy = (float)py + 0.5f;
+    float E[3];
+#pragma unroll
+    for (int i = 0; i < 3; ++i) {
+        const int j = (i + 1) % 3, k = (i + 2) % 3;
+        const float c0 = hY[j] * hW[k] - hW[j] * hY[k];
+        const float c1 = hW[j] * hX[k] - hX[j] * hW[k];
+        const float c2 = hX[j] * hY[k] - hY[j] * hX[k];
+        E[i] = fmaf(c0, fx, fmaf(c1, fy, c2));
+    }
+    const float einv = 1.0f / ((E[0] + E[1]) + E[2]);
+    const float b0 = E[0] * einv, b1 = E[1] * einv, b2 = E[2] * einv;
+    const float* n0 = attr_ptr(P, vid[0], 1);
+    const float* n1 = attr_ptr(P, vid[1], 1);
+    const float* n2 = attr_ptr(P, vid[2], 1);
+    const float* u0 = attr_ptr(P, vid[0], 2);
+    const float* u1 = attr_ptr(P, vid[1], 2);
+    const float* u2 = attr_ptr(P, vid[2], 2);
+    float n[3], uv[2];
+#pragma unroll
+    for (int i = 0; i < 3; ++i) n[i] = (b0 * n0[i] + b1 * n1[i]) + b2 * n2[i];
+#pragma unroll
+    for (int i = 0; i < 2; ++i) uv[i] = (b0 * u0[i] + b1 * u1[i]) + b2 * u2[i];
+    shade_blinn_phong(n[0], n[1], n[2], fmaf(uv[0], 0.3f, 0.35f), fmaf(uv[1], 0.3f, 0.35f), 0.7f, out);
+}
+
 // Vertex ids of a winning primitive; IDX32: u32 index buffer (one 12-B load).
 template <bool IDX32>
 __device__ __forceinline__ void resolve_vids(const DrawParams& P, uint32_t prim, uint32_t v[3]) {
@@ -1000,7 +1234,7 @@ __device__ __forceinline__ void resolve_pixels(const DrawParams& P, int x0, int 
         int px[kB], py[kB];
         bool have[kB], inside[kB];
         unsigned long long key[kB];
-        uint32_t prim[kB], vid[kB][3];
+        uint32_t prim[kB], gp[kB], vid[kB][3];  // setup record, draw primitive, its vertex ids
         int4 c0[kB], c1[kB];
 #pragma unroll
         for (int b = 0; b < kB; ++b) {
@@ -1011,7 +1245,8 @@ __device__ __forceinline__ void resolve_pixels(const DrawParams& P, int x0, int 
             key[b] = s_key[i];
             const uint32_t seq = inside[b] ? winner_seq<MODE>(key[b]) : 0u;
             have[b] = seq != 0;
-            prim[b] = have[b] ? seq - 1u : fallback;
+            prim[b] = have[b] ? seq_record<PROG>(P, seq - 1u) : fallback;
+            gp[b] = have[b] ? seq_prim<PROG>(seq - 1u) : record_prim<PROG>(P, fallback);
         }
         float col[kB][4];
         float zw[kB];
@@ -1021,7 +1256,7 @@ __device__ __forceinline__ void resolve_pixels(const DrawParams& P, int x0, int 
                 const int4* cp = reinterpret_cast<const int4*>(P.records + prim[b]);
                 c0[b] = cp[0];
                 c1[b] = cp[1];
-                resolve_vids<IDX32>(P, prim[b], vid[b]);
+                resolve_vids<IDX32>(P, gp[b], vid[b]);
             }
 #pragma unroll
             for (int b = 0; b < kB; ++b) {
@@ -1035,7 +1270,10 @@ __device__ __forceinline__ void resolve_pixels(const DrawParams& P, int x0, int 
                 r.v2 = sw ? vid[b][1] : vid[b][2];
                 const EdgeEvalF e = eval_edges_f(r, px[b], py[b]);
                 col[b][0] = col[b][1] = col[b][2] = col[b][3] = 0.0f;
-                if (P.color_bpp && !(P.debug & kDebugSkipShade)) shade_winner<PROG>(P, r, e, col[b]);
+                if (P.color_bpp && !(P.debug & kDebugSkipShade)) {
+                    if constexpr (PROG == kProgMesh) shade_mesh(P, vid[b], px[b], py[b], col[b]);
+                    else shade_winner<PROG>(P, r, e, col[b]);
+                }
                 zw[b] = (MODE == kDepthLastWins) ? interp_depth_f(r, e.f1, e.f2) : key_depth<MODE>(key[b]);
             }
         } else {
@@ -1190,7 +1428,7 @@ __global__ __launch_bounds__(NT, ZR_TILE_WGS * kTileThreads / NT) void k_tile(Dr
                 const bool large = compact_is_large(q0);
                 if (valid && !large) {
                     const TriRecord r = decode_compact(P, q0, q1, true);
-                    raster_lane<MODE, INITD>(P, r, my_prim + 1u, x0, y0, s_key, s_initd, sub, (int)ksh);
+                    raster_lane<MODE, INITD>(P, r, entry_seq<PROG>(P, my_prim), x0, y0, s_key, s_initd, sub, (int)ksh);
                 }
                 // large primitives: the whole wave sweeps one primitive at a time (full record)
                 unsigned long long big = __ballot(valid && large && sub == 0);
@@ -1199,7 +1437,7 @@ __global__ __launch_bounds__(NT, ZR_TILE_WGS * kTileThreads / NT) void k_tile(Dr
                     big &= big - 1ull;
                     const uint32_t prim = (uint32_t)rl((int)my_prim, i);
                     const TriRecord r = load_uniform_record(P.records_big + prim);
-                    raster_prim<MODE, INITD>(P, r, prim + 1u, x0, y0, lane, s_key, s_initd);
+                    raster_prim<MODE, INITD>(P, r, entry_seq<PROG>(P, prim), x0, y0, lane, s_key, s_initd);
                 }
             }
             __syncthreads();
@@ -1223,13 +1461,14 @@ __global__ __launch_bounds__(NT, ZR_TILE_WGS * kTileThreads / NT) void k_tile(Dr
                 }
                 const bool large = compact_is_large(q0);
                 if (hit && !large)
-                    raster_lane<MODE, INITD>(P, decode_compact(P, q0, q1, true), j + 1u, x0, y0, s_key, s_initd, 0, 0);
+                    raster_lane<MODE, INITD>(P, decode_compact(P, q0, q1, true), entry_seq<PROG>(P, j), x0, y0, s_key, s_initd,
+                                             0, 0);
                 unsigned long long big = __ballot(hit && large);
                 while (big) {
                     const uint32_t i = (uint32_t)__builtin_ctzll(big);
                     big &= big - 1ull;
                     const uint32_t prim = (uint32_t)rl((int)j, i);
-                    raster_prim<MODE, INITD>(P, load_uniform_record(P.records_big + prim), prim + 1u, x0, y0, lane,
+                    raster_prim<MODE, INITD>(P, load_uniform_record(P.records_big + prim), entry_seq<PROG>(P, prim), x0, y0, lane,
                                              s_key, s_initd);
                 }
             }
@@ -1282,21 +1521,26 @@ size_t setup_bin_lds_bytes(uint32_t ntiles, uint32_t bbox_entries) {
     return (2 * (size_t)ntiles + kSetupMiscWords) * sizeof(uint32_t) + (size_t)bbox_entries * sizeof(BBox);
 }
 
-const void* setup_bin_kernel(uint32_t batch) {
+const void* setup_bin_kernel(uint32_t batch, bool mesh) {
+    if (mesh) return reinterpret_cast<const void*>(&k_setup_bin<1, true>);
     switch (batch) {
-    case 1: return reinterpret_cast<const void*>(&k_setup_bin<1>);
-    case 2: return reinterpret_cast<const void*>(&k_setup_bin<2>);
-    default: return reinterpret_cast<const void*>(&k_setup_bin<4>);
+    case 1: return reinterpret_cast<const void*>(&k_setup_bin<1, false>);
+    case 2: return reinterpret_cast<const void*>(&k_setup_bin<2, false>);
+    default: return reinterpret_cast<const void*>(&k_setup_bin<4, false>);
     }
 }
 
 void launch_setup_bin(const DrawParams& p, void* stream) {
     const size_t lds = setup_bin_lds_bytes(p.ntiles, p.bbox_lds);
     const hipStream_t s = (hipStream_t)stream;
+    if (p.program == kProgMesh) {  // batch 1: the clip path is heavy
+        hipLaunchKernelGGL((k_setup_bin<1, true>), dim3(p.setup_wgs), dim3(kSetupThreads), lds, s, p);
+        return;
+    }
     switch (p.setup_batch) {
-    case 1: hipLaunchKernelGGL(k_setup_bin<1>, dim3(p.setup_wgs), dim3(kSetupThreads), lds, s, p); break;
-    case 2: hipLaunchKernelGGL(k_setup_bin<2>, dim3(p.setup_wgs), dim3(kSetupThreads), lds, s, p); break;
-    default: hipLaunchKernelGGL(k_setup_bin<4>, dim3(p.setup_wgs), dim3(kSetupThreads), lds, s, p); break;
+    case 1: hipLaunchKernelGGL((k_setup_bin<1, false>), dim3(p.setup_wgs), dim3(kSetupThreads), lds, s, p); break;
+    case 2: hipLaunchKernelGGL((k_setup_bin<2, false>), dim3(p.setup_wgs), dim3(kSetupThreads), lds, s, p); break;
+    default: hipLaunchKernelGGL((k_setup_bin<4, false>), dim3(p.setup_wgs), dim3(kSetupThreads), lds, s, p); break;
     }
 }
 
@@ -1334,6 +1578,7 @@ void launch_tile(const DrawParams& p, void* stream) {
     switch (p.program) {
     case kProgTriangle: launch_tile_p<kProgTriangle>(p, s, initd); break;
     case kProgFlat: launch_tile_p<kProgFlat>(p, s, initd); break;
+    case kProgMesh: launch_tile_p<kProgMesh>(p, s, initd); break;
     default: launch_tile_p<kProgBlinn>(p, s, initd); break;
     }
 }

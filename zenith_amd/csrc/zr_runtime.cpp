@@ -67,6 +67,12 @@ const ShaderEntry kShaders[] = {
     {"blinn_phong.slang", "vsmain", ZR_SHADER_STAGE_VERTEX, kProgBlinn, 0, {},
      3, {{0, ZR_FORMAT_R32G32B32_SFLOAT}, {1, ZR_FORMAT_R32G32B32_SFLOAT}, {2, ZR_FORMAT_R32G32B32_SFLOAT}}},
     {"blinn_phong.slang", "psmain", ZR_SHADER_STAGE_FRAGMENT, kProgBlinn, 0, {}, 0, {}},
+    // mesh.slang: camera program over zenith-asset's Vertex
+    // {position, normal, uv} (zenith-asset/src/render.rs:12-16); View = view_proj
+    {"mesh.slang", "vsmain", ZR_SHADER_STAGE_VERTEX, kProgMesh, 1,
+     {{"View", 0, 0, ZR_DESCRIPTOR_TYPE_UNIFORM_BUFFER, 1, ZR_SHADER_STAGE_VERTEX}},
+     3, {{0, ZR_FORMAT_R32G32B32_SFLOAT}, {1, ZR_FORMAT_R32G32B32_SFLOAT}, {2, ZR_FORMAT_R32G32_SFLOAT}}},
+    {"mesh.slang", "psmain", ZR_SHADER_STAGE_FRAGMENT, kProgMesh, 0, {}, 0, {}},
 };
 
 std::string basename_of(const char* path) {
@@ -115,6 +121,7 @@ struct zr_pipeline_t {
     uint32_t stride;
     uint32_t nattr;
     uint32_t attr_offset[4];
+    uint32_t attr_size[4];
     std::vector<zr_shader_binding> bindings;  // merged reflection
     uint32_t cull_mode;
     int32_t front_face;
@@ -223,6 +230,7 @@ struct zr_device_t {
     bool overlap = false;
     int cu_count = 0;
     uint32_t occupancy_checked_tiles = 0;
+    bool occupancy_checked_mesh = false;
     uint32_t setup_sched = 1;  // k_setup_bin unit schedule (ZR_SETUP_SCHED: 0 contiguous, 1 interleaved)
     uint32_t setup_batch = 2;  // k_setup_bin primitives per lane in flight (ZR_SETUP_BATCH: 1, 2, 4)
     uint32_t tile_threads = 0; // k_tile workgroup size override (ZR_TILE_NT: 256, 512; 0 = by tile count)
@@ -519,7 +527,8 @@ zr_result fill_target(const ExecState& s, DrawParams& P) {
 
 zr_result ensure_scratch(zr_device* d, ScratchSet& S, DrawParams& P) {
     zr_result rc;
-    const uint64_t prims = std::max<uint64_t>(P.prims, 1);
+    // the mesh program's fans 1 and 2 have records and bboxes of their own
+    const uint64_t prims = std::max<uint64_t>(P.prims, 1) * (P.program == kProgMesh ? kMeshFans : 1u);
     if ((rc = grow(d, S.records, S.records_cap, prims, sizeof(TriCompact)))) return rc;
     if ((rc = grow(d, S.records_big, S.records_big_cap, prims, sizeof(TriRecord)))) return rc;
     if ((rc = grow(d, S.bboxes, S.bboxes_cap, prims, sizeof(BBox)))) return rc;
@@ -583,7 +592,10 @@ zr_result exec_draw(zr_device* d, ExecState& s, const Cmd& c, bool indexed) {
     P.vb_bytes = vb->size > s.vb[0].offset ? vb->size - s.vb[0].offset : 0;
     P.stride = pp->stride;
     P.nattr = pp->nattr;
-    for (int i = 0; i < 4; ++i) P.attr_offset[i] = pp->attr_offset[i];
+    for (int i = 0; i < 4; ++i) {
+        P.attr_offset[i] = pp->attr_offset[i];
+        P.attr_size[i] = pp->attr_size[i];
+    }
     if (indexed) {
         P.ib = (const uint8_t*)s.ib->ptr + s.ib_offset;
         P.ib_bytes = s.ib->size > s.ib_offset ? s.ib->size - s.ib_offset : 0;
@@ -602,6 +614,11 @@ zr_result exec_draw(zr_device* d, ExecState& s, const Cmd& c, bool indexed) {
     // primitives; the setup pass then runs over the received blocks' dense
     // positions (at most shard_count * span of them).
     const bool partitioned = s.exchange != nullptr;
+    const bool mesh = pp->program == kProgMesh;
+    if (partitioned && mesh)
+        return fail(ZR_ERROR_FEATURE_NOT_PRESENT, "partitioned tile shards do not route clipped (mesh program) draws");
+    if (mesh && prims * kMeshFans > kBinPrimMask)
+        return fail(ZR_ERROR_FEATURE_NOT_PRESENT, "mesh program: more than (2^26-1)/3 primitives in one draw");
     uint64_t positions = prims;
     uint64_t span = 0;
     if (partitioned) {
@@ -654,19 +671,26 @@ zr_result exec_draw(zr_device* d, ExecState& s, const Cmd& c, bool indexed) {
                 return fail(ZR_ERROR_VALIDATION_FAILED, "Time uniform range out of bounds");
             P.time_ptr = (const float*)((const uint8_t*)it->second.first->ptr + it->second.second);
         }
+        if (pp->program == kProgMesh && !strcmp(b.name, "View")) {
+            if (it->second.second + 64 > it->second.first->size || (it->second.second & 3u))
+                return fail(ZR_ERROR_VALIDATION_FAILED, "View uniform range out of bounds (float4x4 view_proj)");
+            P.view_proj = (const float*)((const uint8_t*)it->second.first->ptr + it->second.second);
+        }
     }
+    if (mesh && !P.view_proj) return fail(ZR_ERROR_VALIDATION_FAILED, "descriptor 'View' not bound");
     // binning geometry: k_setup_bin runs one kSetupThreads workgroup per CU at most
     // (every workgroup resident: it synchronises through grid barriers)
     if (P.ntiles > kMaxTilesPerPass)
         return fail(ZR_ERROR_FEATURE_NOT_PRESENT, "more than 16384 owned 32x32 tiles in one pass");
-    P.setup_batch = d->setup_batch;
+    P.setup_batch = mesh ? 1u : d->setup_batch;  // the mesh instance is k_setup_bin<1, true>
     P.setup_sched = d->setup_sched;
-    if (d->occupancy_checked_tiles != P.ntiles) {
+    if (d->occupancy_checked_tiles != P.ntiles || d->occupancy_checked_mesh != mesh) {
         int nb = 0;
-        ZR_HIP(hipOccupancyMaxActiveBlocksPerMultiprocessor(&nb, setup_bin_kernel(P.setup_batch), kSetupThreads,
+        ZR_HIP(hipOccupancyMaxActiveBlocksPerMultiprocessor(&nb, setup_bin_kernel(P.setup_batch, mesh), kSetupThreads,
                                                             setup_bin_lds_bytes(P.ntiles, 0)));
         if (nb < 1) return fail(ZR_ERROR_FEATURE_NOT_PRESENT, "k_setup_bin cannot be resident on a CU");
         d->occupancy_checked_tiles = P.ntiles;
+        d->occupancy_checked_mesh = mesh;
     }
     {
         // one workgroup per CU (fewer for small draws); a wave processes units of
@@ -684,7 +708,8 @@ zr_result exec_draw(zr_device* d, ExecState& s, const Cmd& c, bool indexed) {
         const uint64_t entries = own_max << shift;
         const uint64_t hist = setup_bin_lds_bytes(P.ntiles, 0);
         const uint64_t budget = std::min<uint64_t>(kSetupBboxLdsBytes, hist < kSetupLdsBudget ? kSetupLdsBudget - hist : 0);
-        P.bbox_lds = (entries * sizeof(BBox) <= budget) ? (uint32_t)entries : 0u;
+        // (mesh: fans 1 and 2 keep their bboxes in global memory, so all of them do)
+        P.bbox_lds = (!mesh && entries * sizeof(BBox) <= budget) ? (uint32_t)entries : 0u;
     }
     P.tile_threads = d->tile_threads ? d->tile_threads : tile_threads_for(P.ntiles, (uint32_t)std::max(d->cu_count, 1));
     P.debug = d->debug;
@@ -857,7 +882,10 @@ ZR_API zr_result zr_device_create(int32_t hip_device, zr_device** out) {
     d->own_stream = d->stream;
     ZR_HIP(hipStreamCreateWithFlags(&d->setup_stream, hipStreamNonBlocking));
     for (uint32_t b : {1u, 2u, 4u})  // histograms + bbox array may exceed the 64 KB default
-        ZR_HIP(hipFuncSetAttribute(setup_bin_kernel(b), hipFuncAttributeMaxDynamicSharedMemorySize, (int)kSetupLdsBudget));
+        ZR_HIP(hipFuncSetAttribute(setup_bin_kernel(b, false), hipFuncAttributeMaxDynamicSharedMemorySize,
+                                   (int)kSetupLdsBudget));
+    ZR_HIP(hipFuncSetAttribute(setup_bin_kernel(1, true), hipFuncAttributeMaxDynamicSharedMemorySize,
+                               (int)kSetupLdsBudget));
     ZR_HIP(hipDeviceGetAttribute(&d->cu_count, hipDeviceAttributeMultiprocessorCount, hip_device));
     void* st = nullptr;
     ZR_HIP(hipHostMalloc(&st, kStWords * 4, hipHostMallocMapped));
@@ -1238,6 +1266,7 @@ ZR_API zr_result zr_pipeline_create(zr_device* d, const zr_graphic_pipeline_desc
     }
     p->nattr = (uint32_t)vs->inputs.size();
     memset(p->attr_offset, 0, sizeof p->attr_offset);
+    memset(p->attr_size, 0, sizeof p->attr_size);
     for (uint32_t i = 0; i < desc->vertex_attribute_count; ++i) {
         const auto& a = desc->vertex_attributes[i];
         if (a.binding != 0 || a.location >= 4 || (a.offset & 3u)) {
@@ -1245,6 +1274,8 @@ ZR_API zr_result zr_pipeline_create(zr_device* d, const zr_graphic_pipeline_desc
             return fail(ZR_ERROR_FEATURE_NOT_PRESENT, "vertex attributes must live in binding 0, 4-byte aligned");
         }
         p->attr_offset[a.location] = a.offset;
+        p->attr_size[a.location] = a.format == ZR_FORMAT_R32G32_SFLOAT ? 8u : a.format == ZR_FORMAT_R32_SFLOAT ? 4u
+                                   : a.format == ZR_FORMAT_R32G32B32A32_SFLOAT ? 16u : 12u;
     }
     if (p->nattr && (p->stride == 0 || (p->stride & 3u))) {
         delete p;

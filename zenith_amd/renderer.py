@@ -109,7 +109,7 @@ class SceneRenderer:
         path = PROGRAM_FILES[scene.program]
         self.vs = rhi.Shader.from_file(f"{scene.name}.vs", device, path, "vsmain", rhi.ShaderStage.Vertex)
         self.fs = rhi.Shader.from_file(f"{scene.name}.ps", device, path, "psmain", rhi.ShaderStage.Fragment)
-        fields = [("position", 3)] + [(f"a{i}", 3) for i in range(1, scene.stride // 12)]
+        fields = [("position", 3)] + [(f"a{i}", n) for i, n in enumerate(scene.layout[1:], 1)]
         shader = (rhi.GraphicShaderInputBuilder().vertex_shader(self.vs).fragment_shader(self.fs)
                   .vertex_layout(fields).build())
         color_info = rhi.ColorAttachmentDesc().clear_input()
@@ -128,6 +128,9 @@ class SceneRenderer:
         self.time_buffer = None
         if scene.program == 0:
             self.time_buffer = rhi.Buffer(device, rhi.BufferDesc.uniform(f"{scene.name}.time", 4))
+        self.view_buffer = None
+        if scene.view_proj is not None:  # mesh.slang's View { float4x4 view_proj }
+            self.view_buffer = rhi.Buffer(device, rhi.BufferDesc.uniform(f"{scene.name}.view", 64))
         self.encoder = rhi.CommandEncoder(device)
 
     def record(self, color: rhi.Texture, depth: Optional[rhi.Texture], shard: Optional[tuple] = None,
@@ -146,6 +149,12 @@ class SceneRenderer:
                 rng.write(np.float32(s.time).tobytes())
                 binder = ctx.create_binder()
                 binder.bind_buffer("Time", rng)
+                ctx.bind_descriptor_sets(binder)
+            if self.view_buffer is not None:
+                rng = self.view_buffer.as_range(0, 64)
+                rng.write(np.asarray(s.view_proj, np.float32).tobytes())
+                binder = ctx.create_binder()
+                binder.bind_buffer("View", rng)
                 ctx.bind_descriptor_sets(binder)
             ctx.begin_rendering((W, H))
             ctx.bind_pipeline()

@@ -31,13 +31,17 @@ OP_NEVER, OP_LESS, OP_EQUAL, OP_LEQUAL, OP_GREATER, OP_NOTEQUAL, OP_GEQUAL, OP_A
 INDEX_U16, INDEX_U32 = 0, 1
 LOAD_LOAD, LOAD_CLEAR, LOAD_DONT_CARE = 0, 1, 2
 
-PROGRAM_TRIANGLE, PROGRAM_FLAT_COLOR, PROGRAM_BLINN_PHONG = 0, 1, 2
+PROGRAM_TRIANGLE, PROGRAM_FLAT_COLOR, PROGRAM_BLINN_PHONG, PROGRAM_MESH = 0, 1, 2, 3
 PROGRAM_FILES = {
     PROGRAM_TRIANGLE: "content/shaders/triangle.slang",
     PROGRAM_FLAT_COLOR: "content/shaders/flat_color.slang",
     PROGRAM_BLINN_PHONG: "content/shaders/blinn_phong.slang",
+    PROGRAM_MESH: "content/shaders/mesh.slang",
 }
-PROGRAM_ATTRS = {PROGRAM_TRIANGLE: 2, PROGRAM_FLAT_COLOR: 2, PROGRAM_BLINN_PHONG: 3}
+# float components of each vertex input, location order
+PROGRAM_LAYOUT = {PROGRAM_TRIANGLE: (3, 3), PROGRAM_FLAT_COLOR: (3, 3), PROGRAM_BLINN_PHONG: (3, 3, 3),
+                  PROGRAM_MESH: (3, 3, 2)}  # mesh: zenith-asset Vertex {position, normal, uv}
+PROGRAM_ATTRS = {k: len(v) for k, v in PROGRAM_LAYOUT.items()}
 
 
 @dataclasses.dataclass
@@ -65,10 +69,15 @@ class Scene:
     first: int = 0                                   # first_index / first_vertex
     vertex_offset: int = 0
     count: int | None = None                         # default: all indices / vertices
+    view_proj: tuple | None = None                   # mesh program: View.view_proj, 16 floats column-major
+
+    @property
+    def layout(self) -> tuple:
+        return PROGRAM_LAYOUT[self.program]
 
     @property
     def stride(self) -> int:
-        return 12 * PROGRAM_ATTRS[self.program]
+        return 4 * sum(self.layout)
 
     @property
     def index_type(self) -> int:
@@ -233,3 +242,95 @@ def config_bytes_per_triangle(cfg: str) -> int:
     """B_in of SURVEY.md §8d: 3 vertices at the stride + 3 u32 indices."""
     prog = CONFIGS[cfg][5]
     return 3 * 12 * PROGRAM_ATTRS[prog] + 3 * 4
+
+
+# ------------------------------------------------------------------ camera
+# zenith-core/src/camera.rs: Camera::view_projection = proj * view (:85-87) with
+# proj = Mat4::perspective_infinite_reverse_rh(fov_y, aspect, near) (:50, :60) and
+# view = Mat4::look_to_rh(position, forward, WORLD_SPACE_UP = +Z) (:121-124), in
+# glam 0.30's column-major layout, restated in float32 as glam computes them.
+NEAR_PLANE = 0.1          # camera.rs:16
+WORLD_UP = (0.0, 0.0, 1.0)
+
+
+def perspective_infinite_reverse_rh(fov_y: float, aspect: float, z_near: float) -> np.ndarray:
+    """glam Mat4::perspective_infinite_reverse_rh: columns
+    (f/aspect,0,0,0), (0,f,0,0), (0,0,0,-1), (0,0,z_near,0), f = 1/tan(fov_y/2)."""
+    f = np.float32(1.0) / np.float32(math.tan(np.float32(0.5) * np.float32(fov_y)))
+    m = np.zeros((4, 4), np.float32)  # m[col][row]
+    m[0, 0] = f / np.float32(aspect)
+    m[1, 1] = f
+    m[2, 3] = -1.0
+    m[3, 2] = np.float32(z_near)
+    return m
+
+
+def look_to_rh(eye, direction, up) -> np.ndarray:
+    """glam Mat4::look_to_rh: f = normalize(dir), s = normalize(f x up), u = s x f;
+    columns (s.x,u.x,-f.x,0), (s.y,u.y,-f.y,0), (s.z,u.z,-f.z,0),
+    (-dot(eye,s), -dot(eye,u), dot(eye,f), 1)."""
+    e = np.asarray(eye, np.float32)
+    f = np.asarray(direction, np.float32)
+    f = f / np.float32(np.sqrt(np.dot(f, f)))
+    s_ = np.cross(f, np.asarray(up, np.float32)).astype(np.float32)
+    s_ = s_ / np.float32(np.sqrt(np.dot(s_, s_)))
+    u = np.cross(s_, f).astype(np.float32)
+    m = np.zeros((4, 4), np.float32)
+    m[0] = (s_[0], u[0], -f[0], 0.0)
+    m[1] = (s_[1], u[1], -f[1], 0.0)
+    m[2] = (s_[2], u[2], -f[2], 0.0)
+    m[3] = (-np.dot(e, s_), -np.dot(e, u), np.dot(e, f), 1.0)
+    return m
+
+
+def view_projection(eye, forward, fov_y=math.pi / 6, aspect=1.77777, z_near=NEAR_PLANE) -> tuple:
+    """proj * view as 16 column-major floats (the View uniform's bytes)."""
+    proj = perspective_infinite_reverse_rh(fov_y, aspect, z_near)
+    view = look_to_rh(eye, forward, WORLD_UP)
+    vp = (view.astype(np.float64) @ proj.astype(np.float64))  # column-major: (P V)[c] = sum_k V[c][k] P[k]
+    return tuple(float(x) for x in vp.astype(np.float32).reshape(-1))
+
+
+def mesh_soup_scene(seed: int, n: int, width: int, height: int, extent: float = 6.0,
+                    eye=(0.0, -3.0, 0.5), forward=(0.0, 1.0, -0.1), name: str | None = None) -> Scene:
+    """Camera-space test scene for the mesh program: n triangles with vertices
+    scattered in a box in front of (and around) the camera, so primitives cross
+    the near plane, lie behind the camera or straddle the view edges.  Reverse-Z:
+    depth GREATER, clear 0 (camera.rs:50), cull BACK / CCW front (pipeline.rs
+    defaults)."""
+    g = np.random.default_rng(seed)
+    c = g.uniform((-extent, -4.0, -extent / 2), (extent, 12.0, extent / 2), (n, 1, 3))
+    d = g.uniform(-1.5, 1.5, (n, 3, 3))
+    pos = (c + d).reshape(-1, 3).astype(np.float32)
+    nrm = g.normal(size=(3 * n, 3)).astype(np.float32)
+    uv = g.uniform(0.0, 1.0, (3 * n, 2)).astype(np.float32)
+    verts = np.concatenate([pos, nrm, uv], axis=1)
+    vp = view_projection(eye, forward, aspect=width / height)
+    return Scene(name or f"mesh_soup_s{seed}_n{n}", width, height, PROGRAM_MESH, verts,
+                 np.arange(3 * n, dtype=np.uint32), depth=True, depth_op=OP_GREATER, depth_clear=0.0,
+                 cull_mode=CULL_BACK, view_proj=vp)
+
+
+CERBERUS_NPZ = "tests/golden/cerberus.mesh.npz"  # relative to the repo root
+
+
+def mesh_scene(vertices: np.ndarray, indices: np.ndarray, width: int, height: int, eye, forward,
+               name: str = "mesh", fov_y: float = math.pi / 6) -> Scene:
+    """A baked Mesh<Vertex> (zenith_amd.assets) through a camera: reverse-Z depth
+    (GREATER, clear 0), cull BACK with CCW front faces, clear (0.1, 0.1, 0.1, 1)."""
+    vp = view_projection(eye, forward, fov_y=fov_y, aspect=width / height)
+    return Scene(name, width, height, PROGRAM_MESH, np.ascontiguousarray(vertices, np.float32),
+                 np.ascontiguousarray(indices, np.uint32), depth=True, depth_op=OP_GREATER, depth_clear=0.0,
+                 cull_mode=CULL_BACK, view_proj=vp)
+
+
+def cerberus_scene(width: int = 640, height: int = 480, eye=(291.6, -31.5, 111.9), target=(-3.7, -52.2, -14.2),
+                   npz: str | None = None) -> Scene:
+    """content/mesh/cerberus (33,543 triangles, CC-BY-4.0, tests/golden/CERBERUS.txt)
+    baked as gltf_loader.rs does, seen by a camera at `eye` looking at `target`."""
+    import os
+    path = npz or os.path.join(os.path.dirname(os.path.dirname(os.path.abspath(__file__))), CERBERUS_NPZ)
+    with np.load(path, allow_pickle=False) as z:
+        v, i = z["vertices"], z["indices"]
+    fwd = tuple(float(t - e) for t, e in zip(target, eye))
+    return mesh_scene(v, i, width, height, eye, fwd, name=f"cerberus_{width}x{height}")
