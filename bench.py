@@ -269,9 +269,11 @@ def main():
         "warmup": a.warmup, "ms_per_step": round(ms_per_step, 4), "higher_is_better": True,
         "scaling": "strong", "vs_baseline": None, "dtype": "f32",
         "data": "synthetic (SplitMix64 triangle soup, SURVEY.md §8d)",
-        "config": {"workload": f"{a.config}: {N} tris soup, {W}x{H}, "
-                               f"{'Blinn-Phong' if scene.program == scenes.PROGRAM_BLINN_PHONG else 'flat'} "
-                               f"+ D32 LESS, B8G8R8A8_SRGB",
+        "config": {"workload": (f"{a.config}: {N} tris (reference asset, mesh.slang camera), {W}x{H}, "
+                                f"D32 GREATER (reverse-Z), B8G8R8A8_SRGB" if scene.program == scenes.PROGRAM_MESH else
+                                f"{a.config}: {N} tris soup, {W}x{H}, "
+                                f"{'Blinn-Phong' if scene.program == scenes.PROGRAM_BLINN_PHONG else 'flat'} "
+                                f"+ D32 LESS, B8G8R8A8_SRGB"),
                    "triangles": N, "width": W, "height": H, "tile": shard.TILE,
                    "parallelism": f"tile-rows x{world}" + (
                        f", {a.setup} setup" + (" (RCCL all-to-all)" if exchange is not None else "")

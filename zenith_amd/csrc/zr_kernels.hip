@@ -1229,6 +1229,10 @@ __device__ __forceinline__ void resolve_pixels(const DrawParams& P, int x0, int 
                                                const unsigned long long* s_key, const float* s_srgb) {
     constexpr int kPer = kTilePixels / NT;
     constexpr int kB = kPer < 2 ? kPer : 2;
+    // recomputed here, not reused from the tile's init: a pixel coordinate kept
+    // live across the raster loop spills at 64 VGPRs
+    int tid = (int)threadIdx.x;
+    asm volatile("" : "+v"(tid));
 #pragma unroll 1
     for (int k0 = 0; k0 < kPer; k0 += kB) {
         int px[kB], py[kB];
@@ -1238,7 +1242,7 @@ __device__ __forceinline__ void resolve_pixels(const DrawParams& P, int x0, int 
         int4 c0[kB], c1[kB];
 #pragma unroll
         for (int b = 0; b < kB; ++b) {
-            const int i = threadIdx.x + (k0 + b) * NT;
+            const int i = tid + (k0 + b) * NT;
             px[b] = x0 + (i & (kTile - 1));
             py[b] = y0 + (i >> kTileShift);
             inside[b] = !(px[b] < P.ra_x0 || px[b] > P.ra_x1 || py[b] < P.ra_y0 || py[b] > P.ra_y1);

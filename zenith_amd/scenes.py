@@ -220,6 +220,9 @@ CONFIGS = {
     "c2": (2, 1_000_000, 1920, 1080, 6.0, PROGRAM_BLINN_PHONG),
     "c3": (3, 1_000_000, 3840, 2160, 12.0, PROGRAM_BLINN_PHONG),
     "c4": (4, 10_000_000, 1920, 1080, 0.5, PROGRAM_FLAT_COLOR),
+    # not a BASELINE config: the reference's real asset through the camera program
+    # (SURVEY.md §8f rows 2-3), 33,543 triangles at 1080p
+    "cerberus": (None, 33_543, 1920, 1080, None, PROGRAM_MESH),
 }
 
 
@@ -235,13 +238,15 @@ def soup_scene(seed: int, n: int, width: int, height: int, L: float, program: in
 def config_scene(cfg: str, n: int | None = None, width: int | None = None,
                  height: int | None = None) -> Scene:
     seed, tris, w, h, L, prog = CONFIGS[cfg]
+    if cfg == "cerberus":
+        return cerberus_scene(width or w, height or h)
     return soup_scene(seed, n or tris, width or w, height or h, L, prog, name=cfg)
 
 
 def config_bytes_per_triangle(cfg: str) -> int:
     """B_in of SURVEY.md §8d: 3 vertices at the stride + 3 u32 indices."""
     prog = CONFIGS[cfg][5]
-    return 3 * 12 * PROGRAM_ATTRS[prog] + 3 * 4
+    return 3 * 4 * sum(PROGRAM_LAYOUT[prog]) + 3 * 4
 
 
 # ------------------------------------------------------------------ camera
