@@ -299,6 +299,11 @@ ZR_API zr_result zr_cmd_end(zr_cmd *cmd);   /* returns the latched recording err
 /* graph.rs:539-601 / command.rs:188-194 */
 ZR_API void zr_cmd_begin_rendering(zr_cmd *cmd, const zr_rendering_info *info);
 ZR_API void zr_cmd_end_rendering(zr_cmd *cmd);
+/* vkCmdClearColorImage over the whole colour texture (one level / layer), as
+ * zenith-sandbox's SimpleApp clear node records it through CommandEncoder::custom
+ * (zenith-sandbox/src/main.rs:35-45).  Outside a render pass; the clear value is
+ * linear float RGBA (encoded like a render-pass clear, sRGB formats included). */
+ZR_API void zr_cmd_clear_color_image(zr_cmd *cmd, zr_texture *tex, const float clear_value[4]);
 /* GraphicNodeExecutionContext::bind_pipeline (graph.rs:527-531) */
 ZR_API void zr_cmd_bind_pipeline(zr_cmd *cmd, const zr_pipeline *p);
 /* DescriptorSetBinder::bind_buffer + bind_descriptor_sets (descriptor.rs:323-357,

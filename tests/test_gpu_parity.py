@@ -457,3 +457,43 @@ def test_mesh_shards_and_spill(monkeypatch, device):
         assert dev.last_draw_stats()["overflowed_draws"] == 1
     finally:
         dev.close()
+
+
+# ------------------------------------------------- present / clear (§8f row 4)
+@pytest.mark.parametrize("fmt", [zr.FORMAT_B8G8R8A8_SRGB, zr.FORMAT_R8G8B8A8_UNORM, zr.FORMAT_R32G32B32A32_SFLOAT])
+def test_clear_color_image(device, fmt):
+    """zenith-sandbox's SimpleApp frame: cmd_clear_color_image (0.2, 0.3, 0.8, 1)
+    over the whole image, encoded like the oracle's clear."""
+    W, H = 200, 150
+    tex = rhi.Texture(device, rhi.TextureDesc.new_color("swapchain", W, H, fmt))
+    app = renderer.SimpleAppRenderer(device)
+    device.submit_and_wait(app.render_to(tex))
+    img = tex.read()
+    s = scenes.Scene("clear", W, H, scenes.PROGRAM_FLAT_COLOR, np.zeros((0, 6), np.float32),
+                     np.zeros(0, np.uint32), color_format=fmt, clear_color=renderer.SimpleAppRenderer.CLEAR)
+    ref, _ = oracle.render(s)
+    assert np.ascontiguousarray(img).tobytes() == ref.tobytes()
+    if fmt == zr.FORMAT_B8G8R8A8_SRGB:
+        from zenith_amd import present
+        back = present.read_png_rgba(present.png_bytes(img, fmt))
+        assert tuple(back[0, 0]) == tuple(img[0, 0, [2, 1, 0, 3]])
+    tex.destroy()
+
+
+def test_clear_then_draw_load(device):
+    """A clear, then a render pass that LOADs the cleared colour and draws."""
+    s = scenes.soup_scene(36, 500, 160, 120, 10.0, scenes.PROGRAM_FLAT_COLOR)
+    s.depth = False  # no depth attachment: the last primitive wins, in order
+    tex = rhi.Texture(device, rhi.TextureDesc.new_color("rt", s.width, s.height, s.color_format))
+    enc = rhi.CommandEncoder(device)
+    enc.begin()
+    enc.clear_color_image(tex, s.clear_color)
+    enc.end()
+    device.submit_and_wait(enc)
+    r = renderer.SceneRenderer(device, s)
+    ref, _ = oracle.render(s)
+    enc2 = r.record(tex, None)
+    device.submit_and_wait(enc2)
+    assert np.array_equal(tex.read(), ref)  # the pass's CLEAR equals the image clear's value
+    enc.destroy()
+    tex.destroy()

@@ -134,7 +134,7 @@ struct zr_pipeline_t {
 };
 
 enum CmdType { C_BEGIN_RENDERING, C_END_RENDERING, C_BIND_PIPELINE, C_BIND_UNIFORM, C_SET_VIEWPORT, C_SET_SCISSOR,
-               C_BIND_VB, C_BIND_IB, C_DRAW, C_SET_SHARD };
+               C_BIND_VB, C_BIND_IB, C_DRAW, C_SET_SHARD, C_CLEAR_IMAGE };
 
 struct RenderingState {
     zr_rect2d area;
@@ -812,6 +812,22 @@ zr_result execute(zr_device* d, zr_cmd* cmd) {
             s.depth_clear_pending = s.rs.has_depth && s.rs.depth.load_op == ZR_ATTACHMENT_LOAD_OP_CLEAR;
             break;
         case C_END_RENDERING: rc = exec_end_rendering(d, s); break;
+        case C_CLEAR_IMAGE: {
+            // the k_clear of a render pass with LOAD_OP_CLEAR and no draw, over the
+            // whole image on every rank (not a tile-row shard)
+            if (s.rendering) { rc = fail(ZR_ERROR_VALIDATION_FAILED, "clear_color_image inside a render pass"); break; }
+            ExecState cs;
+            cs.rendering = true;
+            cs.rs = c.rendering;
+            cs.color_clear_pending = true;
+            const zr_texture* t = c.rendering.color.texture;
+            if (t->gather_pending) {
+                if (d->capturing) return ZR_NOT_READY;
+                ZR_HIP(hipStreamWaitEvent(d->stream, t->gather_done, 0));
+            }
+            rc = exec_end_rendering(d, cs);
+            break;
+        }
         case C_BIND_PIPELINE: s.pipe = c.pipeline; break;
         case C_BIND_UNIFORM: s.ubos[{c.a, c.b}] = {c.buffer, c.offset}; break;
         case C_SET_VIEWPORT: s.vp = c.vp; s.vp_set = true; break;
@@ -1370,6 +1386,21 @@ ZR_API void zr_cmd_end_rendering(zr_cmd* c) {
     k.type = C_END_RENDERING;
     c->cmds.push_back(k);
     c->in_rendering = false;
+}
+
+ZR_API void zr_cmd_clear_color_image(zr_cmd* c, zr_texture* t, const float clear_value[4]) {
+    if (!c) return;
+    if (c->in_rendering) return latch(c, ZR_ERROR_VALIDATION_FAILED, "clear_color_image inside a render pass");
+    if (!t || !clear_value) return latch(c, ZR_ERROR_VALIDATION_FAILED, "clear_color_image: NULL argument");
+    if (t->format == ZR_FORMAT_D32_SFLOAT) return latch(c, ZR_ERROR_VALIDATION_FAILED, "clear_color_image on a depth texture");
+    Cmd k;
+    k.type = C_CLEAR_IMAGE;
+    k.rendering.area = zr_rect2d{0, 0, t->width, t->height};
+    k.rendering.has_color = true;
+    k.rendering.color.texture = t;
+    k.rendering.color.load_op = ZR_ATTACHMENT_LOAD_OP_CLEAR;
+    for (int i = 0; i < 4; ++i) k.rendering.color.clear_value[i] = clear_value[i];
+    c->cmds.push_back(k);
 }
 
 ZR_API void zr_cmd_bind_pipeline(zr_cmd* c, const zr_pipeline* p) {

@@ -188,3 +188,22 @@ def render_scene(device: rhi.RenderDevice, scene: Scene, shard: Optional[tuple] 
     if depth is not None:
         depth.destroy()
     return out
+
+
+class SimpleAppRenderer:
+    """zenith-sandbox's SimpleApp (zenith-sandbox/src/main.rs:12-50): one lambda
+    node that clears the swapchain image to (0.2, 0.3, 0.8, 1.0) with
+    cmd_clear_color_image."""
+
+    CLEAR = (0.2, 0.3, 0.8, 1.0)  # main.rs:40
+
+    def __init__(self, device: rhi.RenderDevice):
+        self.device = device
+        self._encoder = rhi.CommandEncoder(device)
+
+    def render_to(self, output: rhi.Texture) -> rhi.CommandEncoder:
+        enc = self._encoder
+        enc.begin()
+        enc.clear_color_image(output, self.CLEAR)
+        enc.end()
+        return enc

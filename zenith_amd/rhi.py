@@ -552,6 +552,11 @@ class CommandEncoder:
         lib().zr_cmd_draw_indexed(self.handle, index_count, instance_count, first_index, vertex_offset,
                                   first_instance)
 
+    def clear_color_image(self, texture: "Texture", value=(0.0, 0.0, 0.0, 0.0)):
+        """vkCmdClearColorImage as zenith-sandbox records it through
+        CommandEncoder::custom (zenith-sandbox/src/main.rs:35-45)."""
+        lib().zr_cmd_clear_color_image(self.handle, texture.handle, C.byref((C.c_float * 4)(*value)))
+
     def set_tile_shard(self, rank: int, count: int, exchange=None):
         """Tile-row shard of the following render passes.  With ``exchange`` (a
         :class:`zenith_amd.shard.Exchange`) primitive setup is partitioned across

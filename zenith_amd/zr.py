@@ -211,6 +211,7 @@ _SIGS = {
     "zr_cmd_draw": (None, [_P, C.c_uint32, C.c_uint32, C.c_uint32, C.c_uint32]),
     "zr_cmd_draw_indexed": (None, [_P, C.c_uint32, C.c_uint32, C.c_uint32, C.c_int32, C.c_uint32]),
     "zr_cmd_set_tile_shard": (None, [_P, C.c_uint32, C.c_uint32]),
+    "zr_cmd_clear_color_image": (None, [_P, _P, C.POINTER(C.c_float * 4)]),
     "zr_cmd_set_tile_shard_exchange": (None, [_P, C.c_uint32, C.c_uint32, _P, _P]),
     "zr_device_set_stream": (_R, [_P, _P]),
     "zr_device_stream": (_P, [_P]),
