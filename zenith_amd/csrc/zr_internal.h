@@ -203,6 +203,7 @@ struct DrawParams {
     uint32_t setup_batch;     // primitives per lane in flight (template instance of k_setup_bin)
     uint32_t setup_sched;     // unit schedule: 0 contiguous per workgroup, 1 interleaved (u % G)
     uint32_t bbox_lds;        // 0: bboxes in global memory; else LDS entries per workgroup (own units * unit size)
+    uint32_t* wg_offsets;     // split setup: [setup_wgs][ntiles] each workgroup's offsets in the tile lists
     uint32_t debug;           // kDebug* bits (timing experiments only)
     unsigned long long* dbg_ts; // [setup_wgs][8] s_memrealtime stamps (kDebugStamps only)
     uint32_t* status;         // host-mapped
@@ -226,6 +227,8 @@ size_t setup_bin_lds_bytes(uint32_t ntiles, uint32_t bbox_entries);
 const void* setup_bin_kernel(uint32_t batch, bool mesh);
 void launch_tile(const DrawParams& p, void* stream);
 void launch_clear(const DrawParams& p, void* stream);
-void launch_route(const DrawParams& p, void* stream);     // partitioned setup: route own range (2 kernels)
+void launch_route(const DrawParams& p, void* stream);
+void launch_setup_split(const DrawParams& p, int pass, void* stream);  // k_setup_bin's halves, 2 launches
+const void* setup_split_kernel(int pass);     // partitioned setup: route own range (2 kernels)
 
 }  // namespace zr

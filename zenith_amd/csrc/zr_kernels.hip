@@ -763,7 +763,12 @@ __device__ __forceinline__ uint32_t own_unit(const DrawParams& P, uint32_t units
     return w + i * G;
 }
 
-template <uint32_t KB, bool MESH>
+// PASS 0: the whole persistent kernel.  PASS 1 / 2: its halves on either side of
+// the grid barrier as two launches (no co-residency needed, so the first half of
+// draw i+1 can fill CUs the tile pass of draw i frees): pass 1
+// leaves each workgroup's per-tile offsets in P.wg_offsets and the bboxes in
+// P.bboxes, pass 2 reloads them.
+template <uint32_t KB, bool MESH, int PASS>
 __global__ __launch_bounds__(kSetupThreads) void k_setup_bin(DrawParams P) {
     extern __shared__ __attribute__((aligned(16))) uint32_t s_lds[];  // [2 * ntiles + kSetupMiscWords] + bboxes
     const uint32_t nt = P.ntiles, G = gridDim.x, w = blockIdx.x, tid = threadIdx.x;
@@ -794,7 +799,7 @@ __global__ __launch_bounds__(kSetupThreads) void k_setup_bin(DrawParams P) {
 
     // ---- phase 1
     int nvalid = 0, ndropped = 0;
-    {
+    if (PASS != 2) {
         const uint32_t lane = tid & 63u, wave = tid >> 6;
         const uint32_t rounds = (1u << P.unit_shift) / (64u * KB);
         for (uint32_t i = 0;; ++i) {
@@ -828,23 +833,32 @@ __global__ __launch_bounds__(kSetupThreads) void k_setup_bin(DrawParams P) {
     ZR_STAMP(1);
     if (P.debug & kDebugPhase1Only) return;
 
-    // ---- phase 2: reserve this workgroup's slots in every tile's list.  Each
-    // workgroup starts at a different 64-tile block so that the workgroups' adds
-    // spread over the counter lines instead of all queueing on the same ones.
-    {
+    if (PASS != 2) {
+        // ---- phase 2: reserve this workgroup's slots in every tile's list.  Each
+        // workgroup starts at a different 64-tile block so that the workgroups' adds
+        // spread over the counter lines instead of all queueing on the same ones.
         const uint32_t rot = nt ? ((w * 64u) % nt) : 0u;
         for (uint32_t i = tid; i < nt; i += kSetupThreads) {
             const uint32_t t = i + rot < nt ? i + rot : i + rot - nt;
             const uint32_t c = s_hist[t];
             s_hist[t] = c ? __hip_atomic_fetch_add(&P.tile_counts[t], c, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) : 0u;
         }
-    }
-    if (tid == 0) {
-        if (s_misc[0]) atomicAdd(&P.counters[kCtSetup], s_misc[0]);
-        if (s_misc[1]) atomicAdd(&P.counters[kCtDropped], s_misc[1]);
+        if (tid == 0) {
+            if (s_misc[0]) atomicAdd(&P.counters[kCtSetup], s_misc[0]);
+            if (s_misc[1]) atomicAdd(&P.counters[kCtDropped], s_misc[1]);
+        }
     }
     ZR_STAMP(2);
-    grid_barrier(P.counters, G, w, P.status, !P.bbox_lds);
+    if (PASS == 1) {  // the second launch continues from here
+        __syncthreads();
+        for (uint32_t t = tid; t < nt; t += kSetupThreads) P.wg_offsets[(size_t)w * nt + t] = s_hist[t];
+        return;
+    }
+    if (PASS == 0) grid_barrier(P.counters, G, w, P.status, !P.bbox_lds);
+    if (PASS == 2) {
+        for (uint32_t t = tid; t < nt; t += kSetupThreads) s_hist[t] = P.wg_offsets[(size_t)w * nt + t];
+        __syncthreads();
+    }
     ZR_STAMP(3);
     if (P.debug & kDebugStopAfterScan) return;
 
@@ -1526,25 +1540,39 @@ size_t setup_bin_lds_bytes(uint32_t ntiles, uint32_t bbox_entries) {
 }
 
 const void* setup_bin_kernel(uint32_t batch, bool mesh) {
-    if (mesh) return reinterpret_cast<const void*>(&k_setup_bin<1, true>);
+    if (mesh) return reinterpret_cast<const void*>(&k_setup_bin<1, true, 0>);
     switch (batch) {
-    case 1: return reinterpret_cast<const void*>(&k_setup_bin<1, false>);
-    case 2: return reinterpret_cast<const void*>(&k_setup_bin<2, false>);
-    default: return reinterpret_cast<const void*>(&k_setup_bin<4, false>);
+    case 1: return reinterpret_cast<const void*>(&k_setup_bin<1, false, 0>);
+    case 2: return reinterpret_cast<const void*>(&k_setup_bin<2, false, 0>);
+    default: return reinterpret_cast<const void*>(&k_setup_bin<4, false, 0>);
     }
+}
+
+const void* setup_split_kernel(int pass) {
+    return pass == 1 ? reinterpret_cast<const void*>(&k_setup_bin<2, false, 1>)
+                     : reinterpret_cast<const void*>(&k_setup_bin<2, false, 2>);
+}
+
+void launch_setup_split(const DrawParams& p, int pass, void* stream) {
+    const size_t lds = setup_bin_lds_bytes(p.ntiles, 0);
+    const hipStream_t s = (hipStream_t)stream;
+    if (pass == 1)
+        hipLaunchKernelGGL((k_setup_bin<2, false, 1>), dim3(p.setup_wgs), dim3(kSetupThreads), lds, s, p);
+    else
+        hipLaunchKernelGGL((k_setup_bin<2, false, 2>), dim3(p.setup_wgs), dim3(kSetupThreads), lds, s, p);
 }
 
 void launch_setup_bin(const DrawParams& p, void* stream) {
     const size_t lds = setup_bin_lds_bytes(p.ntiles, p.bbox_lds);
     const hipStream_t s = (hipStream_t)stream;
     if (p.program == kProgMesh) {  // batch 1: the clip path is heavy
-        hipLaunchKernelGGL((k_setup_bin<1, true>), dim3(p.setup_wgs), dim3(kSetupThreads), lds, s, p);
+        hipLaunchKernelGGL((k_setup_bin<1, true, 0>), dim3(p.setup_wgs), dim3(kSetupThreads), lds, s, p);
         return;
     }
     switch (p.setup_batch) {
-    case 1: hipLaunchKernelGGL((k_setup_bin<1, false>), dim3(p.setup_wgs), dim3(kSetupThreads), lds, s, p); break;
-    case 2: hipLaunchKernelGGL((k_setup_bin<2, false>), dim3(p.setup_wgs), dim3(kSetupThreads), lds, s, p); break;
-    default: hipLaunchKernelGGL((k_setup_bin<4, false>), dim3(p.setup_wgs), dim3(kSetupThreads), lds, s, p); break;
+    case 1: hipLaunchKernelGGL((k_setup_bin<1, false, 0>), dim3(p.setup_wgs), dim3(kSetupThreads), lds, s, p); break;
+    case 2: hipLaunchKernelGGL((k_setup_bin<2, false, 0>), dim3(p.setup_wgs), dim3(kSetupThreads), lds, s, p); break;
+    default: hipLaunchKernelGGL((k_setup_bin<4, false, 0>), dim3(p.setup_wgs), dim3(kSetupThreads), lds, s, p); break;
     }
 }
 

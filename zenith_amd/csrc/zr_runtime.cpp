@@ -205,6 +205,8 @@ struct ScratchSet {
     uint64_t rmasks_cap = 0;
     uint32_t* rcounts = nullptr;// route: ids per chunk and destination
     uint64_t rcounts_cap = 0;
+    uint32_t* wg_offsets = nullptr;  // split setup: per-workgroup tile offsets
+    uint64_t wg_offsets_cap = 0;
     hipEvent_t setup_done = nullptr;  // k_setup_bin of the last draw that used this set
     hipEvent_t tile_done = nullptr;   // k_tile of the last draw that used this set
     bool tile_done_valid = false;
@@ -228,6 +230,12 @@ struct zr_device_t {
     // early workgroups hold CU slots at the grid barrier while the tile pass of the
     // previous draw still needs them).  Default: one stream, set 0.
     bool overlap = false;
+    // k_setup_bin as two launches split at its grid barrier, on the setup stream,
+    // so draw i+1's setup fills CUs draw i's tile pass frees.  Measured (1 GPU):
+    // C1 (100k tris) 1180 -> 1274 Mtri/s, C2 7925 -> 8007, C3 equal, C4 (10M)
+    // 25.1 -> 23.8 G (the co-running passes contend), so by default only draws of
+    // <= 2^18 primitives split.  ZR_SETUP_SPLIT=0 / 1 forces it off / on.
+    int setup_split = -1;
     int cu_count = 0;
     uint32_t occupancy_checked_tiles = 0;
     bool occupancy_checked_mesh = false;
@@ -236,6 +244,7 @@ struct zr_device_t {
     uint32_t tile_threads = 0; // k_tile workgroup size override (ZR_TILE_NT: 256, 512; 0 = by tile count)
     uint32_t debug = 0;
     uint64_t initial_bins = 0;  // 0 = max(2^20, 2 * primitives of the first draw)
+    uint64_t min_bins = 0;      // bin capacity an overflow asked for
     unsigned long long* dbg_ts = nullptr;  // kDebugStamps
     uint32_t dbg_wgs = 0, dbg_tiles = 0;
     std::string dbg_ts_path;
@@ -431,6 +440,7 @@ zr_result device_sync(zr_device* d) {
         // buffer for the largest draw seen so later draws read tile lists again.
         const uint64_t need = (uint64_t)st[kStMaxPairs] * 5 / 4 + 4096;
         st[kStOverflow] = 0;
+        d->min_bins = std::max(d->min_bins, need);  // also for a scratch set not allocated yet
         for (ScratchSet& S : d->sets) {
             if (!S.bins || S.bins_cap >= need) continue;
             ZR_HIP(hipFree(S.bins));
@@ -543,7 +553,7 @@ zr_result ensure_scratch(zr_device* d, ScratchSet& S, DrawParams& P) {
         ZR_HIP(hipMemset(S.counters, 0, S.counters_cap * 4));
     }
     if (!S.bins) {
-        const uint64_t want = d->initial_bins ? d->initial_bins : std::max<uint64_t>(1u << 20, prims * 2);
+        const uint64_t want = std::max(d->min_bins, d->initial_bins ? d->initial_bins : std::max<uint64_t>(1u << 20, prims * 2));
         if ((rc = grow(d, S.bins, S.bins_cap, want, 4))) return rc;
     }
     if (!S.setup_done) {
@@ -711,6 +721,11 @@ zr_result exec_draw(zr_device* d, ExecState& s, const Cmd& c, bool indexed) {
         // (mesh: fans 1 and 2 keep their bboxes in global memory, so all of them do)
         P.bbox_lds = (!mesh && entries * sizeof(BBox) <= budget) ? (uint32_t)entries : 0u;
     }
+    // split setup: default batch, not mesh / list mode; bboxes and per-workgroup
+    // offsets cross the launch boundary through global memory
+    const bool split = (d->setup_split > 0 || (d->setup_split < 0 && prims <= (1u << 18))) && !mesh &&
+                       !partitioned && !d->use_graphs && !d->debug && P.setup_batch == 2;
+    if (split) P.bbox_lds = 0;
     P.tile_threads = d->tile_threads ? d->tile_threads : tile_threads_for(P.ntiles, (uint32_t)std::max(d->cu_count, 1));
     P.debug = d->debug;
     if (d->debug & kDebugStamps) {
@@ -724,7 +739,7 @@ zr_result exec_draw(zr_device* d, ExecState& s, const Cmd& c, bool indexed) {
     // Partitioned draws always use both scratch sets and streams: the route and the
     // exchange of draw i+1 run on setup_stream while draw i's setup + tile pass
     // run on the main stream.
-    const bool overlap = (d->overlap && !d->debug && !d->use_graphs) || partitioned;
+    const bool overlap = (d->overlap && !d->debug && !d->use_graphs) || partitioned || split;
     ScratchSet& S = d->sets[overlap ? d->cur_set : 0];
     if (overlap) d->cur_set ^= 1u;
     if ((rc = ensure_scratch(d, S, P))) return rc;
@@ -762,6 +777,15 @@ zr_result exec_draw(zr_device* d, ExecState& s, const Cmd& c, bool indexed) {
         ZR_HIP(hipEventRecord(S.setup_done, ss));
         ZR_HIP(hipStreamWaitEvent(d->stream, S.setup_done, 0));
         timed_launch(d, "setup_bin", d->stream, [&] { launch_setup_bin(P, d->stream); });
+    } else if (split) {
+        if ((rc = grow(d, S.wg_offsets, S.wg_offsets_cap, (uint64_t)P.setup_wgs * P.ntiles, 4))) return rc;
+        P.wg_offsets = S.wg_offsets;
+        timed_launch(d, "setup_bin", ss, [&] {
+            launch_setup_split(P, 1, ss);
+            launch_setup_split(P, 2, ss);
+        });
+        ZR_HIP(hipEventRecord(S.setup_done, ss));
+        ZR_HIP(hipStreamWaitEvent(d->stream, S.setup_done, 0));
     } else {
         timed_launch(d, "setup_bin", ss, [&] { launch_setup_bin(P, ss); });
         if (overlap) {
@@ -884,6 +908,7 @@ ZR_API zr_result zr_device_create(int32_t hip_device, zr_device** out) {
     if (const char* cap = getenv("ZR_BIN_CAPACITY")) d->initial_bins = std::max<uint64_t>(64, strtoull(cap, nullptr, 0));
     if (const char* g = getenv("ZR_GRAPH")) d->use_graphs = strtoul(g, nullptr, 0) != 0;
     if (const char* o = getenv("ZR_OVERLAP")) d->overlap = strtoul(o, nullptr, 0) != 0;
+    if (const char* o = getenv("ZR_SETUP_SPLIT")) d->setup_split = strtoul(o, nullptr, 0) != 0 ? 1 : 0;
     if (const char* sc = getenv("ZR_SETUP_SCHED")) d->setup_sched = std::min<uint32_t>(1, (uint32_t)strtoul(sc, nullptr, 0));
     if (const char* nt = getenv("ZR_TILE_NT")) {
         const unsigned long v = strtoul(nt, nullptr, 0);
@@ -902,6 +927,9 @@ ZR_API zr_result zr_device_create(int32_t hip_device, zr_device** out) {
                                    (int)kSetupLdsBudget));
     ZR_HIP(hipFuncSetAttribute(setup_bin_kernel(1, true), hipFuncAttributeMaxDynamicSharedMemorySize,
                                (int)kSetupLdsBudget));
+    for (int pass : {1, 2})
+        ZR_HIP(hipFuncSetAttribute(setup_split_kernel(pass), hipFuncAttributeMaxDynamicSharedMemorySize,
+                                   (int)kSetupLdsBudget));
     ZR_HIP(hipDeviceGetAttribute(&d->cu_count, hipDeviceAttributeMultiprocessorCount, hip_device));
     void* st = nullptr;
     ZR_HIP(hipHostMalloc(&st, kStWords * 4, hipHostMallocMapped));
@@ -925,7 +953,7 @@ ZR_API void zr_device_destroy(zr_device* d) {
     for (ScratchSet& S : d->sets) {
         for (void* p : {(void*)S.records, (void*)S.records_big, (void*)S.bboxes, (void*)S.tile_counts,
                         (void*)S.tile_offsets, (void*)S.counters, (void*)S.bins, (void*)S.xsend, (void*)S.xrecv,
-                        (void*)S.gids, (void*)S.rmasks, (void*)S.rcounts})
+                        (void*)S.gids, (void*)S.rmasks, (void*)S.rcounts, (void*)S.wg_offsets})
             if (p) (void)hipFree(p);
         if (S.setup_done) (void)hipEventDestroy(S.setup_done);
         if (S.tile_done) (void)hipEventDestroy(S.tile_done);
