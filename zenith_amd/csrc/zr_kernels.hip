@@ -33,6 +33,10 @@ namespace zr {
 #ifndef ZR_TILE_LPT
 #define ZR_TILE_LPT 1        // waves claim raster chunks largest-first from an LDS counter (0: static)
 #endif
+#ifndef ZR_TILE_WIDE
+#define ZR_TILE_WIDE 0       // 1: bbox ∩ tile of 253+ px goes to the wave path instead of one lane
+                             // (measured: cerberus tile pass 124 -> 107 us, C3 306 -> 327, C2 77 -> 79)
+#endif
 #ifndef ZR_TILE_SUBLANE
 #define ZR_TILE_SUBLANE 1    // sparse segments: k lanes per entry split its bbox rows (0: one lane per entry)
 #endif
@@ -1444,17 +1448,27 @@ __global__ __launch_bounds__(NT, ZR_TILE_WGS * kTileThreads / NT) void k_tile(Dr
                 const bool valid = j < n && !(P.debug & kDebugLoadOnly);
                 if (P.debug & kDebugLoadOnly) asm volatile("" ::"v"(q0.x), "v"(q1.x), "v"(my_prim));
                 const bool large = compact_is_large(q0);
-                if (valid && !large) {
+                // wide: bbox ∩ tile of 253+ pixels (the last sort bucket, which lumps
+                // 253..1024); one lane would walk them for up to 1024 steps
+                const bool wide = ZR_TILE_WIDE && j >= s_bucket[kSortBuckets - 1];
+                if (valid && !large && !wide) {
                     const TriRecord r = decode_compact(P, q0, q1, true);
                     raster_lane<MODE, INITD>(P, r, entry_seq<PROG>(P, my_prim), x0, y0, s_key, s_initd, sub, (int)ksh);
                 }
-                // large primitives: the whole wave sweeps one primitive at a time (full record)
-                unsigned long long big = __ballot(valid && large && sub == 0);
+                // large and wide primitives: the whole wave sweeps one at a time
+                unsigned long long big = __ballot(valid && (large || wide) && sub == 0);
                 while (big) {
                     const uint32_t i = (uint32_t)__builtin_ctzll(big);
                     big &= big - 1ull;
                     const uint32_t prim = (uint32_t)rl((int)my_prim, i);
-                    const TriRecord r = load_uniform_record(P.records_big + prim);
+                    TriRecord r;
+                    if (rl((int)large, i)) {
+                        r = load_uniform_record(P.records_big + prim);
+                    } else {
+                        const int4 a = make_int4(rl(q0.x, i), rl(q0.y, i), rl(q0.z, i), rl(q0.w, i));
+                        const int4 b = make_int4(rl(q1.x, i), rl(q1.y, i), rl(q1.z, i), rl(q1.w, i));
+                        r = decode_compact(P, a, b, true);
+                    }
                     raster_prim<MODE, INITD>(P, r, entry_seq<PROG>(P, prim), x0, y0, lane, s_key, s_initd);
                 }
             }
