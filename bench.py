@@ -154,7 +154,15 @@ def main():
     exchange = None
     runtime_comm = distributed and a.comm == "runtime"
     if runtime_comm:
-        shard.init_runtime_rccl(dev, rank, world)
+        # every rank must be able to load RCCL before any joins a communicator
+        # (a rank that cannot would leave the others blocked in the init)
+        ok = torch.tensor([1 if shard.runtime_rccl_available() else 0], device=cuda)
+        dist.all_reduce(ok, op=dist.ReduceOp.MIN)
+        if int(ok.item()):
+            shard.init_runtime_rccl(dev, rank, world)
+        else:
+            runtime_comm = False
+            print("bench: the runtime cannot load RCCL on every rank; using torch.distributed's", file=sys.stderr)
     if a.setup == "partitioned" and runtime_comm:
         exchange = "rccl"
     elif a.setup == "partitioned" and distributed:
@@ -277,7 +285,8 @@ def main():
                    "triangles": N, "width": W, "height": H, "tile": shard.TILE,
                    "parallelism": f"tile-rows x{world}" + (
                        f", {a.setup} setup" + (" (RCCL all-to-all)" if exchange is not None else "")
-                       + f" + RCCL row gather ({a.comm} communicators)" if distributed else "")},
+                       + f" + RCCL row gather ({'runtime' if runtime_comm else 'torch'} communicators)"
+                       if distributed else "")},
         "fps": round(1e3 / ms_per_step, 2),
         "ms_per_step_profiled": round((tp1 - tp0) / a.steps * 1e3, 4),
         "host_enqueue_ms_per_step": round((t_enq - t0) / a.steps * 1e3, 4),

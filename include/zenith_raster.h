@@ -357,6 +357,7 @@ ZR_API void zr_cmd_set_tile_shard_exchange(zr_cmd *cmd, uint32_t rank, uint32_t 
  * RCCL is loaded at run time (the process's copy if one is loaded, else
  * librccl.so); ZR_ERROR_INITIALIZATION_FAILED when unavailable. */
 #define ZR_RCCL_ID_BYTES 128
+ZR_API int32_t zr_rccl_available(void); /* 1 if RCCL can be loaded in this process */
 ZR_API zr_result zr_rccl_get_unique_id(void *out);
 ZR_API zr_result zr_device_init_rccl(zr_device *dev, const void *exchange_id, const void *gather_id, int32_t nranks,
                                      int32_t rank);

@@ -1594,6 +1594,11 @@ zr_result rccl_exchange(void* user, void* stream, const void* send, void* recv, 
 
 }  // namespace
 
+ZR_API int32_t zr_rccl_available(void) {
+    std::string err;
+    return rccl_load(err) ? 1 : 0;
+}
+
 ZR_API zr_result zr_rccl_get_unique_id(void* out) {
     if (!out) return fail(ZR_ERROR_VALIDATION_FAILED, "out is NULL");
     std::string err;

@@ -206,6 +206,12 @@ class ThreadGroupExchange(Exchange):
         g.barrier.wait()  # every rank copied before any send buffer is rewritten
 
 
+def runtime_rccl_available() -> bool:
+    """True if libzenith_raster can load RCCL in this process."""
+    from . import zr
+    return zr.lib().zr_rccl_available() == 1
+
+
 def init_runtime_rccl(device, rank: int, world: int, group=None) -> None:
     """Gives ``device`` (rhi.RenderDevice) the runtime's own RCCL communicators:
     rank 0 makes the two ids, torch.distributed carries them to every rank, and

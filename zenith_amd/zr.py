@@ -215,6 +215,7 @@ _SIGS = {
     "zr_cmd_set_tile_shard_exchange": (None, [_P, C.c_uint32, C.c_uint32, _P, _P]),
     "zr_device_set_stream": (_R, [_P, _P]),
     "zr_device_stream": (_P, [_P]),
+    "zr_rccl_available": (C.c_int32, []),
     "zr_rccl_get_unique_id": (_R, [_P]),
     "zr_device_init_rccl": (_R, [_P, _P, _P, C.c_int32, C.c_int32]),
     "zr_rccl_exchange_fn": (_P, []),
