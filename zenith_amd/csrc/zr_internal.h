@@ -116,15 +116,14 @@ enum StatusWord : uint32_t {
     kStBarrierTimeout = 5,
     kStWords = 16,
 };
-// Device-side counters (zeroed with the tile counts before each draw).
-// Device counters of k_setup_bin.  Zero between draws: the last workgroup to
-// finish (kCtExit) resets them, so a draw needs no memset launch.
+// Device counters of k_setup_bin.  Zero between draws: the draw's k_tile resets
+// them (and the tile counts), so a draw needs no memset launch.
 // The grid barrier is two-level (arrivals on 8 group counters, blockIdx % 8, then
 // one top counter; release through 8 group flags), each word on a 128-B line of
 // its own: 256 workgroups on one counter cost ~10 us after the last arrival.
 constexpr uint32_t kBarrierGroups = 8;
 enum CounterWord : uint32_t {
-    kCtSetup = 0, kCtDropped = 1, kCtExit = 3,
+    kCtSetup = 0, kCtDropped = 1,
     kCtGroup = 32,                            // + 32 * group: arrivals of the group
     kCtTop = 32 * (1 + kBarrierGroups),       // groups complete
     kCtRelease = 32 * (2 + kBarrierGroups),   // + 32 * group: barrier open

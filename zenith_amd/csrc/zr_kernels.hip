@@ -925,25 +925,8 @@ __global__ __launch_bounds__(kSetupThreads) void k_setup_bin(DrawParams P) {
         }
     }
     ZR_STAMP(5);
-    // Every workgroup has left the barrier and read the tile totals once it counts
-    // itself out here, so the last one can zero the counters for the next draw.
-    if (tid == 0) {
-        const uint32_t prev = __hip_atomic_fetch_add(&P.counters[kCtExit], 1u, __ATOMIC_RELAXED,
-                                                     __HIP_MEMORY_SCOPE_AGENT);
-        s_misc[2] = prev == G - 1u ? 1u : 0u;
-        if (prev == G - 1u) {
-            // every workgroup's count adds were performed before its exit add (its
-            // wave 0 waited for the exit add's return, which follows them in order)
-            volatile uint32_t* st = P.status;
-            st[kStTrianglesSetup] = __hip_atomic_load(&P.counters[kCtSetup], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-            st[kStDroppedClip] = __hip_atomic_load(&P.counters[kCtDropped], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-        }
-    }
-    __syncthreads();
-    if (s_misc[2]) {
-        for (uint32_t t = tid; t < nt; t += kSetupThreads) st_sc1(&P.tile_counts[t], 0u);
-        for (uint32_t i = tid; i < kCtWords; i += kSetupThreads) st_sc1(&P.counters[i], 0u);
-    }
+    // The counters go back to zero in k_tile (it runs after every workgroup here
+    // read them): an exit fan-in of all workgroups on one counter cost ~3 us.
     ZR_STAMP(6);
 }
 
@@ -1368,7 +1351,18 @@ __global__ __launch_bounds__(NT, ZR_TILE_WGS * kTileThreads / NT) void k_tile(Dr
     }
     if (threadIdx.x < 255) s_srgb[threadIdx.x] = c_srgbT[threadIdx.x];
     if (threadIdx.x == 0) s_any = 0xFFFFFFFFu;
+    // k_setup_bin's counters back to zero for the next draw on this scratch set
+    // (the tile lists live in tile_offsets / bins): each tile its own count,
+    // tile 0 the grid counters, after reporting the draw's primitive stats
+    if (threadIdx.x == 0) P.tile_counts[t] = 0u;
+    if (t == 0 && threadIdx.x == 0) {
+        volatile uint32_t* st = P.status;
+        st[kStTrianglesSetup] = P.counters[kCtSetup];
+        st[kStDroppedClip] = P.counters[kCtDropped];
+    }
     __syncthreads();
+    if (t == 0)
+        for (uint32_t i = threadIdx.x; i < kCtWords; i += NT) P.counters[i] = 0u;
 
     const uint32_t wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
     const int lane = threadIdx.x & 63;

@@ -587,6 +587,7 @@ zr_result exec_draw(zr_device* d, ExecState& s, const Cmd& c, bool indexed) {
     memset(&P, 0, sizeof P);
     zr_result rc = fill_target(s, P);
     if (rc) return rc;
+    if (P.ntiles == 0) return ZR_SUCCESS;  // a tile-row shard that owns no row of this target
     if (!pp->has_fs) {
         P.color = nullptr;
         P.color_bpp = 0;
