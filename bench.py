@@ -236,11 +236,18 @@ def main():
     # ms_per_step_profiled, not used for `value`).
     dev.kernel_times(reset=True)
     dev.set_profiling(True)
+    # frame-boundary events on the raster stream: per-frame intervals (median / p90,
+    # SURVEY.md §8d) of the queued, steady-state frame stream
+    fev = [torch.cuda.Event(enable_timing=True) for _ in range(a.steps + 1)]
+    fev[0].record(main_stream)
     tp0 = time.perf_counter()
-    for _ in range(a.steps):
+    for i in range(a.steps):
         step()
+        fev[i + 1].record(main_stream)
     dev.wait_idle()
     tp1 = time.perf_counter()
+    torch.cuda.synchronize()
+    frame_ms = sorted(fev[i].elapsed_time(fev[i + 1]) for i in range(a.steps))
     dev.set_profiling(False)
     kt = dev.kernel_times()
     stats = dev.last_draw_stats()
@@ -290,6 +297,8 @@ def main():
         "fps": round(1e3 / ms_per_step, 2),
         "ms_per_step_profiled": round((tp1 - tp0) / a.steps * 1e3, 4),
         "host_enqueue_ms_per_step": round((t_enq - t0) / a.steps * 1e3, 4),
+        "frame_ms_median_profiled": round(frame_ms[len(frame_ms) // 2], 4),
+        "frame_ms_p90_profiled": round(frame_ms[min(len(frame_ms) - 1, (9 * len(frame_ms)) // 10)], 4),
         "host_submit_ms_per_step": round(host_t[0] / a.steps * 1e3, 4),
         "host_gather_ms_per_step": round(host_t[1] / a.steps * 1e3, 4),
         "frame_alg_bytes": frame_bytes,

@@ -33,6 +33,9 @@ namespace zr {
 #ifndef ZR_TILE_LPT
 #define ZR_TILE_LPT 1        // waves claim raster chunks largest-first from an LDS counter (0: static)
 #endif
+#ifndef ZR_RESOLVE_BATCH
+#define ZR_RESOLVE_BATCH 2   // pixels per thread whose gathers are in flight together in the resolve
+#endif
 #ifndef ZR_TILE_WIDE
 #define ZR_TILE_WIDE 0       // 1: bbox ∩ tile of 253+ px goes to the wave path instead of one lane
                              // (measured: cerberus tile pass 124 -> 107 us, C3 306 -> 327, C2 77 -> 79)
@@ -1229,7 +1232,7 @@ template <int PROG, int MODE, bool IDX32, int NT>
 __device__ __forceinline__ void resolve_pixels(const DrawParams& P, int x0, int y0, uint32_t cnt, uint32_t fallback,
                                                const unsigned long long* s_key, const float* s_srgb) {
     constexpr int kPer = kTilePixels / NT;
-    constexpr int kB = kPer < 2 ? kPer : 2;
+    constexpr int kB = kPer < ZR_RESOLVE_BATCH ? kPer : ZR_RESOLVE_BATCH;
     // recomputed here, not reused from the tile's init: a pixel coordinate kept
     // live across the raster loop spills at 64 VGPRs
     int tid = (int)threadIdx.x;
