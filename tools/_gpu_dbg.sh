@@ -1,4 +1,4 @@
 set -o pipefail
-O=gpurun_out/dbg1; mkdir -p $O
-ZR_DEBUG=128 ZR_DEBUG_TS=$O/stamps_cerb.txt timeout -k 10 200 python bench.py --config cerberus --steps 3 --warmup 1 --no-cpu-baseline > $O/dbg.json 2>> $O/err || exit 1
+O=gpurun_out/dbg2; mkdir -p $O
+for v in 0 16 1 2 3; do ZR_DEBUG=$v timeout -k 10 120 python bench.py --no-cpu-baseline > $O/d$v.json 2>>$O/err || exit 1; done
 echo done

@@ -234,7 +234,8 @@ struct zr_device_t {
     // so draw i+1's setup fills CUs draw i's tile pass frees.  Measured (1 GPU):
     // C1 (100k tris) 1180 -> 1274 Mtri/s, C2 7925 -> 8007, C3 equal, C4 (10M)
     // 25.1 -> 23.8 G (the co-running passes contend), so by default only draws of
-    // <= 2^18 primitives split.  ZR_SETUP_SPLIT=0 / 1 forces it off / on.
+    // <= 2^18 primitives split, and tile-row shards (whose tile pass leaves most
+    // CUs idle: C2 G=2/4/8 +2.8/+2.3/+0.7 %, C3 G=8 +7 %).  ZR_SETUP_SPLIT=0 / 1 forces it off / on.
     int setup_split = -1;
     int cu_count = 0;
     uint32_t occupancy_checked_tiles = 0;
@@ -724,7 +725,7 @@ zr_result exec_draw(zr_device* d, ExecState& s, const Cmd& c, bool indexed) {
     }
     // split setup: default batch, not mesh / list mode; bboxes and per-workgroup
     // offsets cross the launch boundary through global memory
-    const bool split = (d->setup_split > 0 || (d->setup_split < 0 && prims <= (1u << 18))) && !mesh &&
+    const bool split = (d->setup_split > 0 || (d->setup_split < 0 && (prims <= (1u << 18) || P.shard_count > 1))) && !mesh &&
                        !partitioned && !d->use_graphs && !d->debug && P.setup_batch == 2;
     if (split) P.bbox_lds = 0;
     P.tile_threads = d->tile_threads ? d->tile_threads : tile_threads_for(P.ntiles, (uint32_t)std::max(d->cu_count, 1));
