@@ -332,10 +332,15 @@ def mesh_scene(vertices: np.ndarray, indices: np.ndarray, width: int, height: in
 def cerberus_scene(width: int = 640, height: int = 480, eye=(291.6, -31.5, 111.9), target=(-3.7, -52.2, -14.2),
                    npz: str | None = None) -> Scene:
     """content/mesh/cerberus (33,543 triangles, CC-BY-4.0, tests/golden/CERBERUS.txt)
-    baked as gltf_loader.rs does, seen by a camera at `eye` looking at `target`."""
+    baked as gltf_loader.rs does, seen by a camera at `eye` looking at `target`.
+    `npz`: the fixture (default) or a baked ``.mesh`` file (assets.bake_gltf)."""
     import os
     path = npz or os.path.join(os.path.dirname(os.path.dirname(os.path.abspath(__file__))), CERBERUS_NPZ)
-    with np.load(path, allow_pickle=False) as z:
-        v, i = z["vertices"], z["indices"]
+    if path.endswith(".mesh"):  # zenith-asset's baked file (assets.load_mesh)
+        from .assets import load_mesh
+        v, i, _ = load_mesh(path)
+    else:
+        with np.load(path, allow_pickle=False) as z:
+            v, i = z["vertices"], z["indices"]
     fwd = tuple(float(t - e) for t, e in zip(target, eye))
     return mesh_scene(v, i, width, height, eye, fwd, name=f"cerberus_{width}x{height}")
