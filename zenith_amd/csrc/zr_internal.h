@@ -13,6 +13,8 @@ constexpr int kTilePixels = kTile * kTile;
 #endif
 constexpr int kTileThreads = ZR_TILE_THREADS;  // k_tile workgroup: 4 waves of 64 (build knob)
 constexpr uint32_t kSortCap = 1024;     // tile-list segment sorted by area in LDS
+constexpr uint32_t kBigQueue = 512;     // k_tile: queued wave-path primitives per segment
+constexpr uint32_t kBigWide = 0x80000000u;  // queue entry: wide compact primitive (ZR_TILE_WIDE)
 constexpr uint32_t kSortBuckets = 64;   // bbox-shape classes: 8 width classes x 8 height classes
 constexpr int kSetupThreads = 1024;  // setup / bin workgroups (one LDS histogram each)
 constexpr uint32_t kSetupLdsBudget = 160u * 1024u;     // one k_setup_bin workgroup per CU owns the LDS
@@ -176,6 +178,10 @@ struct DrawParams {
     // tiling / sharding
     uint32_t tiles_x, tiles_y, shard_rank, shard_count, owned_rows, ntiles;
     uint32_t tile_threads;    // k_tile workgroup size: 256 or 512 (tile_threads_for)
+    uint32_t tile_split;      // k_tile workgroups per tile (tile_split_for); > 1 uses the three below
+    unsigned long long* tile_keys;  // [ntiles][kTilePixels] merged visibility keys, ~0 between draws
+    uint32_t* tile_arrive;    // [ntiles] parts done, 0 between draws
+    uint32_t* tile_any;       // [ntiles] spill path: min primitive touching the tile, ~0 between draws
     // partitioned setup (list mode).  In list mode `prims` is the
     // capacity of the received blocks (shard_count * span); the setup pass runs
     // over the dense positions [0, sum of the blocks' counts).
@@ -190,6 +196,7 @@ struct DrawParams {
     // scratch (binning without contended global atomics)
     TriCompact* records;      // [prims] compact records (every binned primitive)
     TriRecord* records_big;   // [prims] full records, written for large primitives only
+    float4* mesh_edges;       // mesh program: [prims][3] homogeneous edge coefficients (shade_mesh)
     BBox* bboxes;             // [prims]; bb0 == kEmptyBox when culled / no owned tile
     uint32_t* tile_counts;    // [ntiles]
     uint32_t* tile_offsets;   // [ntiles] exclusive scan (list starts)
@@ -218,6 +225,24 @@ constexpr uint32_t kSetupMiscWords = 96;
 inline uint32_t tile_threads_for(uint32_t ntiles, uint32_t cus) {
     const uint32_t per_cu = ntiles / (cus ? cus : 1u);
     return per_cu >= 6u ? (uint32_t)kTileThreads : 512u;
+}
+
+#ifndef ZR_TILE_SPLIT_BUILD
+// Split tiles (DrawParams::tile_split) are built only on request: measured slower
+// on C2 shards (1 GPU, rank 0 of 8: tile pass 32.7 us at K = 1, 38.1 at 2, 42.1
+// at 4; with the setup overlap 74.6 vs 85.3 us per frame), because a tile's time
+// there is record-gather latency rather than raster work.
+#define ZR_TILE_SPLIT_BUILD 0
+#endif
+// k_tile workgroups per tile: the largest power of two <= 8 that keeps the pass
+// within the workgroups the CUs hold at once (4 per CU at 512 threads, 8 at 256),
+// so a pass of few tiles (tile-row shards) spreads each tile's list over K
+// workgroups instead of leaving CUs idle.
+inline uint32_t tile_split_for(uint32_t ntiles, uint32_t cus, uint32_t tile_threads) {
+    const uint64_t slots = (uint64_t)(cus ? cus : 1u) * (tile_threads >= 512u ? 4u : 8u);
+    uint32_t k = 1;
+    while (k < 8u && (uint64_t)ntiles * k * 2u <= slots) k *= 2u;
+    return k;
 }
 
 // Launchers (zr_kernels.hip).  All enqueue on `stream`; no host synchronisation.

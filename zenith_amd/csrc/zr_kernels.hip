@@ -503,6 +503,30 @@ __device__ __forceinline__ BBox write_record(const DrawParams& P, uint32_t rec, 
     return box;
 }
 
+// The mesh program's barycentric planes: with the homogeneous screen vertices
+// h_i = (x_i hw + w_i cx, y_i hh + w_i cy, w_i) of the primitive (not of its
+// clipped fans), E_i(p) = p . (h_j x h_k) = c0 fx + c1 fy + c2; e[3 i + n] = c_n
+// (zr_oracle.c shade, same operations).  Stored once per primitive by setup so the
+// resolve neither re-reads positions nor re-runs the vertex stage per pixel.
+__device__ __forceinline__ void mesh_edge_planes(const DrawParams& P, const float3 p[3], float e[9]) {
+    float hX[3], hY[3], hW[3];
+#pragma unroll
+    for (int k = 0; k < 3; ++k) {
+        float c[4];
+        mesh_transform(P.view_proj, p[k], c);
+        hX[k] = fmaf(c[0], P.hw, c[3] * P.cx);
+        hY[k] = fmaf(c[1], P.hh, c[3] * P.cy);
+        hW[k] = c[3];
+    }
+#pragma unroll
+    for (int i = 0; i < 3; ++i) {
+        const int j = (i + 1) % 3, k = (i + 2) % 3;
+        e[3 * i + 0] = hY[j] * hW[k] - hW[j] * hY[k];
+        e[3 * i + 1] = hW[j] * hX[k] - hX[j] * hW[k];
+        e[3 * i + 2] = hX[j] * hY[k] - hY[j] * hX[k];
+    }
+}
+
 // Setup record index of fan k of mesh primitive p (zr_internal.h kMeshFans).
 __device__ __forceinline__ uint32_t mesh_record(const DrawParams& P, uint32_t p, uint32_t k) {
     return k ? P.prims + 2u * p + k - 1u : p;
@@ -519,9 +543,21 @@ __device__ __forceinline__ void setup_finish_mesh(const DrawParams& P, uint32_t 
     MeshFans m;
     if (mesh_geometry(P, in, m, ndropped)) {
         ++nvalid;
+        bool owned = false;
         for (uint32_t k = 0; k < kMeshFans; ++k) {
             if (!((m.valid >> k) & 1u)) continue;
-            if (count_owned(P, m.f[k], s_hist)) box[k] = write_record(P, mesh_record(P, prim, k), m.f[k]);
+            if (count_owned(P, m.f[k], s_hist)) {
+                box[k] = write_record(P, mesh_record(P, prim, k), m.f[k]);
+                owned = true;
+            }
+        }
+        if (owned) {  // the resolve's barycentric planes (shade_mesh)
+            float e[9];
+            mesh_edge_planes(P, in.p, e);
+            float4* q = P.mesh_edges + (size_t)prim * 3u;
+            q[0] = make_float4(e[0], e[1], e[2], e[3]);
+            q[1] = make_float4(e[4], e[5], e[6], e[7]);
+            q[2] = make_float4(e[8], 0.0f, 0.0f, 0.0f);
         }
     }
     *bbox_out = box[0];
@@ -1171,30 +1207,18 @@ __device__ __forceinline__ uint32_t record_prim(const DrawParams& P, uint32_t e)
 // mesh.slang psmain: perspective-correct barycentrics of the primitive (not of
 // its clipped fan triangle) from its homogeneous screen vertices
 // h_i = (x_i hw + w_i cx, y_i hh + w_i cy, w_i): b_i = E_i / sum E with
-// E_i = p . (h_j x h_k) at the pixel centre; then normal and uv interpolated and
-// lit like blinn_phong.slang with kd = (0.35 + 0.3 u, 0.35 + 0.3 v, 0.7)
+// E_i = p . (h_j x h_k) at the pixel centre (the planes setup stored,
+// mesh_edge_planes); then normal and uv interpolated and lit like blinn_phong.slang with kd = (0.35 + 0.3 u, 0.35 + 0.3 v, 0.7)
 // (zr_oracle.c shade, same operation order).
-__device__ __forceinline__ void shade_mesh(const DrawParams& P, const uint32_t vid[3], int px, int py, float out[4]) {
-    float hX[3], hY[3], hW[3];
-#pragma unroll
-    for (int k = 0; k < 3; ++k) {
-        const float3 p = *reinterpret_cast<const float3*>(attr_ptr(P, vid[k], 0));
-        float c[4];
-        mesh_transform(P.view_proj, p, c);
-        hX[k] = fmaf(c[0], P.hw, c[3] * P.cx);
-        hY[k] = fmaf(c[1], P.hh, c[3] * P.cy);
-        hW[k] = c[3];
-    }
+__device__ __forceinline__ void shade_mesh(const DrawParams& P, uint32_t prim, const uint32_t vid[3], int px, int py,
+                                           float out[4]) {
+    const float4* q = P.mesh_edges + (size_t)prim * 3u;
+    const float4 qa = q[0], qb = q[1], qc = q[2];
+    const float c[9] = {qa.x, qa.y, qa.z, qa.w, qb.x, qb.y, qb.z, qb.w, qc.x};
     const float fx = (float)px + 0.5f, fy = (float)py + 0.5f;
     float E[3];
 #pragma unroll
-    for (int i = 0; i < 3; ++i) {
-        const int j = (i + 1) % 3, k = (i + 2) % 3;
-        const float c0 = hY[j] * hW[k] - hW[j] * hY[k];
-        const float c1 = hW[j] * hX[k] - hX[j] * hW[k];
-        const float c2 = hX[j] * hY[k] - hY[j] * hX[k];
-        E[i] = fmaf(c0, fx, fmaf(c1, fy, c2));
-    }
+    for (int i = 0; i < 3; ++i) E[i] = fmaf(c[3 * i], fx, fmaf(c[3 * i + 1], fy, c[3 * i + 2]));
     const float einv = 1.0f / ((E[0] + E[1]) + E[2]);
     const float b0 = E[0] * einv, b1 = E[1] * einv, b2 = E[2] * einv;
     const float* n0 = attr_ptr(P, vid[0], 1);
@@ -1279,7 +1303,7 @@ __device__ __forceinline__ void resolve_pixels(const DrawParams& P, int x0, int 
                 const EdgeEvalF e = eval_edges_f(r, px[b], py[b]);
                 col[b][0] = col[b][1] = col[b][2] = col[b][3] = 0.0f;
                 if (P.color_bpp && !(P.debug & kDebugSkipShade)) {
-                    if constexpr (PROG == kProgMesh) shade_mesh(P, vid[b], px[b], py[b], col[b]);
+                    if constexpr (PROG == kProgMesh) shade_mesh(P, gp[b], vid[b], px[b], py[b], col[b]);
                     else shade_winner<PROG>(P, r, e, col[b]);
                 }
                 zw[b] = (MODE == kDepthLastWins) ? interp_depth_f(r, e.f1, e.f2) : key_depth<MODE>(key[b]);
@@ -1316,11 +1340,31 @@ __global__ __launch_bounds__(NT, ZR_TILE_WGS * kTileThreads / NT) void k_tile(Dr
     __shared__ float s_srgb[256];
     __shared__ uint32_t s_any;  // spill path: some primitive touching the tile (resolve's in-bounds fallback)
     __shared__ uint32_t s_claim;  // next 64-entry chunk of the segment to rasterize
-    const uint32_t t = (P.debug & kDebugReverseTiles) ? P.ntiles - 1u - blockIdx.x : blockIdx.x;
+    // wave-path primitives of the segment (large / wide), rasterized after its
+    // chunks by whichever wave claims them next: the area sort groups them, so the
+    // wave owning their chunk would otherwise sweep them all alone
+    __shared__ uint32_t s_big[kBigQueue];
+    __shared__ uint32_t s_nbig, s_bclaim;
+    __shared__ uint32_t s_last;  // split tiles: this workgroup arrived last and resolves
+    // Split tiles (P.tile_split = K > 1, passes with few tiles per CU): K workgroups
+    // share a tile, each rasterizing a K-th of its list into LDS keys of its own;
+    // they merge them into the tile's global keys with 64-bit atomic mins, and the
+    // last to arrive resolves.  Workgroups b with equal b % 8 take the K parts of a
+    // tile, so they usually run on one XCD (correctness never depends on it).
+    const uint32_t K = ZR_TILE_SPLIT_BUILD ? P.tile_split : 1u;
+    uint32_t t, ks = 0;
+    if (K <= 1) {
+        t = (P.debug & kDebugReverseTiles) ? P.ntiles - 1u - blockIdx.x : blockIdx.x;
+    } else {
+        const uint32_t grp = blockIdx.x / (8u * K), r = blockIdx.x - grp * 8u * K;
+        t = grp * 8u + (r & 7u);
+        ks = r >> 3;
+        if (t >= P.ntiles) return;
+    }
     const uint32_t oy = t / P.tiles_x, tx = t - oy * P.tiles_x;
     const uint32_t ty = oy * P.shard_count + P.shard_rank;
     const int x0 = (int)tx * kTile, y0 = (int)ty * kTile;
-    const bool stamp = (P.debug & kDebugStamps) && threadIdx.x == 0 && t < kMaxTilesPerPass;
+    const bool stamp = (P.debug & kDebugStamps) && threadIdx.x == 0 && t < kMaxTilesPerPass && ks == 0;
     unsigned long long* ts = P.dbg_ts + 8192 * 8 + (size_t)t * 8;
     if (stamp) ts[0] = __builtin_amdgcn_s_memrealtime();
 
@@ -1332,7 +1376,10 @@ __global__ __launch_bounds__(NT, ZR_TILE_WGS * kTileThreads / NT) void k_tile(Dr
     // later draws) is rasterized exactly but slowly: every tile scans all records'
     // bboxes (k_setup_bin stored them) instead of reading its list.
     const bool spill = P.tile_offsets[P.ntiles] > P.bin_capacity;
-    const uint32_t cnt = spill ? 0u : end - begin;
+    const uint32_t cnt_all = spill ? 0u : end - begin;
+    // this workgroup's part of the list (all of it unless split)
+    const uint32_t lbeg = begin + (uint32_t)(((uint64_t)cnt_all * ks) / max(K, 1u));
+    const uint32_t cnt = begin + (uint32_t)(((uint64_t)cnt_all * (ks + 1u)) / max(K, 1u)) - lbeg;
     constexpr uint32_t kPerThread = kSortCap / NT;
     uint32_t ent[kPerThread];
     auto load_segment = [&](uint32_t seg) {
@@ -1340,7 +1387,7 @@ __global__ __launch_bounds__(NT, ZR_TILE_WGS * kTileThreads / NT) void k_tile(Dr
 #pragma unroll
         for (uint32_t k = 0; k < kPerThread; ++k) {
             const uint32_t i = threadIdx.x + k * NT;
-            ent[k] = i < n ? P.bins[begin + seg + i] : 0u;  // prim | area bucket (k_setup_bin phase 4)
+            ent[k] = i < n ? P.bins[lbeg + seg + i] : 0u;  // prim | area bucket (k_setup_bin phase 4)
         }
     };
     if (cnt && !(P.debug & kDebugSkipRaster)) load_segment(0);
@@ -1357,14 +1404,14 @@ __global__ __launch_bounds__(NT, ZR_TILE_WGS * kTileThreads / NT) void k_tile(Dr
     // k_setup_bin's counters back to zero for the next draw on this scratch set
     // (the tile lists live in tile_offsets / bins): each tile its own count,
     // tile 0 the grid counters, after reporting the draw's primitive stats
-    if (threadIdx.x == 0) P.tile_counts[t] = 0u;
-    if (t == 0 && threadIdx.x == 0) {
+    if (threadIdx.x == 0 && ks == 0) P.tile_counts[t] = 0u;
+    if (t == 0 && ks == 0 && threadIdx.x == 0) {
         volatile uint32_t* st = P.status;
         st[kStTrianglesSetup] = P.counters[kCtSetup];
         st[kStDroppedClip] = P.counters[kCtDropped];
     }
     __syncthreads();
-    if (t == 0)
+    if (t == 0 && ks == 0)
         for (uint32_t i = threadIdx.x; i < kCtWords; i += NT) P.counters[i] = 0u;
 
     const uint32_t wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
@@ -1380,7 +1427,7 @@ __global__ __launch_bounds__(NT, ZR_TILE_WGS * kTileThreads / NT) void k_tile(Dr
             const uint32_t n = min(kSortCap, cnt - seg);
             if (seg) load_segment(seg);
             if (threadIdx.x < kSortBuckets) s_bucket[threadIdx.x] = 0u;
-            if (threadIdx.x == 0) s_claim = 0u;
+            if (threadIdx.x == 0) s_claim = s_nbig = s_bclaim = 0u;
             __syncthreads();
             uint32_t pr[kPerThread], bk[kPerThread], sl[kPerThread];
 #pragma unroll
@@ -1452,8 +1499,21 @@ __global__ __launch_bounds__(NT, ZR_TILE_WGS * kTileThreads / NT) void k_tile(Dr
                     const TriRecord r = decode_compact(P, q0, q1, true);
                     raster_lane<MODE, INITD>(P, r, entry_seq<PROG>(P, my_prim), x0, y0, s_key, s_initd, sub, (int)ksh);
                 }
-                // large and wide primitives: the whole wave sweeps one at a time
-                unsigned long long big = __ballot(valid && (large || wide) && sub == 0);
+                // large and wide primitives: queued for the segment's wave pass; the
+                // whole wave sweeps them itself only when the queue is full
+                const bool is_big = valid && (large || wide) && sub == 0;
+                unsigned long long big = __ballot(is_big);
+                if (big) {
+                    uint32_t base = 0;
+                    if (lane == 0) base = atomicAdd(&s_nbig, (uint32_t)__popcll(big));
+                    base = (uint32_t)__builtin_amdgcn_readfirstlane((int)base);
+                    if (base + (uint32_t)__popcll(big) <= kBigQueue) {
+                        if (is_big)
+                            s_big[base + (uint32_t)__popcll(big & ((1ull << lane) - 1ull))] =
+                                my_prim | (large ? 0u : kBigWide);
+                        big = 0;
+                    }
+                }
                 while (big) {
                     const uint32_t i = (uint32_t)__builtin_ctzll(big);
                     big &= big - 1ull;
@@ -1470,10 +1530,29 @@ __global__ __launch_bounds__(NT, ZR_TILE_WGS * kTileThreads / NT) void k_tile(Dr
                 }
             }
             __syncthreads();
+            const uint32_t nbig = min(s_nbig, kBigQueue);
+            for (;;) {  // the segment's queued wave-path primitives, one per claim
+                uint32_t i = 0;
+                if (lane == 0) i = atomicAdd(&s_bclaim, 1u);
+                i = (uint32_t)__builtin_amdgcn_readfirstlane((int)i);
+                if (i >= nbig) break;
+                const uint32_t e = s_big[i], prim = e & ~kBigWide;
+                TriRecord r;
+                if (!(e & kBigWide)) {
+                    r = load_uniform_record(P.records_big + prim);
+                } else {
+                    const int4* rp = reinterpret_cast<const int4*>(P.records + prim);
+                    r = decode_compact(P, rp[0], rp[1], true);
+                }
+                raster_prim<MODE, INITD>(P, r, entry_seq<PROG>(P, prim), x0, y0, lane, s_key, s_initd);
+            }
+            __syncthreads();
         }
         if (spill) {
-            const uint32_t n_rec = P.tile_offsets[P.ntiles + 1];  // setup records of the draw
-            for (uint32_t cb = wave * 64u; cb < n_rec; cb += NT) {
+            const uint32_t n_all = P.tile_offsets[P.ntiles + 1];  // setup records of the draw
+            const uint32_t r0 = (uint32_t)(((uint64_t)n_all * ks) / max(K, 1u));
+            const uint32_t n_rec = (uint32_t)(((uint64_t)n_all * (ks + 1u)) / max(K, 1u));
+            for (uint32_t cb = r0 + wave * 64u; cb < n_rec; cb += NT) {
                 const uint32_t j = cb + (uint32_t)lane;
                 bool hit = false;
                 int4 q0 = make_int4(0, 0, 0, 0), q1 = q0;
@@ -1506,13 +1585,53 @@ __global__ __launch_bounds__(NT, ZR_TILE_WGS * kTileThreads / NT) void k_tile(Dr
     __syncthreads();
     if (stamp) ts[3] = __builtin_amdgcn_s_memrealtime();
 
+    uint32_t any = s_any;  // spill path: a primitive touching the tile, or ~0
+    if (K > 1) {
+        // merge into the tile's global keys: agent-scope atomics (coherent across
+        // XCDs), drained before arriving; pixels no fragment reached are skipped
+        // when every pixel starts from the clear depth
+        unsigned long long* gk = P.tile_keys + (size_t)t * kTilePixels;
+        const unsigned long long ik = init_key<MODE>(P.clear_depth);
+        for (int i = threadIdx.x; i < kTilePixels; i += NT) {
+            const unsigned long long k = s_key[i];
+            if (P.load_depth || k != ik)
+                __hip_atomic_fetch_min(&gk[i], k, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        }
+        if (spill && threadIdx.x == 0 && any != 0xFFFFFFFFu)
+            __hip_atomic_fetch_min(&P.tile_any[t], any, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        __syncthreads();
+        if (threadIdx.x == 0) {
+            const uint32_t prev = __hip_atomic_fetch_add(&P.tile_arrive[t], 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            s_last = prev + 1u == K;
+        }
+        __syncthreads();
+        if (!s_last) return;
+        // the resolver: every part's keys, then the tile's merge state back to
+        // neutral for the next draw (~0 keys, zero arrivals)
+        for (int i = threadIdx.x; i < kTilePixels; i += NT) {
+            const unsigned long long g = __hip_atomic_load(&gk[i], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            if (g < s_key[i]) s_key[i] = g;
+            __hip_atomic_store(&gk[i], ~0ull, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        }
+        if (threadIdx.x == 0) {
+            __hip_atomic_store(&P.tile_arrive[t], 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            if (spill) {
+                s_any = __hip_atomic_load(&P.tile_any[t], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                __hip_atomic_store(&P.tile_any[t], 0xFFFFFFFFu, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            }
+        }
+        __syncthreads();
+        any = s_any;
+    }
+
     // Resolve: four pixels per thread in two batches of two (the index width is a
     // template parameter so the batch's gathers are issued back to back).
-    uint32_t fallback = cnt ? (P.bins[begin] & kBinPrimMask) : 0u;  // any binned primitive: loads in bounds
-    uint32_t rcnt = cnt;
+    uint32_t fallback = cnt_all ? (P.bins[begin] & kBinPrimMask) : 0u;  // any binned primitive: loads in bounds
+    uint32_t rcnt = cnt_all;
     if (spill) {
-        rcnt = s_any != 0xFFFFFFFFu ? 1u : 0u;
-        fallback = rcnt ? s_any : 0u;
+        rcnt = any != 0xFFFFFFFFu ? 1u : 0u;
+        fallback = rcnt ? any : 0u;
     }
     if (P.index_size == 4)
         resolve_pixels<PROG, MODE, true, NT>(P, x0, y0, rcnt, fallback, s_key, s_srgb);
@@ -1524,7 +1643,7 @@ __global__ __launch_bounds__(NT, ZR_TILE_WGS * kTileThreads / NT) void k_tile(Dr
         asm volatile("s_getreg_b32 %0, hwreg(HW_REG_HW_ID)" : "=s"(hw));
         asm volatile("s_getreg_b32 %0, hwreg(HW_REG_XCC_ID)" : "=s"(xcc));
         ts[5] = ((unsigned long long)xcc << 32) | hw;
-        ts[6] = cnt;
+        ts[6] = cnt_all;
     }
 }
 
@@ -1587,12 +1706,17 @@ void launch_setup_bin(const DrawParams& p, void* stream) {
     }
 }
 
+// k_tile's grid: one workgroup per tile, or K per tile in groups of 8 tiles
+static inline uint32_t tile_grid(const DrawParams& p) {
+    return p.tile_split <= 1 ? p.ntiles : blocks_for(p.ntiles, 8u) * 8u * p.tile_split;
+}
+
 template <int PROG, int MODE, int NT>
 static void launch_tile_pmt(const DrawParams& p, hipStream_t s, bool initd) {
     if (initd)
-        hipLaunchKernelGGL((k_tile<PROG, MODE, true, NT>), dim3(p.ntiles), dim3(NT), 0, s, p);
+        hipLaunchKernelGGL((k_tile<PROG, MODE, true, NT>), dim3(tile_grid(p)), dim3(NT), 0, s, p);
     else
-        hipLaunchKernelGGL((k_tile<PROG, MODE, false, NT>), dim3(p.ntiles), dim3(NT), 0, s, p);
+        hipLaunchKernelGGL((k_tile<PROG, MODE, false, NT>), dim3(tile_grid(p)), dim3(NT), 0, s, p);
 }
 
 template <int PROG, int MODE>

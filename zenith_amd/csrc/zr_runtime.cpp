@@ -185,12 +185,18 @@ struct ScratchSet {
     uint64_t records_cap = 0;  // primitives
     TriRecord* records_big = nullptr;
     uint64_t records_big_cap = 0;
+    float4* mesh_edges = nullptr;
+    uint64_t mesh_edges_cap = 0;
     BBox* bboxes = nullptr;
     uint64_t bboxes_cap = 0;
     uint32_t* tile_counts = nullptr;
     uint64_t tiles_cap = 0;
     uint32_t* tile_offsets = nullptr;
     uint64_t tiles_cap2 = 0;
+    unsigned long long* tile_keys = nullptr;  // split tiles (DrawParams::tile_split)
+    uint32_t* tile_arrive = nullptr;
+    uint32_t* tile_any = nullptr;
+    uint64_t split_tiles_cap = 0;
     uint32_t* counters = nullptr;
     uint64_t counters_cap = 0;
     uint32_t* bins = nullptr;
@@ -243,6 +249,7 @@ struct zr_device_t {
     uint32_t setup_sched = 1;  // k_setup_bin unit schedule (ZR_SETUP_SCHED: 0 contiguous, 1 interleaved)
     uint32_t setup_batch = 2;  // k_setup_bin primitives per lane in flight (ZR_SETUP_BATCH: 1, 2, 4)
     uint32_t tile_threads = 0; // k_tile workgroup size override (ZR_TILE_NT: 256, 512; 0 = by tile count)
+    int tile_split = -1;       // k_tile workgroups per tile (ZR_TILE_SPLIT: 1, 2, 4, 8; -1 = tile_split_for)
     uint32_t debug = 0;
     uint64_t initial_bins = 0;  // 0 = max(2^20, 2 * primitives of the first draw)
     uint64_t min_bins = 0;      // bin capacity an overflow asked for
@@ -543,12 +550,27 @@ zr_result ensure_scratch(zr_device* d, ScratchSet& S, DrawParams& P) {
     if ((rc = grow(d, S.records, S.records_cap, prims, sizeof(TriCompact)))) return rc;
     if ((rc = grow(d, S.records_big, S.records_big_cap, prims, sizeof(TriRecord)))) return rc;
     if ((rc = grow(d, S.bboxes, S.bboxes_cap, prims, sizeof(BBox)))) return rc;
+    if (P.program == kProgMesh && (rc = grow(d, S.mesh_edges, S.mesh_edges_cap, std::max<uint64_t>(P.prims, 1) * 3u,
+                                             sizeof(float4))))
+        return rc;
     {  // per-tile counters start at zero; k_setup_bin leaves them zero after every draw
         const uint64_t cap = S.tiles_cap;
         if ((rc = grow(d, S.tile_counts, S.tiles_cap, P.ntiles + 1, 4))) return rc;
         if (S.tiles_cap != cap) ZR_HIP(hipMemset(S.tile_counts, 0, S.tiles_cap * 4));
     }
     if ((rc = grow(d, S.tile_offsets, S.tiles_cap2, P.ntiles + 2, 4))) return rc;
+    if (P.tile_split > 1 && (S.split_tiles_cap < P.ntiles || !S.tile_keys)) {
+        // merge state of split tiles: neutral (~0 keys, 0 arrivals, ~0 any) between
+        // draws; k_tile's resolvers put it back after every draw
+        uint64_t cap = 0, cap2 = 0, cap3 = 0;
+        if ((rc = grow(d, S.tile_keys, cap, (uint64_t)P.ntiles * kTilePixels, 8))) return rc;
+        if ((rc = grow(d, S.tile_arrive, cap2, P.ntiles, 4))) return rc;
+        if ((rc = grow(d, S.tile_any, cap3, P.ntiles, 4))) return rc;
+        ZR_HIP(hipMemset(S.tile_keys, 0xFF, cap * 8));
+        ZR_HIP(hipMemset(S.tile_arrive, 0, cap2 * 4));
+        ZR_HIP(hipMemset(S.tile_any, 0xFF, cap3 * 4));
+        S.split_tiles_cap = cap / kTilePixels;
+    }
     if (!S.counters) {  // zeroed once; k_setup_bin leaves them zero after every draw
         if ((rc = grow(d, S.counters, S.counters_cap, kCtWords, 4))) return rc;
         ZR_HIP(hipMemset(S.counters, 0, S.counters_cap * 4));
@@ -563,9 +585,13 @@ zr_result ensure_scratch(zr_device* d, ScratchSet& S, DrawParams& P) {
     }
     P.records = S.records;
     P.records_big = S.records_big;
+    P.mesh_edges = S.mesh_edges;
     P.bboxes = S.bboxes;
     P.tile_counts = S.tile_counts;
     P.tile_offsets = S.tile_offsets;
+    P.tile_keys = S.tile_keys;
+    P.tile_arrive = S.tile_arrive;
+    P.tile_any = S.tile_any;
     P.counters = S.counters;
     P.bins = S.bins;
     P.bin_capacity = (uint32_t)std::min<uint64_t>(S.bins_cap, 0xFFFFFFFFull);
@@ -729,6 +755,13 @@ zr_result exec_draw(zr_device* d, ExecState& s, const Cmd& c, bool indexed) {
                        !partitioned && !d->use_graphs && !d->debug && P.setup_batch == 2;
     if (split) P.bbox_lds = 0;
     P.tile_threads = d->tile_threads ? d->tile_threads : tile_threads_for(P.ntiles, (uint32_t)std::max(d->cu_count, 1));
+#if ZR_TILE_SPLIT_BUILD
+    P.tile_split = d->tile_split >= 0 ? (uint32_t)d->tile_split
+                                      : tile_split_for(P.ntiles, (uint32_t)std::max(d->cu_count, 1), P.tile_threads);
+    if (P.tile_split < 1) P.tile_split = 1;
+#else
+    P.tile_split = 1;  // k_tile built without split tiles (zr_kernels.hip ZR_TILE_SPLIT_BUILD)
+#endif
     P.debug = d->debug;
     if (d->debug & kDebugStamps) {
         if (!d->dbg_ts) ZR_HIP(hipMalloc((void**)&d->dbg_ts, (8192 + kMaxTilesPerPass) * 8 * sizeof(unsigned long long)));
@@ -916,6 +949,10 @@ ZR_API zr_result zr_device_create(int32_t hip_device, zr_device** out) {
         const unsigned long v = strtoul(nt, nullptr, 0);
         d->tile_threads = v >= 512 ? 512u : v ? 256u : 0u;
     }
+    if (const char* o = getenv("ZR_TILE_SPLIT")) {
+        const unsigned long v = strtoul(o, nullptr, 0);
+        d->tile_split = v >= 8 ? 8 : v >= 4 ? 4 : v >= 2 ? 2 : 1;
+    }
     if (const char* b = getenv("ZR_SETUP_BATCH")) {
         const unsigned long v = strtoul(b, nullptr, 0);
         d->setup_batch = v >= 4 ? 4u : (v >= 2 ? 2u : 1u);
@@ -953,8 +990,8 @@ ZR_API void zr_device_destroy(zr_device* d) {
     for (hipEvent_t e : d->event_pool) (void)hipEventDestroy(e);
     if (d->dbg_ts) (void)hipFree(d->dbg_ts);
     for (ScratchSet& S : d->sets) {
-        for (void* p : {(void*)S.records, (void*)S.records_big, (void*)S.bboxes, (void*)S.tile_counts,
-                        (void*)S.tile_offsets, (void*)S.counters, (void*)S.bins, (void*)S.xsend, (void*)S.xrecv,
+        for (void* p : {(void*)S.records, (void*)S.records_big, (void*)S.mesh_edges, (void*)S.bboxes, (void*)S.tile_counts,
+                        (void*)S.tile_offsets, (void*)S.tile_keys, (void*)S.tile_arrive, (void*)S.tile_any, (void*)S.counters, (void*)S.bins, (void*)S.xsend, (void*)S.xrecv,
                         (void*)S.gids, (void*)S.rmasks, (void*)S.rcounts, (void*)S.wg_offsets})
             if (p) (void)hipFree(p);
         if (S.setup_done) (void)hipEventDestroy(S.setup_done);
