@@ -1,6 +1,6 @@
 set -o pipefail
-O=gpurun_out/ab8; mkdir -p $O
-for r in 1 2 3; do for v in 0 1; do ZR_SETUP_SPLIT=$v timeout -k 10 120 python bench.py --no-cpu-baseline > $O/c2_s${v}_$r.json 2>>$O/err || exit 2; done; done
-for r in 1 2; do for v in 0 1; do ZR_SETUP_SPLIT=$v timeout -k 10 120 python bench.py --config c3 --no-cpu-baseline > $O/c3_s${v}_$r.json 2>>$O/err || exit 3; done; done
-timeout -k 10 120 python bench.py --emulate-shard 4 --no-cpu-baseline > $O/g4_auto.json 2>>$O/err || exit 4
+O=gpurun_out/rot1; mkdir -p $O
+timeout -k 10 600 python -u -m pytest tests -m gpu -x -q --timeout 120 --timeout-method thread > $O/pytest.log 2>&1 || exit 1
+for r in 1 2; do for c in c2 cerberus c1; do timeout -k 10 120 python bench.py --config $c --no-cpu-baseline > $O/${c}_$r.json 2>>$O/err || exit 3; done; done
+ZR_TILE_NT=512 timeout -k 10 120 python bench.py --config cerberus --no-cpu-baseline > $O/cerb512.json 2>>$O/err || exit 3
 echo done

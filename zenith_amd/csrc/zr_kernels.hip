@@ -1092,6 +1092,16 @@ __device__ __forceinline__ TriRecord load_uniform_record(const TriRecord* p) {
 
 __device__ __forceinline__ bool compact_is_large(const int4 q0) { return (int16_t)(q0.z & 0xFFFF) == kCompactLarge; }
 
+// Row sweeps raster_prim makes over a record's bbox ∩ tile (kDebugStamps).
+__device__ __forceinline__ uint32_t prim_sweeps(const TriRecord& r, int x0, int y0) {
+    const int bw = min((int)(r.bb1 & 0xFFFFu), x0 + kTile - 1) - max((int)(r.bb0 & 0xFFFFu), x0) + 1;
+    const int bh = min((int)(r.bb1 >> 16), y0 + kTile - 1) - max((int)(r.bb0 >> 16), y0) + 1;
+    if (bw <= 0 || bh <= 0) return 0u;
+    const int sh = bw <= 1 ? 0 : 32 - __clz(bw - 1);
+    const int rows = 64 >> sh;
+    return (uint32_t)((bh + rows - 1) / rows);
+}
+
 template <int MODE, bool INITD>
 __device__ __forceinline__ void raster_prim(const DrawParams& P, const TriRecord& r, uint32_t seq, int x0, int y0,
                                             int lane, unsigned long long* s_key, const float* s_initd) {
@@ -1345,6 +1355,7 @@ __global__ __launch_bounds__(NT, ZR_TILE_WGS * kTileThreads / NT) void k_tile(Dr
     // wave owning their chunk would otherwise sweep them all alone
     __shared__ uint32_t s_big[kBigQueue];
     __shared__ uint32_t s_nbig, s_bclaim;
+    __shared__ uint32_t s_dbg[2];  // kDebugStamps: lane-walk steps of the chunks, wave-path sweeps
     __shared__ uint32_t s_last;  // split tiles: this workgroup arrived last and resolves
     // Split tiles (P.tile_split = K > 1, passes with few tiles per CU): K workgroups
     // share a tile, each rasterizing a K-th of its list into LDS keys of its own;
@@ -1401,6 +1412,7 @@ __global__ __launch_bounds__(NT, ZR_TILE_WGS * kTileThreads / NT) void k_tile(Dr
     }
     if (threadIdx.x < 255) s_srgb[threadIdx.x] = c_srgbT[threadIdx.x];
     if (threadIdx.x == 0) s_any = 0xFFFFFFFFu;
+    if (threadIdx.x < 2) s_dbg[threadIdx.x] = 0u;
     // k_setup_bin's counters back to zero for the next draw on this scratch set
     // (the tile lists live in tile_offsets / bins): each tile its own count,
     // tile 0 the grid counters, after reporting the draw's primitive stats
@@ -1499,6 +1511,18 @@ __global__ __launch_bounds__(NT, ZR_TILE_WGS * kTileThreads / NT) void k_tile(Dr
                     const TriRecord r = decode_compact(P, q0, q1, true);
                     raster_lane<MODE, INITD>(P, r, entry_seq<PROG>(P, my_prim), x0, y0, s_key, s_initd, sub, (int)ksh);
                 }
+                if (P.debug & kDebugStamps) {  // work of the chunk: its longest lane walk
+                    int steps = 0;
+                    if (valid && !large && !wide) {
+                        const TriRecord r = decode_compact(P, q0, q1, true);
+                        const int bw = min((int)(r.bb1 & 0xFFFFu), x0 + kTile - 1) - max((int)(r.bb0 & 0xFFFFu), x0) + 1;
+                        const int bh = min((int)(r.bb1 >> 16), y0 + kTile - 1) - max((int)(r.bb0 >> 16), y0) + 1;
+                        steps = (bw > 0 && bh > sub) ? bw * ((bh - sub + (1 << ksh) - 1) >> ksh) : 0;
+                    }
+#pragma unroll
+                    for (int o = 1; o < 64; o <<= 1) steps = max(steps, __shfl_xor(steps, o, 64));
+                    if (lane == 0) atomicAdd(&s_dbg[0], (uint32_t)steps);
+                }
                 // large and wide primitives: queued for the segment's wave pass; the
                 // whole wave sweeps them itself only when the queue is full
                 const bool is_big = valid && (large || wide) && sub == 0;
@@ -1527,6 +1551,7 @@ __global__ __launch_bounds__(NT, ZR_TILE_WGS * kTileThreads / NT) void k_tile(Dr
                         r = decode_compact(P, a, b, true);
                     }
                     raster_prim<MODE, INITD>(P, r, entry_seq<PROG>(P, prim), x0, y0, lane, s_key, s_initd);
+                    if ((P.debug & kDebugStamps) && lane == 0) atomicAdd(&s_dbg[1], prim_sweeps(r, x0, y0));
                 }
             }
             __syncthreads();
@@ -1545,6 +1570,7 @@ __global__ __launch_bounds__(NT, ZR_TILE_WGS * kTileThreads / NT) void k_tile(Dr
                     r = decode_compact(P, rp[0], rp[1], true);
                 }
                 raster_prim<MODE, INITD>(P, r, entry_seq<PROG>(P, prim), x0, y0, lane, s_key, s_initd);
+                if ((P.debug & kDebugStamps) && lane == 0) atomicAdd(&s_dbg[1], prim_sweeps(r, x0, y0));
             }
             __syncthreads();
         }
@@ -1644,6 +1670,7 @@ __global__ __launch_bounds__(NT, ZR_TILE_WGS * kTileThreads / NT) void k_tile(Dr
         asm volatile("s_getreg_b32 %0, hwreg(HW_REG_XCC_ID)" : "=s"(xcc));
         ts[5] = ((unsigned long long)xcc << 32) | hw;
         ts[6] = cnt_all;
+        ts[7] = ((unsigned long long)s_dbg[1] << 32) | s_dbg[0];
     }
 }
 

@@ -406,11 +406,12 @@ void dump_stamps(zr_device* d) {
             if (g) {
                 unsigned long long t1 = ~0ull;
                 for (uint32_t w = 0; w < d->dbg_tiles; ++w) t1 = std::min(t1, tt[w * 8]);
-                fprintf(g, "tile,t0,t1,t2,t3,t4,hwid,xcc,count\n");
+                fprintf(g, "tile,t0,t1,t2,t3,t4,hwid,xcc,count,lane_steps,wave_sweeps\n");
                 for (uint32_t w = 0; w < d->dbg_tiles; ++w) {
                     fprintf(g, "%u", w);
                     for (int i = 0; i <= 4; ++i) fprintf(g, ",%.2f", (double)(tt[w * 8 + i] - t1) * 0.01);
-                    fprintf(g, ",%llu,%llu,%llu\n", tt[w * 8 + 5] & 0xFFFFFFFFull, tt[w * 8 + 5] >> 32, tt[w * 8 + 6]);
+                    fprintf(g, ",%llu,%llu,%llu,%llu,%llu\n", tt[w * 8 + 5] & 0xFFFFFFFFull, tt[w * 8 + 5] >> 32, tt[w * 8 + 6],
+                            tt[w * 8 + 7] & 0xFFFFFFFFull, tt[w * 8 + 7] >> 32);
                 }
                 fclose(g);
             }
