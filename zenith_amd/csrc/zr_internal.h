@@ -106,7 +106,7 @@ constexpr uint32_t kMaxShards = 32;  // destination masks are u32
 // Timing-experiment switches (ZR_DEBUG env var); never set in production runs.
 enum : uint32_t { kDebugSkipRaster = 1u, kDebugSkipShade = 2u, kDebugLoadOnly = 16u,
                   kDebugPhase1Only = 32u, kDebugStopAfterScan = 64u, kDebugStamps = 128u,
-                  kDebugReverseTiles = 256u };
+                  kDebugReverseTiles = 256u, kDebugSkipLanePath = 512u, kDebugSkipWavePath = 1024u };
 
 // Status words in host-mapped pinned memory (read by the runtime at sync points).
 enum StatusWord : uint32_t {

@@ -1507,7 +1507,7 @@ __global__ __launch_bounds__(NT, ZR_TILE_WGS * kTileThreads / NT) void k_tile(Dr
                 // wide: bbox ∩ tile of 253+ pixels (the last sort bucket, which lumps
                 // 253..1024); one lane would walk them for up to 1024 steps
                 const bool wide = ZR_TILE_WIDE && j >= s_bucket[kSortBuckets - 1];
-                if (valid && !large && !wide) {
+                if (valid && !large && !wide && !(P.debug & kDebugSkipLanePath)) {
                     const TriRecord r = decode_compact(P, q0, q1, true);
                     raster_lane<MODE, INITD>(P, r, entry_seq<PROG>(P, my_prim), x0, y0, s_key, s_initd, sub, (int)ksh);
                 }
@@ -1560,7 +1560,7 @@ __global__ __launch_bounds__(NT, ZR_TILE_WGS * kTileThreads / NT) void k_tile(Dr
                 uint32_t i = 0;
                 if (lane == 0) i = atomicAdd(&s_bclaim, 1u);
                 i = (uint32_t)__builtin_amdgcn_readfirstlane((int)i);
-                if (i >= nbig) break;
+                if (i >= nbig || (P.debug & kDebugSkipWavePath)) break;
                 const uint32_t e = s_big[i], prim = e & ~kBigWide;
                 TriRecord r;
                 if (!(e & kBigWide)) {
