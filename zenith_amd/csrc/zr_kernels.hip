@@ -27,6 +27,11 @@
 namespace zr {
 
 // Build-time tuning knobs of k_tile (A/B builds: tools/build_variant.sh).
+#ifndef ZR_TILE_WORK_STATS
+// Per-tile lane-walk steps and wave-path sweeps in the debug stamps (build knob:
+// the counting code costs k_tile 5 VGPRs, one wave per SIMD at 512 threads).
+#define ZR_TILE_WORK_STATS 0
+#endif
 #ifndef ZR_TILE_WGS
 #define ZR_TILE_WGS 8        // k_tile workgroups per CU the register budget is sized for
 #endif
@@ -1511,7 +1516,7 @@ __global__ __launch_bounds__(NT, ZR_TILE_WGS * kTileThreads / NT) void k_tile(Dr
                     const TriRecord r = decode_compact(P, q0, q1, true);
                     raster_lane<MODE, INITD>(P, r, entry_seq<PROG>(P, my_prim), x0, y0, s_key, s_initd, sub, (int)ksh);
                 }
-                if (P.debug & kDebugStamps) {  // work of the chunk: its longest lane walk
+                if (ZR_TILE_WORK_STATS && (P.debug & kDebugStamps)) {  // work of the chunk: its longest lane walk
                     int steps = 0;
                     if (valid && !large && !wide) {
                         const TriRecord r = decode_compact(P, q0, q1, true);
@@ -1551,7 +1556,7 @@ __global__ __launch_bounds__(NT, ZR_TILE_WGS * kTileThreads / NT) void k_tile(Dr
                         r = decode_compact(P, a, b, true);
                     }
                     raster_prim<MODE, INITD>(P, r, entry_seq<PROG>(P, prim), x0, y0, lane, s_key, s_initd);
-                    if ((P.debug & kDebugStamps) && lane == 0) atomicAdd(&s_dbg[1], prim_sweeps(r, x0, y0));
+                    if (ZR_TILE_WORK_STATS && (P.debug & kDebugStamps) && lane == 0) atomicAdd(&s_dbg[1], prim_sweeps(r, x0, y0));
                 }
             }
             __syncthreads();
@@ -1570,7 +1575,7 @@ __global__ __launch_bounds__(NT, ZR_TILE_WGS * kTileThreads / NT) void k_tile(Dr
                     r = decode_compact(P, rp[0], rp[1], true);
                 }
                 raster_prim<MODE, INITD>(P, r, entry_seq<PROG>(P, prim), x0, y0, lane, s_key, s_initd);
-                if ((P.debug & kDebugStamps) && lane == 0) atomicAdd(&s_dbg[1], prim_sweeps(r, x0, y0));
+                if (ZR_TILE_WORK_STATS && (P.debug & kDebugStamps) && lane == 0) atomicAdd(&s_dbg[1], prim_sweeps(r, x0, y0));
             }
             __syncthreads();
         }
