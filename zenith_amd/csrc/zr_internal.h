@@ -222,9 +222,12 @@ struct DrawParams {
 // than 4 (61 / 43 us), so it is not built.
 // k_setup_bin LDS words besides the two tile arrays: misc (32) + list prefix (64).
 constexpr uint32_t kSetupMiscWords = 96;
-inline uint32_t tile_threads_for(uint32_t ntiles, uint32_t cus) {
+// A draw of fewer than 32 primitives per tile (cerberus at 1080p: 16) also gets 8
+// waves: its few heavy tiles (large triangles) end the pass alone on their CUs
+// (cerberus tile pass 124 -> 113 us; C1, 49 per tile, is 14% slower at 8 waves).
+inline uint32_t tile_threads_for(uint32_t ntiles, uint32_t cus, uint64_t prims) {
     const uint32_t per_cu = ntiles / (cus ? cus : 1u);
-    return per_cu >= 6u ? (uint32_t)kTileThreads : 512u;
+    return (per_cu >= 6u && prims >= 32ull * ntiles) ? (uint32_t)kTileThreads : 512u;
 }
 
 #ifndef ZR_TILE_SPLIT_BUILD

@@ -755,7 +755,7 @@ zr_result exec_draw(zr_device* d, ExecState& s, const Cmd& c, bool indexed) {
     const bool split = (d->setup_split > 0 || (d->setup_split < 0 && (prims <= (1u << 18) || P.shard_count > 1))) && !mesh &&
                        !partitioned && !d->use_graphs && !d->debug && P.setup_batch == 2;
     if (split) P.bbox_lds = 0;
-    P.tile_threads = d->tile_threads ? d->tile_threads : tile_threads_for(P.ntiles, (uint32_t)std::max(d->cu_count, 1));
+    P.tile_threads = d->tile_threads ? d->tile_threads : tile_threads_for(P.ntiles, (uint32_t)std::max(d->cu_count, 1), prims);
 #if ZR_TILE_SPLIT_BUILD
     P.tile_split = d->tile_split >= 0 ? (uint32_t)d->tile_split
                                       : tile_split_for(P.ntiles, (uint32_t)std::max(d->cu_count, 1), P.tile_threads);
