@@ -458,6 +458,38 @@ __device__ __forceinline__ bool mesh_geometry(const DrawParams& P, const PrimIn&
     return m.valid != 0;
 }
 
+// mesh_geometry for a primitive that needs no clipping (all vertices inside
+// 0 <= z <= w): one fan, the same operations on fixed indices, so everything
+// stays in registers (the general path's polygon arrays live in scratch).
+__device__ __forceinline__ bool mesh_geometry_unclipped(const DrawParams& P, const PrimIn& in, const float c[3][4],
+                                                        PrimGeom& g, int& ndropped) {
+    int32_t X[3], Y[3];
+    float Z[3];
+#pragma unroll
+    for (int k = 0; k < 3; ++k) {
+        const float x = c[k][0], y = c[k][1], z = c[k][2], w = c[k][3];
+        if (!(w > 0.0f)) { ++ndropped; return false; }
+        const float xd = x / w, yd = y / w, zd = z / w;
+        const float xf = fmaf(xd, P.hw, P.cx), yf = fmaf(yd, P.hh, P.cy);
+        if (!(fabsf(xf) < 4194304.0f && fabsf(yf) < 4194304.0f)) { ++ndropped; return false; }
+        X[k] = (int32_t)rintf(xf * 256.0f);
+        Y[k] = (int32_t)rintf(yf * 256.0f);
+        Z[k] = fmaf(zd, P.dr, P.dmin) + 0.0f;  // -0 -> +0
+    }
+    const long long A2 = (long long)(X[1] - X[0]) * (Y[2] - Y[0]) - (long long)(X[2] - X[0]) * (Y[1] - Y[0]);
+    const bool ccw = A2 < 0;
+    const bool front = (P.front_face == 0) ? ccw : !ccw;
+    if (A2 == 0 || ((P.cull_mode & 1u) && front) || ((P.cull_mode & 2u) && !front)) return false;
+#pragma unroll
+    for (int k = 0; k < 3; ++k) {
+        g.X[k] = X[k];
+        g.Y[k] = Y[k];
+        g.z[k] = Z[k];
+        g.rv[k] = in.vid[k];
+    }
+    return orient_and_bound(P, g, A2);
+}
+
 // Counts the owned (tile, primitive) pairs of a set-up triangle in the LDS
 // histogram; returns how many there are.
 __device__ __forceinline__ uint32_t count_owned(const DrawParams& P, const PrimGeom& g, uint32_t* s_hist) {
@@ -545,24 +577,48 @@ __device__ __forceinline__ void setup_finish_mesh(const DrawParams& P, uint32_t 
     BBox box[kMeshFans];
 #pragma unroll
     for (uint32_t k = 0; k < kMeshFans; ++k) box[k] = BBox{kEmptyBox, 0u};
-    MeshFans m;
-    if (mesh_geometry(P, in, m, ndropped)) {
-        ++nvalid;
-        bool owned = false;
-        for (uint32_t k = 0; k < kMeshFans; ++k) {
-            if (!((m.valid >> k) & 1u)) continue;
-            if (count_owned(P, m.f[k], s_hist)) {
-                box[k] = write_record(P, mesh_record(P, prim, k), m.f[k]);
-                owned = true;
+    bool fast = in.ok;
+    float c[3][4];
+    if (fast) {
+#pragma unroll
+        for (int k = 0; k < 3; ++k) mesh_transform(P.view_proj, in.p[k], c[k]);
+#pragma unroll
+        for (int k = 0; k < 3; ++k) fast = fast && c[k][2] >= 0.0f && c[k][3] - c[k][2] >= 0.0f;
+    }
+    if (fast) {
+        PrimGeom g;
+        if (mesh_geometry_unclipped(P, in, c, g, ndropped)) {
+            ++nvalid;
+            if (count_owned(P, g, s_hist)) {
+                box[0] = write_record(P, prim, g);
+                float e[9];
+                mesh_edge_planes(P, in.p, e);
+                float4* q = P.mesh_edges + (size_t)prim * 3u;
+                q[0] = make_float4(e[0], e[1], e[2], e[3]);
+                q[1] = make_float4(e[4], e[5], e[6], e[7]);
+                q[2] = make_float4(e[8], 0.0f, 0.0f, 0.0f);
             }
         }
-        if (owned) {  // the resolve's barycentric planes (shade_mesh)
-            float e[9];
-            mesh_edge_planes(P, in.p, e);
-            float4* q = P.mesh_edges + (size_t)prim * 3u;
-            q[0] = make_float4(e[0], e[1], e[2], e[3]);
-            q[1] = make_float4(e[4], e[5], e[6], e[7]);
-            q[2] = make_float4(e[8], 0.0f, 0.0f, 0.0f);
+    } else {  // clipped (or invalid): the general path
+        MeshFans m;
+        if (mesh_geometry(P, in, m, ndropped)) {
+            ++nvalid;
+            bool owned = false;
+            for (uint32_t k = 0; k < kMeshFans; ++k) {
+                if (!((m.valid >> k) & 1u)) continue;
+                if (count_owned(P, m.f[k], s_hist)) {
+                    box[k] = write_record(P, mesh_record(P, prim, k), m.f[k]);
+                    owned = true;
+                }
+            }
+            if (owned) {  // the resolve's barycentric planes (shade_mesh)
+                float e[9];
+                mesh_edge_planes(P, in.p, e);
+                float4* q = P.mesh_edges + (size_t)prim * 3u;
+                q[0] = make_float4(e[0], e[1], e[2], e[3]);
+                q[1] = make_float4(e[4], e[5], e[6], e[7]);
+                q[2] = make_float4(e[8], 0.0f, 0.0f, 0.0f);
+            }
         }
     }
     *bbox_out = box[0];
