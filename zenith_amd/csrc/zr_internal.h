@@ -256,6 +256,6 @@ void launch_tile(const DrawParams& p, void* stream);
 void launch_clear(const DrawParams& p, void* stream);
 void launch_route(const DrawParams& p, void* stream);
 void launch_setup_split(const DrawParams& p, int pass, void* stream);  // k_setup_bin's halves, 2 launches
-const void* setup_split_kernel(int pass);     // partitioned setup: route own range (2 kernels)
+const void* setup_split_kernel(int pass, bool mesh);     // partitioned setup: route own range (2 kernels)
 
 }  // namespace zr

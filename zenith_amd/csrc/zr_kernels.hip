@@ -1766,7 +1766,10 @@ const void* setup_bin_kernel(uint32_t batch, bool mesh) {
     }
 }
 
-const void* setup_split_kernel(int pass) {
+const void* setup_split_kernel(int pass, bool mesh) {
+    if (mesh)
+        return pass == 1 ? reinterpret_cast<const void*>(&k_setup_bin<1, true, 1>)
+                         : reinterpret_cast<const void*>(&k_setup_bin<1, true, 2>);
     return pass == 1 ? reinterpret_cast<const void*>(&k_setup_bin<2, false, 1>)
                      : reinterpret_cast<const void*>(&k_setup_bin<2, false, 2>);
 }
@@ -1774,6 +1777,13 @@ const void* setup_split_kernel(int pass) {
 void launch_setup_split(const DrawParams& p, int pass, void* stream) {
     const size_t lds = setup_bin_lds_bytes(p.ntiles, 0);
     const hipStream_t s = (hipStream_t)stream;
+    if (p.program == kProgMesh) {  // batch 1, as the persistent mesh instance
+        if (pass == 1)
+            hipLaunchKernelGGL((k_setup_bin<1, true, 1>), dim3(p.setup_wgs), dim3(kSetupThreads), lds, s, p);
+        else
+            hipLaunchKernelGGL((k_setup_bin<1, true, 2>), dim3(p.setup_wgs), dim3(kSetupThreads), lds, s, p);
+        return;
+    }
     if (pass == 1)
         hipLaunchKernelGGL((k_setup_bin<2, false, 1>), dim3(p.setup_wgs), dim3(kSetupThreads), lds, s, p);
     else

@@ -750,10 +750,10 @@ zr_result exec_draw(zr_device* d, ExecState& s, const Cmd& c, bool indexed) {
         // (mesh: fans 1 and 2 keep their bboxes in global memory, so all of them do)
         P.bbox_lds = (!mesh && entries * sizeof(BBox) <= budget) ? (uint32_t)entries : 0u;
     }
-    // split setup: default batch, not mesh / list mode; bboxes and per-workgroup
+    // split setup: default batch or the mesh instance, not list mode; bboxes and per-workgroup
     // offsets cross the launch boundary through global memory
-    const bool split = (d->setup_split > 0 || (d->setup_split < 0 && (prims <= (1u << 18) || P.shard_count > 1))) && !mesh &&
-                       !partitioned && !d->use_graphs && !d->debug && P.setup_batch == 2;
+    const bool split = (d->setup_split > 0 || (d->setup_split < 0 && (prims <= (1u << 18) || P.shard_count > 1))) &&
+                       !partitioned && !d->use_graphs && !d->debug && (mesh || P.setup_batch == 2);
     if (split) P.bbox_lds = 0;
     P.tile_threads = d->tile_threads ? d->tile_threads : tile_threads_for(P.ntiles, (uint32_t)std::max(d->cu_count, 1), prims);
 #if ZR_TILE_SPLIT_BUILD
@@ -968,8 +968,9 @@ ZR_API zr_result zr_device_create(int32_t hip_device, zr_device** out) {
     ZR_HIP(hipFuncSetAttribute(setup_bin_kernel(1, true), hipFuncAttributeMaxDynamicSharedMemorySize,
                                (int)kSetupLdsBudget));
     for (int pass : {1, 2})
-        ZR_HIP(hipFuncSetAttribute(setup_split_kernel(pass), hipFuncAttributeMaxDynamicSharedMemorySize,
-                                   (int)kSetupLdsBudget));
+        for (bool mesh : {false, true})
+            ZR_HIP(hipFuncSetAttribute(setup_split_kernel(pass, mesh), hipFuncAttributeMaxDynamicSharedMemorySize,
+                                       (int)kSetupLdsBudget));
     ZR_HIP(hipDeviceGetAttribute(&d->cu_count, hipDeviceAttributeMultiprocessorCount, hip_device));
     void* st = nullptr;
     ZR_HIP(hipHostMalloc(&st, kStWords * 4, hipHostMallocMapped));
