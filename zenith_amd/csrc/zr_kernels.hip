@@ -1,21 +1,23 @@
-// zr_kernels.hip — the MI355X (gfx950) draw path: setup -> scan -> bin -> tile.
+// zr_kernels.hip — the MI355X (gfx950) draw path.
 //
-// Pass structure:
-//   k_setup  chunks of primitives per workgroup: index + vertex fetch, vertex stage
-//            (triangle.slang:19-25: SV_Position = float4(position, 1)), viewport
-//            transform, 8-bit sub-pixel snap, facing/cull, orientation, top-left
-//            biases, clipped pixel bbox -> 64-B TriRecord; per-workgroup LDS
-//            histogram of tile overlaps -> counts[wg][tile].
-//   k_colsum/k_scan_tiles/k_apply  column scan of counts -> per-(wg, tile)
-//            list offsets, per-tile list starts and lengths.
-//   k_bin    same chunks: scatter primitive ids into per-tile lists through LDS
-//            cursors (no global atomics anywhere in binning).
-//   k_tile   one 256-thread workgroup per 32x32 screen tile: LDS-resident 64-bit
-//            visibility keys (depth | primitive sequence) updated with ds_min_u64
-//            by a wave per primitive (lanes over the primitive's bbox ∩ tile),
-//            then a resolve that shades each pixel's winner once (psmain),
-//            encodes to the attachment format and writes colour + depth with
-//            coalesced row stores.  The attachment CLEAR is fused into the resolve.
+//   k_setup_bin  one persistent launch, one 1024-thread workgroup per CU: vertex
+//                stage, clip (mesh program), viewport, 8-bit sub-pixel snap,
+//                facing/cull, orientation, top-left biases, clipped pixel bbox ->
+//                32-B compact record (64-B full record for large primitives);
+//                LDS histogram of tile overlaps; returning atomics on the tile
+//                counters; an XCD-hierarchical grid barrier; tile scan; scatter of
+//                (tile, primitive | area bucket) pairs into the tile lists.  Also
+//                built as two launches cut at the barrier (split setup).
+//   k_tile       one 256- or 512-thread workgroup per 32x32 tile: LDS-resident
+//                64-bit visibility keys (depth | primitive sequence) updated with
+//                ds_min_u64 -- lane per primitive for small ones (area-sorted
+//                64-lane chunks), wave per primitive for large ones -- then a
+//                resolve that shades each pixel's winner once, encodes to the
+//                attachment format and writes colour + depth with coalesced
+//                stores.  The attachment CLEAR is fused into the resolve.
+//   k_route_*    partitioned multi-GPU setup: route primitives to the ranks
+//                owning the tile rows they touch.
+//   k_clear      a render pass without draws.
 //
 // Coverage/depth arithmetic is exact integer + explicitly ordered float math,
 // bit-identical to the in-order CPU oracle (oracle/zr_oracle.c).
@@ -44,6 +46,9 @@ namespace zr {
 #ifndef ZR_TILE_WIDE
 #define ZR_TILE_WIDE 0       // 1: bbox ∩ tile of 253+ px goes to the wave path instead of one lane
                              // (measured: cerberus tile pass 124 -> 107 us, C3 306 -> 327, C2 77 -> 79)
+#endif
+#ifndef ZR_TILE_BIGK
+#define ZR_TILE_BIGK 4       // lanes per entry at least, for the last sort bucket (253+ px of bbox ∩ tile)
 #endif
 #ifndef ZR_TILE_SUBLANE
 #define ZR_TILE_SUBLANE 1    // sparse segments: k lanes per entry split its bbox rows (0: one lane per entry)
@@ -1403,7 +1408,9 @@ __device__ __forceinline__ void resolve_pixels(const DrawParams& P, int x0, int 
 // has few (tile-row shards, small attachments), so a tile's primitives spread
 // over more waves (P.tile_threads, tile_threads_for).
 template <int PROG, int MODE, bool INITD, int NT>
-__global__ __launch_bounds__(NT, ZR_TILE_WGS * kTileThreads / NT) void k_tile(DrawParams P) {
+// (launch bounds: the second argument is the minimum waves per SIMD -- 8, i.e.
+// 64 VGPRs, for both sizes; 8 x 256 or 4 x 512 threads per CU)
+__global__ __launch_bounds__(NT, ZR_TILE_WGS * kTileThreads / 256) void k_tile(DrawParams P) {
     __shared__ unsigned long long s_key[kTilePixels];
     __shared__ float s_initd[INITD ? kTilePixels : 1];
     __shared__ uint32_t s_sorted[kSortCap];
@@ -1540,9 +1547,16 @@ __global__ __launch_bounds__(NT, ZR_TILE_WGS * kTileThreads / NT) void k_tile(Dr
             // takes one statically (measured faster there: C1 78 vs 85 us, C3 299
             // vs 304 us; LPT: C2 80 vs 82 us).
             const uint32_t kl = ZR_TILE_SUBLANE ? min(8u, max(1u, (uint32_t)NT / max(n, 1u))) : 1u;
-            const uint32_t ksh = 31u - __clz(kl);  // lanes per entry: 1, 2, 4 or 8
-            const uint32_t per = 64u >> ksh;       // entries per chunk
-            const uint32_t nch = (n + per - 1u) / per;
+            const uint32_t ksh_s = 31u - __clz(kl);  // lanes per entry: 1, 2, 4 or 8
+            // entries of the last bucket (bbox ∩ tile of 253+ pixels) get at least
+            // ZR_TILE_BIGK lanes: one lane would walk up to 1024 steps and hold
+            // its whole chunk (and the tile) for that long.  Chunks are 64 lanes of
+            // this lane space: the first off63 entries kl lanes each, then the rest.
+            const uint32_t ksh_b = max(ksh_s, (uint32_t)(31 - __clz(ZR_TILE_BIGK)));
+            const uint32_t off63 = s_bucket[kSortBuckets - 1];
+            const uint32_t lsp_s = off63 << ksh_s;                    // lane space of the other buckets
+            const uint32_t lanes_all = lsp_s + ((n - off63) << ksh_b);
+            const uint32_t nch = (lanes_all + 63u) / 64u;
             const bool lpt = ZR_TILE_LPT && nch > NT / 64u;
             for (uint32_t it = 0;; ++it) {
                 uint32_t claim = wave + it * (NT / 64u);  // static: wave w takes chunks w, w + waves, ...
@@ -1551,9 +1565,11 @@ __global__ __launch_bounds__(NT, ZR_TILE_WGS * kTileThreads / NT) void k_tile(Dr
                     claim = (uint32_t)__builtin_amdgcn_readfirstlane((int)claim);
                 }
                 if (claim >= nch) break;
-                const uint32_t cb = (lpt ? nch - 1u - claim : claim) * per;
-                const uint32_t j = cb + ((uint32_t)lane >> ksh);
-                const int sub = lane & ((1 << ksh) - 1);
+                const uint32_t g = (lpt ? nch - 1u - claim : claim) * 64u + (uint32_t)lane;  // lane-space slot
+                const bool gb = g >= lsp_s;
+                const uint32_t ksh = gb ? ksh_b : ksh_s;
+                const uint32_t j = gb ? off63 + ((g - lsp_s) >> ksh_b) : g >> ksh_s;
+                const int sub = (int)((gb ? g - lsp_s : g) & ((1u << ksh) - 1u));
                 uint32_t my_prim = 0;
                 int4 q0 = make_int4(0, 0, 0, 0), q1 = q0;
                 if (j < n) {
@@ -1567,7 +1583,7 @@ __global__ __launch_bounds__(NT, ZR_TILE_WGS * kTileThreads / NT) void k_tile(Dr
                 const bool large = compact_is_large(q0);
                 // wide: bbox ∩ tile of 253+ pixels (the last sort bucket, which lumps
                 // 253..1024); one lane would walk them for up to 1024 steps
-                const bool wide = ZR_TILE_WIDE && j >= s_bucket[kSortBuckets - 1];
+                const bool wide = ZR_TILE_WIDE && j >= off63;
                 if (valid && !large && !wide && !(P.debug & kDebugSkipLanePath)) {
                     const TriRecord r = decode_compact(P, q0, q1, true);
                     raster_lane<MODE, INITD>(P, r, entry_seq<PROG>(P, my_prim), x0, y0, s_key, s_initd, sub, (int)ksh);
