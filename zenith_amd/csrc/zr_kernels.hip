@@ -1142,9 +1142,7 @@ __device__ __forceinline__ TriRecord decode_compact(const DrawParams& P, const i
 
 // A wave-uniform full record, moved to scalar registers right after the load so
 // the wave path does not hold 16 more VGPRs.
-__device__ __forceinline__ TriRecord load_uniform_record(const TriRecord* p) {
-    const int4* q = reinterpret_cast<const int4*>(p);
-    int4 a = q[0], b = q[1], c = q[2], d = q[3];
+__device__ __forceinline__ TriRecord uniform_record(const int4 a, const int4 b, const int4 c, const int4 d) {
     auto u = [](int v) { return __builtin_amdgcn_readfirstlane(v); };
     TriRecord r;
     r.X0 = u(a.x); r.Y0 = u(a.y); r.X1 = u(a.z); r.Y1 = u(a.w);
@@ -1154,6 +1152,11 @@ __device__ __forceinline__ TriRecord load_uniform_record(const TriRecord* p) {
     r.v0 = (uint32_t)u(c.z); r.v1 = (uint32_t)u(c.w); r.v2 = (uint32_t)u(d.x);
     r.bb0 = (uint32_t)u(d.y); r.bb1 = (uint32_t)u(d.z); r.flags = (uint32_t)u(d.w);
     return r;
+}
+
+__device__ __forceinline__ TriRecord load_uniform_record(const TriRecord* p) {
+    const int4* q = reinterpret_cast<const int4*>(p);
+    return uniform_record(q[0], q[1], q[2], q[3]);
 }
 
 __device__ __forceinline__ bool compact_is_large(const int4 q0) { return (int16_t)(q0.z & 0xFFFF) == kCompactLarge; }
@@ -1633,21 +1636,37 @@ __global__ __launch_bounds__(NT, ZR_TILE_WGS * kTileThreads / 256) void k_tile(D
             }
             __syncthreads();
             const uint32_t nbig = min(s_nbig, kBigQueue);
-            for (;;) {  // the segment's queued wave-path primitives, one per claim
+            for (;;) {  // the segment's queued wave-path primitives, two per claim
                 uint32_t i = 0;
-                if (lane == 0) i = atomicAdd(&s_bclaim, 1u);
+                if (lane == 0) i = atomicAdd(&s_bclaim, 2u);
                 i = (uint32_t)__builtin_amdgcn_readfirstlane((int)i);
                 if (i >= nbig || (P.debug & kDebugSkipWavePath)) break;
-                const uint32_t e = s_big[i], prim = e & ~kBigWide;
-                TriRecord r;
-                if (!(e & kBigWide)) {
-                    r = load_uniform_record(P.records_big + prim);
-                } else {
-                    const int4* rp = reinterpret_cast<const int4*>(P.records + prim);
-                    r = decode_compact(P, rp[0], rp[1], true);
+                const bool two = i + 1u < nbig;
+                const uint32_t e0 = s_big[i], e1 = two ? s_big[i + 1u] : e0;
+                if (!((e0 | e1) & kBigWide)) {
+                    // both full records' loads in flight at once (one exposed latency
+                    // per claim), the second held in scalar registers
+                    const int4* a = reinterpret_cast<const int4*>(P.records_big + e0);
+                    const int4* b = reinterpret_cast<const int4*>(P.records_big + e1);
+                    const int4 a0 = a[0], a1 = a[1], a2 = a[2], a3 = a[3];
+                    const int4 b0 = b[0], b1 = b[1], b2 = b[2], b3 = b[3];
+                    const TriRecord ra = uniform_record(a0, a1, a2, a3);
+                    const TriRecord rb = uniform_record(b0, b1, b2, b3);
+                    raster_prim<MODE, INITD>(P, ra, entry_seq<PROG>(P, e0), x0, y0, lane, s_key, s_initd);
+                    if (two) raster_prim<MODE, INITD>(P, rb, entry_seq<PROG>(P, e1), x0, y0, lane, s_key, s_initd);
+                    continue;
                 }
-                raster_prim<MODE, INITD>(P, r, entry_seq<PROG>(P, prim), x0, y0, lane, s_key, s_initd);
-                if (ZR_TILE_WORK_STATS && (P.debug & kDebugStamps) && lane == 0) atomicAdd(&s_dbg[1], prim_sweeps(r, x0, y0));
+                for (uint32_t q = 0; q < (two ? 2u : 1u); ++q) {  // a wide entry (ZR_TILE_WIDE builds)
+                    const uint32_t e = q ? e1 : e0, prim = e & ~kBigWide;
+                    TriRecord r;
+                    if (!(e & kBigWide)) {
+                        r = load_uniform_record(P.records_big + prim);
+                    } else {
+                        const int4* rp = reinterpret_cast<const int4*>(P.records + prim);
+                        r = decode_compact(P, rp[0], rp[1], true);
+                    }
+                    raster_prim<MODE, INITD>(P, r, entry_seq<PROG>(P, prim), x0, y0, lane, s_key, s_initd);
+                }
             }
             __syncthreads();
         }
