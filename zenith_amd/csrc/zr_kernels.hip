@@ -50,6 +50,12 @@ namespace zr {
 #ifndef ZR_TILE_BIGK
 #define ZR_TILE_BIGK 4       // lanes per entry at least, for the last sort bucket (253+ px of bbox ∩ tile)
 #endif
+#ifndef ZR_TILE_MIDK
+#define ZR_TILE_MIDK 2       // lanes per entry at least, for buckets ZR_TILE_MIDB.. (1: off)
+#endif
+#ifndef ZR_TILE_MIDB
+#define ZR_TILE_MIDB 32      // first bucket of the middle run: bbox ∩ tile of 129+ px
+#endif
 #ifndef ZR_TILE_SUBLANE
 #define ZR_TILE_SUBLANE 1    // sparse segments: k lanes per entry split its bbox rows (0: one lane per entry)
 #endif
@@ -1555,10 +1561,19 @@ __global__ __launch_bounds__(NT, ZR_TILE_WGS * kTileThreads / 256) void k_tile(D
             // ZR_TILE_BIGK lanes: one lane would walk up to 1024 steps and hold
             // its whole chunk (and the tile) for that long.  Chunks are 64 lanes of
             // this lane space: the first off63 entries kl lanes each, then the rest.
+            // Likewise buckets from ZR_TILE_MIDB up (bbox ∩ tile > 4 * MIDB px) get at
+            // least ZR_TILE_MIDK lanes.  Three runs of the sorted segment, each a
+            // fixed number of lanes per entry.
             const uint32_t ksh_b = max(ksh_s, (uint32_t)(31 - __clz(ZR_TILE_BIGK)));
+            // (C3 tile pass 262 -> 219 us, cerberus 68 -> 60 us; C1 / C2 within noise.
+            // Gating it on the middle run's length lost those gains: a few mid-size
+            // entries already make the chunk that ends the tile.)
             const uint32_t off63 = s_bucket[kSortBuckets - 1];
-            const uint32_t lsp_s = off63 << ksh_s;                    // lane space of the other buckets
-            const uint32_t lanes_all = lsp_s + ((n - off63) << ksh_b);
+            const uint32_t offm = s_bucket[ZR_TILE_MIDB];
+            const uint32_t ksh_m = max(ksh_s, (uint32_t)(31 - __clz(ZR_TILE_MIDK)));
+            const uint32_t lsp_s = offm << ksh_s;                      // lane space of buckets < MIDB
+            const uint32_t lsp_m = lsp_s + ((off63 - offm) << ksh_m);  // ... and up to the last bucket
+            const uint32_t lanes_all = lsp_m + ((n - off63) << ksh_b);
             const uint32_t nch = (lanes_all + 63u) / 64u;
             const bool lpt = ZR_TILE_LPT && nch > NT / 64u;
             for (uint32_t it = 0;; ++it) {
@@ -1569,10 +1584,11 @@ __global__ __launch_bounds__(NT, ZR_TILE_WGS * kTileThreads / 256) void k_tile(D
                 }
                 if (claim >= nch) break;
                 const uint32_t g = (lpt ? nch - 1u - claim : claim) * 64u + (uint32_t)lane;  // lane-space slot
-                const bool gb = g >= lsp_s;
-                const uint32_t ksh = gb ? ksh_b : ksh_s;
-                const uint32_t j = gb ? off63 + ((g - lsp_s) >> ksh_b) : g >> ksh_s;
-                const int sub = (int)((gb ? g - lsp_s : g) & ((1u << ksh) - 1u));
+                const bool gb = g >= lsp_m, gm = g >= lsp_s;
+                const uint32_t ksh = gb ? ksh_b : gm ? ksh_m : ksh_s;
+                const uint32_t g0 = gb ? g - lsp_m : gm ? g - lsp_s : g;  // slot within its run
+                const uint32_t j = (gb ? off63 : gm ? offm : 0u) + (g0 >> ksh);
+                const int sub = (int)(g0 & ((1u << ksh) - 1u));
                 uint32_t my_prim = 0;
                 int4 q0 = make_int4(0, 0, 0, 0), q1 = q0;
                 if (j < n) {
