@@ -1,5 +1,7 @@
 set -o pipefail
-O=gpurun_out/ab22; mkdir -p $O
-timeout -k 10 600 python -u -m pytest tests -m gpu -x -q --timeout 120 --timeout-method thread > $O/pytest.log 2>&1 || exit 1
-for c in c2 c3 cerberus c1; do timeout -k 10 120 python bench.py --config $c --no-cpu-baseline > $O/${c}.json 2>>$O/err || exit 3; done
+O=gpurun_out/ab24; mkdir -p $O
+for c in c3 c1 cerberus c2 c4; do
+  timeout -k 10 120 python bench.py --config $c --no-cpu-baseline > $O/${c}_head.json 2>>$O/err || exit 3
+  for v in k48 bk b24k; do env ZR_LIB_PATH=$PWD/zenith_amd/variants/$v/libzenith_raster.so timeout -k 10 120 python bench.py --config $c --no-cpu-baseline > $O/${c}_$v.json 2>>$O/err || exit 3; done
+done
 echo done

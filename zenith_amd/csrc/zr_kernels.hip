@@ -48,13 +48,13 @@ namespace zr {
                              // (measured: cerberus tile pass 124 -> 107 us, C3 306 -> 327, C2 77 -> 79)
 #endif
 #ifndef ZR_TILE_BIGK
-#define ZR_TILE_BIGK 4       // lanes per entry at least, for the last sort bucket (253+ px of bbox ∩ tile)
+#define ZR_TILE_BIGK 8       // lanes per entry at least, for the last sort bucket (253+ px of bbox ∩ tile)
 #endif
 #ifndef ZR_TILE_MIDK
-#define ZR_TILE_MIDK 2       // lanes per entry at least, for buckets ZR_TILE_MIDB.. (1: off)
+#define ZR_TILE_MIDK 4       // lanes per entry at least, for buckets ZR_TILE_MIDB.. (1: off)
 #endif
 #ifndef ZR_TILE_MIDB
-#define ZR_TILE_MIDB 32      // first bucket of the middle run: bbox ∩ tile of 129+ px
+#define ZR_TILE_MIDB 24      // first bucket of the middle run: bbox ∩ tile of 97+ px
 #endif
 #ifndef ZR_TILE_SUBLANE
 #define ZR_TILE_SUBLANE 1    // sparse segments: k lanes per entry split its bbox rows (0: one lane per entry)
@@ -1565,8 +1565,10 @@ __global__ __launch_bounds__(NT, ZR_TILE_WGS * kTileThreads / 256) void k_tile(D
             // least ZR_TILE_MIDK lanes.  Three runs of the sorted segment, each a
             // fixed number of lanes per entry.
             const uint32_t ksh_b = max(ksh_s, (uint32_t)(31 - __clz(ZR_TILE_BIGK)));
-            // (C3 tile pass 262 -> 219 us, cerberus 68 -> 60 us; C1 / C2 within noise.
-            // Gating it on the middle run's length lost those gains: a few mid-size
+            // (2 lanes from 129 px, 4 from 253: C3 tile pass 262 -> 219 us, cerberus 68
+            // -> 60 us, C1 / C2 within noise; 4 lanes from 97 px, 8 from 253: C1 58 ->
+            // 51 us, cerberus 60 -> 57, C3 219 -> 226, C2 equal -- the default.
+            // Gating it on the middle run's length lost the gains: a few mid-size
             // entries already make the chunk that ends the tile.)
             const uint32_t off63 = s_bucket[kSortBuckets - 1];
             const uint32_t offm = s_bucket[ZR_TILE_MIDB];
