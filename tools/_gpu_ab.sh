@@ -1,7 +1,6 @@
 set -o pipefail
-O=gpurun_out/ab24; mkdir -p $O
-for c in c3 c1 cerberus c2 c4; do
-  timeout -k 10 120 python bench.py --config $c --no-cpu-baseline > $O/${c}_head.json 2>>$O/err || exit 3
-  for v in k48 bk b24k; do env ZR_LIB_PATH=$PWD/zenith_amd/variants/$v/libzenith_raster.so timeout -k 10 120 python bench.py --config $c --no-cpu-baseline > $O/${c}_$v.json 2>>$O/err || exit 3; done
-done
+O=gpurun_out/ab25; mkdir -p $O
+for b in 2 4 1; do ZR_SETUP_BATCH=$b timeout -k 10 120 python bench.py --config c4 --no-cpu-baseline > $O/c4_b$b.json 2>>$O/err || exit 3; done
+for b in 2 4; do ZR_SETUP_BATCH=$b timeout -k 10 120 python bench.py --config c2 --no-cpu-baseline > $O/c2_b$b.json 2>>$O/err || exit 3; done
+ZR_DEBUG=128 ZR_DEBUG_TS=$O/st.txt timeout -k 10 200 python bench.py --config c4 --steps 2 --warmup 1 --no-cpu-baseline > $O/d.json 2>> $O/err || exit 2
 echo done
