@@ -1,6 +1,9 @@
 set -o pipefail
-O=gpurun_out/ab25; mkdir -p $O
-for b in 2 4 1; do ZR_SETUP_BATCH=$b timeout -k 10 120 python bench.py --config c4 --no-cpu-baseline > $O/c4_b$b.json 2>>$O/err || exit 3; done
-for b in 2 4; do ZR_SETUP_BATCH=$b timeout -k 10 120 python bench.py --config c2 --no-cpu-baseline > $O/c2_b$b.json 2>>$O/err || exit 3; done
-ZR_DEBUG=128 ZR_DEBUG_TS=$O/st.txt timeout -k 10 200 python bench.py --config c4 --steps 2 --warmup 1 --no-cpu-baseline > $O/d.json 2>> $O/err || exit 2
+O=gpurun_out/ab26; mkdir -p $O
+timeout -k 10 600 python -u -m pytest tests -m gpu -x -q --timeout 120 --timeout-method thread > $O/pytest.log 2>&1 || exit 1
+H=$PWD/zenith_amd/variants/head/libzenith_raster.so
+for r in 1 2; do for c in c2 c1 c3 cerberus; do
+  env ZR_LIB_PATH=$H timeout -k 10 120 python bench.py --config $c --no-cpu-baseline > $O/${c}_head_$r.json 2>>$O/err || exit 3
+  timeout -k 10 120 python bench.py --config $c --no-cpu-baseline > $O/${c}_new_$r.json 2>>$O/err || exit 3
+done; done
 echo done

@@ -23,6 +23,8 @@
 // bit-identical to the in-order CPU oracle (oracle/zr_oracle.c).
 #include <hip/hip_runtime.h>
 
+#include <type_traits>
+
 #include "zr_internal.h"
 #include "zr_shading.h"
 
@@ -58,9 +60,6 @@ namespace zr {
 #endif
 #ifndef ZR_TILE_SUBLANE
 #define ZR_TILE_SUBLANE 1    // sparse segments: k lanes per entry split its bbox rows (0: one lane per entry)
-#endif
-#ifndef ZR_EXP_EXTRA_VALU
-#define ZR_EXP_EXTRA_VALU 0  // experiment only: dummy VALU ops per lane-raster step
 #endif
 
 __constant__ float c_srgbT[255] = ZR_SRGB_THRESHOLDS_INIT;
@@ -1241,29 +1240,34 @@ __device__ __forceinline__ void raster_lane(const DrawParams& P, const TriRecord
     int ex = 0;
     uint32_t la = (uint32_t)(((by0 + sub - y0) * kTile + (bx0 - x0)) * 8);  // byte offset of the key
     const uint32_t lj = (uint32_t)((k * kTile - bw + 1) * 8);
-    for (int k = 0; k < n; ++k) {
-        if ((w0 | w1 | w2) >= 0) {
-            const float fb1 = (float)(w1 + b1) * invA2, fb2 = (float)(w2 + b2) * invA2;
-            const float z = fmaf(fb2, dz2, fmaf(fb1, dz1, z0));
-            if (z >= P.dlo && z <= P.dhi && (!INITD || depth_pass(P.depth_op, z, s_initd[la >> 3])))
-                atomicMin(reinterpret_cast<unsigned long long*>(reinterpret_cast<char*>(s_key) + la),
-                          frag_key<MODE>(z, seq));
+    // The depth-range test (fragments outside [dlo, dhi] are discarded, §3) is
+    // dropped from the loop when every lane's vertex depths lie inside the range
+    // by a margin far above the interpolation's rounding (a few ulp of 1): then
+    // no fragment can fall outside.  NaN depths fail the comparisons, so keep it.
+    const float z1v = z0 + dz1, z2v = z0 + dz2, zlo = P.dlo + 1e-4f, zhi = P.dhi - 1e-4f;
+    const bool zsafe = z0 >= zlo && z0 <= zhi && z1v >= zlo && z1v <= zhi && z2v >= zlo && z2v <= zhi;
+    auto sweep = [&](auto ztest) {
+        for (int q = 0; q < n; ++q) {
+            if ((w0 | w1 | w2) >= 0) {
+                const float fb1 = (float)(w1 + b1) * invA2, fb2 = (float)(w2 + b2) * invA2;
+                const float z = fmaf(fb2, dz2, fmaf(fb1, dz1, z0));
+                if ((!decltype(ztest)::value || (z >= P.dlo && z <= P.dhi)) &&
+                    (!INITD || depth_pass(P.depth_op, z, s_initd[la >> 3])))
+                    atomicMin(reinterpret_cast<unsigned long long*>(reinterpret_cast<char*>(s_key) + la),
+                              frag_key<MODE>(z, seq));
+            }
+            const bool wrap = ++ex == bw;
+            ex = wrap ? 0 : ex;
+            w0 += wrap ? j0 : sx0;
+            w1 += wrap ? j1 : sx1;
+            w2 += wrap ? j2 : sx2;
+            la += wrap ? lj : 8u;
         }
-#if ZR_EXP_EXTRA_VALU
-        {  // experiment: extra dependent VALU work per pixel step (sensitivity probe)
-            float acc = (float)w0;
-#pragma unroll
-            for (int i = 0; i < ZR_EXP_EXTRA_VALU; ++i) acc = fmaf(acc, 1.0001f, 0.5f);
-            if (acc == 1234.5f) s_key[0] = 0;
-        }
-#endif
-        const bool wrap = ++ex == bw;
-        ex = wrap ? 0 : ex;
-        w0 += wrap ? j0 : sx0;
-        w1 += wrap ? j1 : sx1;
-        w2 += wrap ? j2 : sx2;
-        la += wrap ? lj : 8u;
-    }
+    };
+    if (__ballot(!zsafe) == 0ull)
+        sweep(std::false_type{});
+    else
+        sweep(std::true_type{});
 }
 
 // Visibility sequence of setup record e (API order): e + 1, or for the mesh
