@@ -497,3 +497,15 @@ def test_clear_then_draw_load(device):
     assert np.array_equal(tex.read(), ref)  # the pass's CLEAR equals the image clear's value
     enc.destroy()
     tex.destroy()
+
+
+@pytest.mark.parametrize("program", [scenes.PROGRAM_FLAT_COLOR, scenes.PROGRAM_BLINN_PHONG])
+def test_depth_range_discard(device, program):
+    """Vertex depths spread over [-0.22, 1.22]: fragments outside [0, 1] are
+    discarded per fragment, so the lane raster's range test runs
+    (its loop without the test serves only waves whose vertices are all inside)."""
+    s = scenes.soup_scene(23, 1500, 192, 128, 14.0, program)
+    z = s.vertices[:, 2]
+    s.vertices[:, 2] = z * np.float32(1.6) - np.float32(0.3)
+    assert (s.vertices[:, 2] < 0).any() and (s.vertices[:, 2] > 1).any()
+    assert_parity(device, s)
