@@ -250,6 +250,7 @@ struct zr_device_t {
     uint32_t setup_batch = 2;  // k_setup_bin primitives per lane in flight (ZR_SETUP_BATCH: 1, 2, 4)
     uint32_t tile_threads = 0; // k_tile workgroup size override (ZR_TILE_NT: 256, 512; 0 = by tile count)
     int tile_split = -1;       // k_tile workgroups per tile (ZR_TILE_SPLIT: 1, 2, 4, 8; -1 = tile_split_for)
+    uint64_t setup_per_wg = 0; // k_setup_bin primitives per workgroup at least (ZR_SETUP_PER_WG; 0 = threads x batch)
     uint32_t debug = 0;
     uint64_t initial_bins = 0;  // 0 = max(2^20, 2 * primitives of the first draw)
     uint64_t min_bins = 0;      // bin capacity an overflow asked for
@@ -735,7 +736,7 @@ zr_result exec_draw(zr_device* d, ExecState& s, const Cmd& c, bool indexed) {
         // one workgroup per CU (fewer for small draws); a wave processes units of
         // 64 * batch * 2^k primitives, at most ~64 units per workgroup on average
         const uint64_t cus = (uint64_t)std::max(d->cu_count, 1);
-        const uint64_t per_wg = (uint64_t)kSetupThreads * P.setup_batch;
+        const uint64_t per_wg = d->setup_per_wg ? d->setup_per_wg : (uint64_t)kSetupThreads * P.setup_batch;
         P.setup_wgs = (uint32_t)std::max<uint64_t>(1, std::min<uint64_t>(cus, (positions + per_wg - 1) / per_wg));
         uint32_t shift = 6;
         while ((1u << shift) < 64u * P.setup_batch) ++shift;
@@ -950,6 +951,7 @@ ZR_API zr_result zr_device_create(int32_t hip_device, zr_device** out) {
         const unsigned long v = strtoul(nt, nullptr, 0);
         d->tile_threads = v >= 512 ? 512u : v ? 256u : 0u;
     }
+    if (const char* o = getenv("ZR_SETUP_PER_WG")) d->setup_per_wg = strtoull(o, nullptr, 0);
     if (const char* o = getenv("ZR_TILE_SPLIT")) {
         const unsigned long v = strtoul(o, nullptr, 0);
         d->tile_split = v >= 8 ? 8 : v >= 4 ? 4 : v >= 2 ? 2 : 1;
