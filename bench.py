@@ -40,6 +40,9 @@ def parse():
     p.add_argument("--config", default="c2", choices=sorted(scenes.CONFIGS))
     p.add_argument("--cpu-seconds", type=float, default=10.0, help="CPU baseline sample length")
     p.add_argument("--no-cpu-baseline", action="store_true")
+    p.add_argument("--rotate", type=int, default=1, metavar="K",
+                   help="K uploaded copies of the geometry, cycled frame to frame (K=3 puts C2's 360 MB of "
+                        "input past the 256 MiB Infinity Cache: the HBM-honest rate, SURVEY.md §8d)")
     p.add_argument("--emulate-shard", type=int, default=0, metavar="G",
                    help="diagnostic (1 GPU): run only rank 0's share of a G-way tile-row shard, no gather "
                         "(partitioned setup: rank 0's routed block stands in for every source's)")
@@ -147,7 +150,7 @@ def main():
               for i, t in enumerate(color_ts)]
     color = colors[0]
     depth = rhi.Texture(dev, rhi.TextureDesc.new_depth("frame.depth", W, H), depth_t.data_ptr())
-    r = renderer.SceneRenderer(dev, scene)
+    rs = [renderer.SceneRenderer(dev, scene) for _ in range(max(1, a.rotate))]
     if a.emulate_shard and distributed:
         raise SystemExit("--emulate-shard is a 1-GPU diagnostic")
     shard_g = a.emulate_shard if a.emulate_shard > 1 else world
@@ -172,8 +175,8 @@ def main():
     elif a.setup == "partitioned" and shard_g > 1:
         exchange = MirrorExchange(cuda, shard_g)
     sh = (rank, shard_g, exchange) if exchange is not None else ((rank, shard_g) if shard_g > 1 else None)
-    encs = [r.record(c, depth, shard=sh, encoder=rhi.CommandEncoder(dev)) for c in colors]
-    enc = encs[0]
+    # encs[copy][target]: frame f draws geometry copy f % K into target f % nbuf
+    encs = [[r.record(c, depth, shard=sh, encoder=rhi.CommandEncoder(dev)) for c in colors] for r in rs]
     gather = shard.TileRowGather(H, W * 4, rank, world, cuda) if distributed and not runtime_comm else None
     # Multi-GPU: torch's current stream is the runtime's main stream, so frames,
     # exchanges and gathers are ordered by streams and events, never a host wait.
@@ -189,11 +192,12 @@ def main():
 
     def step():
         b = frame[0] % nbuf
+        enc = encs[frame[0] % len(encs)][b]
         frame[0] += 1
         if gdone[b] is not None:
             main_stream.wait_event(gdone[b])  # the gather of frame f-2 read this target
         h0 = time.perf_counter()
-        dev.submit(encs[b])
+        dev.submit(enc)
         h1 = time.perf_counter()
         host_t[0] += h1 - h0
         if runtime_comm:
@@ -269,7 +273,7 @@ def main():
     dom = max(launches, key=lambda k: launches[k][0]) if launches else "tile"
     dk = kernels.get(dom, {})
     traffic = None
-    if os.path.exists(a.pmc):
+    if os.path.exists(a.pmc) and len(rs) == 1:  # the PMC summary was measured on one copy
         with open(a.pmc) as fh:
             pmc = json.load(fh)
         if pmc.get("config") == a.config and dom in pmc.get("kernels", {}):
@@ -289,7 +293,7 @@ def main():
                                 f"{a.config}: {N} tris soup, {W}x{H}, "
                                 f"{'Blinn-Phong' if scene.program == scenes.PROGRAM_BLINN_PHONG else 'flat'} "
                                 f"+ D32 LESS, B8G8R8A8_SRGB"),
-                   "triangles": N, "width": W, "height": H, "tile": shard.TILE,
+                   "triangles": N, "width": W, "height": H, "tile": shard.TILE, "input_copies": len(rs),
                    "parallelism": f"tile-rows x{world}" + (
                        f", {a.setup} setup" + (" (RCCL all-to-all)" if exchange is not None else "")
                        + f" + RCCL row gather ({'runtime' if runtime_comm else 'torch'} communicators)"
@@ -320,8 +324,9 @@ def main():
     if stream_ctx is not None:
         dev.wait_idle()
         stream_ctx.__exit__(None, None, None)
-    for e in encs:
-        e.destroy()
+    for row in encs:
+        for e in row:
+            e.destroy()
     for c in colors:
         c.destroy()
     depth.destroy()
