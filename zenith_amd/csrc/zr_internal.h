@@ -138,6 +138,7 @@ struct DrawParams {
     uint64_t vb_bytes;
     const uint8_t* ib;
     uint64_t ib_bytes;
+    uint64_t vid_count;       // vertex v has every attribute inside vb_bytes iff v < vid_count (host-computed)
     uint32_t stride;
     uint32_t nattr;
     uint32_t attr_offset[4];

@@ -61,6 +61,9 @@ namespace zr {
 #ifndef ZR_TILE_SUBLANE
 #define ZR_TILE_SUBLANE 1    // sparse segments: k lanes per entry split its bbox rows (0: one lane per entry)
 #endif
+#ifndef ZR_SETUP_LOAD_PROBE
+#define ZR_SETUP_LOAD_PROBE 0  // 1: ZR_DEBUG=16 makes phase 1 issue its loads only (timing probe)
+#endif
 
 __constant__ float c_srgbT[255] = ZR_SRGB_THRESHOLDS_INIT;
 
@@ -278,11 +281,8 @@ __device__ __forceinline__ void fetch_indices(const DrawParams& P, uint32_t pos,
 
 __device__ __forceinline__ void fetch_positions(const DrawParams& P, PrimIn& in) {
     if (!in.ok) return;
-    bool ok = true;
-#pragma unroll
-    for (int k = 0; k < 3; ++k)
-        for (uint32_t a = 0; a < P.nattr; ++a)
-            ok = ok && ((uint64_t)in.vid[k] * P.stride + P.attr_offset[a] + P.attr_size[a] <= P.vb_bytes);
+    // every attribute of the three vertices inside the buffer (vid_count: DrawParams)
+    const bool ok = in.vid[0] < P.vid_count && in.vid[1] < P.vid_count && in.vid[2] < P.vid_count;
     in.ok = ok;
     if (!ok) return;
 #pragma unroll
@@ -929,6 +929,16 @@ __global__ __launch_bounds__(kSetupThreads) void k_setup_bin(DrawParams P) {
                 for (uint32_t b = 0; b < KB; ++b) fetch_indices(P, pb + b * 64u, n_pos, s_pre, in[b], gid[b]);
 #pragma unroll
                 for (uint32_t b = 0; b < KB; ++b) fetch_positions(P, in[b]);
+#if ZR_SETUP_LOAD_PROBE
+                if (P.debug & kDebugLoadOnly) {  // timing probe: the loads alone
+#pragma unroll
+                    for (uint32_t b = 0; b < KB; ++b)
+                        asm volatile("" ::"v"(in[b].p[0].x), "v"(in[b].p[0].y), "v"(in[b].p[0].z), "v"(in[b].p[1].x),
+                                     "v"(in[b].p[1].y), "v"(in[b].p[1].z), "v"(in[b].p[2].x), "v"(in[b].p[2].y),
+                                     "v"(in[b].p[2].z));
+                    continue;
+                }
+#endif
 #pragma unroll
                 for (uint32_t b = 0; b < KB; ++b) {
                     const uint32_t prim = min(pb + b * 64u, n_pos);

@@ -636,6 +636,11 @@ zr_result exec_draw(zr_device* d, ExecState& s, const Cmd& c, bool indexed) {
         P.attr_offset[i] = pp->attr_offset[i];
         P.attr_size[i] = pp->attr_size[i];
     }
+    {  // one compare per vertex in the kernels instead of one per (vertex, attribute)
+        uint64_t end = 0;
+        for (uint32_t a = 0; a < P.nattr; ++a) end = std::max<uint64_t>(end, (uint64_t)P.attr_offset[a] + P.attr_size[a]);
+        P.vid_count = P.nattr == 0 ? (1ull << 32) : (P.vb_bytes < end ? 0ull : (P.vb_bytes - end) / P.stride + 1ull);
+    }
     if (indexed) {
         P.ib = (const uint8_t*)s.ib->ptr + s.ib_offset;
         P.ib_bytes = s.ib->size > s.ib_offset ? s.ib->size - s.ib_offset : 0;
