@@ -139,6 +139,7 @@ struct DrawParams {
     const uint8_t* ib;
     uint64_t ib_bytes;
     uint64_t vid_count;       // vertex v has every attribute inside vb_bytes iff v < vid_count (host-computed)
+    uint32_t ib_tris;         // u32 indices: triangle t's 3 indices lie inside ib_bytes iff t < ib_tris
     uint32_t stride;
     uint32_t nattr;
     uint32_t attr_offset[4];

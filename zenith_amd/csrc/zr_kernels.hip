@@ -242,12 +242,16 @@ __device__ __forceinline__ void fetch_indices_gid(const DrawParams& P, uint32_t 
     const uint32_t tri = tri_of(P, gid);
     const uint64_t e0 = (uint64_t)P.first + (uint64_t)tri * 3u;
     bool ok = true;
-    if (P.index_size == 4 && (e0 + 3) * 4 <= P.ib_bytes) {
+    if (P.index_size == 4 && tri < P.ib_tris) {  // ib_tris: the triangles whose 3 indices are in the buffer
         const uint3 ix = *reinterpret_cast<const uint3*>(P.ib + e0 * 4);  // one 12-B load
-        const int64_t v0 = (int64_t)ix.x + P.vertex_offset, v1 = (int64_t)ix.y + P.vertex_offset,
-                      v2 = (int64_t)ix.z + P.vertex_offset;
-        ok = v0 >= 0 && v0 <= 0xFFFFFFFFll && v1 >= 0 && v1 <= 0xFFFFFFFFll && v2 >= 0 && v2 <= 0xFFFFFFFFll;
-        in.vid[0] = (uint32_t)v0; in.vid[1] = (uint32_t)v1; in.vid[2] = (uint32_t)v2;
+        if (P.vertex_offset == 0) {  // wave-uniform: u32 ids need no range check
+            in.vid[0] = ix.x; in.vid[1] = ix.y; in.vid[2] = ix.z;
+        } else {
+            const int64_t v0 = (int64_t)ix.x + P.vertex_offset, v1 = (int64_t)ix.y + P.vertex_offset,
+                          v2 = (int64_t)ix.z + P.vertex_offset;
+            ok = v0 >= 0 && v0 <= 0xFFFFFFFFll && v1 >= 0 && v1 <= 0xFFFFFFFFll && v2 >= 0 && v2 <= 0xFFFFFFFFll;
+            in.vid[0] = (uint32_t)v0; in.vid[1] = (uint32_t)v1; in.vid[2] = (uint32_t)v2;
+        }
     } else {
 #pragma unroll
         for (int k = 0; k < 3; ++k) {

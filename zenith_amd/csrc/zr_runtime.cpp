@@ -647,7 +647,10 @@ zr_result exec_draw(zr_device* d, ExecState& s, const Cmd& c, bool indexed) {
         P.index_size = s.index_type == ZR_INDEX_TYPE_UINT16 ? 2u : 4u;
         P.first = c.c;
         P.vertex_offset = c.e;
+        const uint64_t nidx = P.ib_bytes / 4;  // only read for u32 indices (k_setup_bin fetch_indices_gid)
+        P.ib_tris = nidx > P.first ? (uint32_t)std::min<uint64_t>((nidx - P.first) / 3, 0xFFFFFFFFull) : 0u;
     } else {
+        P.ib_tris = 0;
         P.index_size = 0;
         P.first = c.c;
         P.vertex_offset = 0;
