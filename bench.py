@@ -25,11 +25,12 @@ sys.path.insert(0, ROOT)
 
 from zenith_amd import renderer, rhi, scenes, shard, zr  # noqa: E402
 
-HBM_PEAK_GBPS = 8000.0           # MI355X_MICROARCH.md: HBM3E 8.0 TB/s spec
-HBM_MEASURED_GBPS = 6290.0       # same table: float4 copy achievable
+HBM_PEAK_GBPS = 6290.0           # MI355X_MICROARCH.md: HBM3E measured (float4 copy), the peak SURVEY.md §8d fixes
+HBM_SPEC_GBPS = 8000.0           # same table: 8.0 TB/s spec
 METRIC = BASELINE_METRIC = "Mtriangles/s + frames/s at 1080p (1M-tri scene), 1/2/4/8 GPU; HBM GB/s vs roofline"
 RECORD_BYTES = 32                # TriCompact, the per-primitive record k_tile reads per pair (zr_internal.h)
 BIN_ENTRY_BYTES = 4
+SURVEY_PAIR_BYTES = 68           # SURVEY.md §8d fragment pass: 4-B bin entry + 64-B setup record per pair
 
 
 def parse():
@@ -40,9 +41,10 @@ def parse():
     p.add_argument("--config", default="c2", choices=sorted(scenes.CONFIGS))
     p.add_argument("--cpu-seconds", type=float, default=10.0, help="CPU baseline sample length")
     p.add_argument("--no-cpu-baseline", action="store_true")
-    p.add_argument("--rotate", type=int, default=1, metavar="K",
-                   help="K uploaded copies of the geometry, cycled frame to frame (K=3 puts C2's 360 MB of "
-                        "input past the 256 MiB Infinity Cache: the HBM-honest rate, SURVEY.md §8d)")
+    p.add_argument("--cold-copies", type=int, default=3, metavar="K",
+                   help="value_cold: a second timed pass cycling K uploaded copies of the geometry frame to "
+                        "frame (K=3 puts C2's 360 MB of input past the 256 MiB Infinity Cache: the HBM-honest "
+                        "rate, SURVEY.md §8d); 0 skips it")
     p.add_argument("--emulate-shard", type=int, default=0, metavar="G",
                    help="diagnostic (1 GPU): run only rank 0's share of a G-way tile-row shard, no gather "
                         "(partitioned setup: rank 0's routed block stands in for every source's)")
@@ -81,11 +83,35 @@ def algorithmic_bytes(kernel, n_tris, b_in, pairs, pixels, n_route=0):
     return 0
 
 
+def host_cpus():
+    """(threads, nproc --all, CPU model): SURVEY.md §8d times the baseline on all
+    the host cores the process may use, i.e. what `nproc` reports (it honours the
+    affinity mask and OMP_NUM_THREADS, 16 on the GPU box's share)."""
+    import subprocess
+
+    def run(*cmd):
+        try:
+            return subprocess.run(cmd, capture_output=True, text=True, timeout=10).stdout
+        except (OSError, subprocess.SubprocessError):
+            return ""
+    try:
+        threads = int(run("nproc").strip())
+    except ValueError:
+        threads = len(os.sched_getaffinity(0))
+    try:
+        total = int(run("nproc", "--all").strip())
+    except ValueError:
+        total = os.cpu_count() or threads
+    model = next((ln.split(":", 1)[1].strip() for ln in run("lscpu").splitlines()
+                  if ln.startswith("Model name")), "unknown")
+    return max(1, threads), total, model
+
+
 def cpu_baseline(scene, seconds, max_frames=500):
     """The CPU oracle (oracle/, OpenMP over tile-row bands) on the same scene:
     1 warm-up frame, then whole frames until ``seconds`` of wall time have passed."""
     from oracle import oracle
-    threads = min(16, os.cpu_count() or 1)
+    threads, total, model = host_cpus()
     oracle.render(scene, nthreads=threads)  # warm-up
     frames = 0
     t0 = time.perf_counter()
@@ -94,9 +120,9 @@ def cpu_baseline(scene, seconds, max_frames=500):
         frames += 1
     dt = time.perf_counter() - t0
     return {"value": round(scene.triangles * frames / dt / 1e6, 3), "unit": "Mtri/s", "cores": threads,
-            "kind": "port",
+            "kind": "port", "nproc": threads, "nproc_all": total, "cpu_model": model,
             "sample": f"{frames} full frames of {scene.name} ({scene.triangles} tris, {scene.width}x{scene.height}) "
-                      f"after 1 warm-up; {dt:.2f} s wall on {threads} threads"}
+                      f"after 1 warm-up; {dt:.2f} s wall on {threads} threads (nproc; {total} CPUs online, {model})"}
 
 
 class MirrorExchange(shard.Exchange):
@@ -150,7 +176,8 @@ def main():
               for i, t in enumerate(color_ts)]
     color = colors[0]
     depth = rhi.Texture(dev, rhi.TextureDesc.new_depth("frame.depth", W, H), depth_t.data_ptr())
-    rs = [renderer.SceneRenderer(dev, scene) for _ in range(max(1, a.rotate))]
+    # copy 0 is the warm (value) pass's geometry; copies 0..K-1 cycle in the cold pass
+    rs = [renderer.SceneRenderer(dev, scene) for _ in range(max(1, a.cold_copies))]
     if a.emulate_shard and distributed:
         raise SystemExit("--emulate-shard is a 1-GPU diagnostic")
     shard_g = a.emulate_shard if a.emulate_shard > 1 else world
@@ -190,9 +217,9 @@ def main():
 
     host_t = [0.0, 0.0]  # host seconds in submit / gather (diagnostic)
 
-    def step():
+    def step(copies):
         b = frame[0] % nbuf
-        enc = encs[frame[0] % len(encs)][b]
+        enc = encs[frame[0] % copies][b]
         frame[0] += 1
         if gdone[b] is not None:
             main_stream.wait_event(gdone[b])  # the gather of frame f-2 read this target
@@ -212,27 +239,38 @@ def main():
             gdone[b] = torch.cuda.Event()
             gdone[b].record(gstream)
 
-    for _ in range(a.warmup):
-        step()
-    dev.wait_idle()
-    torch.cuda.synchronize()
-    if distributed:
-        dist.barrier()
-    torch.cuda.synchronize()
-    host_t[0] = host_t[1] = 0.0
-    t0 = time.perf_counter()
-    for _ in range(a.steps):
-        step()
-    t_enq = time.perf_counter()  # host enqueue time of the K frames (diagnostic: host-bound if ~ wall)
-    dev.wait_idle()
-    torch.cuda.synchronize()
-    if distributed:
-        dist.barrier()
-    t1 = time.perf_counter()
-    elapsed = torch.tensor([t1 - t0], dtype=torch.float64, device=cuda)
-    if distributed:
-        dist.all_reduce(elapsed, op=dist.ReduceOp.MAX)
-    elapsed = float(elapsed.item())
+    def timed_pass(copies):
+        """W untimed frames, then K frames bracketed by barrier + synchronize;
+        returns (max-over-ranks seconds, host enqueue seconds of this rank)."""
+        frame[0] = 0
+        for _ in range(a.warmup):
+            step(copies)
+        dev.wait_idle()
+        torch.cuda.synchronize()
+        if distributed:
+            dist.barrier()
+        torch.cuda.synchronize()
+        host_t[0] = host_t[1] = 0.0
+        t0 = time.perf_counter()
+        for _ in range(a.steps):
+            step(copies)
+        t_enq = time.perf_counter()  # host enqueue time of the K frames (diagnostic: host-bound if ~ wall)
+        dev.wait_idle()
+        torch.cuda.synchronize()
+        if distributed:
+            dist.barrier()
+        t1 = time.perf_counter()
+        el = torch.tensor([t1 - t0], dtype=torch.float64, device=cuda)
+        if distributed:
+            dist.all_reduce(el, op=dist.ReduceOp.MAX)
+        return float(el.item()), t_enq - t0
+
+    # warm pass (the headline value): one geometry copy, its 120 MB (C2) stays in
+    # the Infinity Cache from frame to frame, as in the reference's static scene
+    elapsed, enq = timed_pass(1)
+    host_submit, host_gather = host_t[0], host_t[1]
+    # cold pass: K copies cycled, so every frame's vertex reads come from HBM
+    elapsed_cold = timed_pass(len(rs))[0] if len(rs) > 1 else None
 
     # Per-kernel durations: the same K steps again with HIP events around every
     # launch on the raster stream (events sit between the kernels, so this pass runs
@@ -245,8 +283,9 @@ def main():
     fev = [torch.cuda.Event(enable_timing=True) for _ in range(a.steps + 1)]
     fev[0].record(main_stream)
     tp0 = time.perf_counter()
+    frame[0] = 0
     for i in range(a.steps):
-        step()
+        step(1)
         fev[i + 1].record(main_stream)
     dev.wait_idle()
     tp1 = time.perf_counter()
@@ -260,8 +299,8 @@ def main():
     b_in = scenes.config_bytes_per_triangle(a.config)
     n_setup, n_route = N, 0
     if exchange is not None:  # this rank's range and the triangles it received
-        _, span, _ = shard.route_geometry(N, shard_g)
-        n_route = max(0, min(N, (rank + 1) * span) - rank * span)
+        lo, hi = shard.route_range(N, rank, shard_g)
+        n_route = hi - lo
         n_setup = stats["triangles_setup"]
     kernels = {}
     for name, (ms, n) in kt.items():
@@ -273,12 +312,17 @@ def main():
     dom = max(launches, key=lambda k: launches[k][0]) if launches else "tile"
     dk = kernels.get(dom, {})
     traffic = None
-    if os.path.exists(a.pmc) and len(rs) == 1:  # the PMC summary was measured on one copy
+    if os.path.exists(a.pmc):  # measured on the warm pass's single copy, like `achieved`
         with open(a.pmc) as fh:
             pmc = json.load(fh)
         if pmc.get("config") == a.config and dom in pmc.get("kernels", {}):
             traffic = pmc["kernels"][dom]["hbm_bytes_per_launch"]
     achieved = dk.get("gbps") or 0.0
+    # SURVEY.md §8d's own fragment-pass figure (64-B records: 68 B per pair) beside
+    # this design's minimum (32-B compact records: 36 B per pair)
+    survey_bytes = pairs * SURVEY_PAIR_BYTES + pixels * 8
+    tile_us = kernels.get("tile", {}).get("avg_us") or 0.0
+    achieved_survey = round(survey_bytes / (tile_us * 1e-6) / 1e9, 1) if tile_us > 0 else None
 
     ms_per_step = elapsed / a.steps * 1e3
     value = N * a.steps / elapsed / 1e6
@@ -288,28 +332,36 @@ def main():
         "warmup": a.warmup, "ms_per_step": round(ms_per_step, 4), "higher_is_better": True,
         "scaling": "strong", "vs_baseline": None, "dtype": "f32",
         "data": "synthetic (SplitMix64 triangle soup, SURVEY.md §8d)",
+        **({"value_cold": round(N * a.steps / elapsed_cold / 1e6, 2),
+            "ms_per_step_cold": round(elapsed_cold / a.steps * 1e3, 4),
+            "cold_copies": len(rs)} if elapsed_cold else {}),
         "config": {"workload": (f"{a.config}: {N} tris (reference asset, mesh.slang camera), {W}x{H}, "
                                 f"D32 GREATER (reverse-Z), B8G8R8A8_SRGB" if scene.program == scenes.PROGRAM_MESH else
                                 f"{a.config}: {N} tris soup, {W}x{H}, "
                                 f"{'Blinn-Phong' if scene.program == scenes.PROGRAM_BLINN_PHONG else 'flat'} "
                                 f"+ D32 LESS, B8G8R8A8_SRGB"),
-                   "triangles": N, "width": W, "height": H, "tile": shard.TILE, "input_copies": len(rs),
+                   "triangles": N, "width": W, "height": H, "tile": shard.TILE, "input_copies": 1,
                    "parallelism": f"tile-rows x{world}" + (
                        f", {a.setup} setup" + (" (RCCL all-to-all)" if exchange is not None else "")
                        + f" + RCCL row gather ({'runtime' if runtime_comm else 'torch'} communicators)"
                        if distributed else "")},
         "fps": round(1e3 / ms_per_step, 2),
         "ms_per_step_profiled": round((tp1 - tp0) / a.steps * 1e3, 4),
-        "host_enqueue_ms_per_step": round((t_enq - t0) / a.steps * 1e3, 4),
+        "host_enqueue_ms_per_step": round(enq / a.steps * 1e3, 4),
         "frame_ms_median_profiled": round(frame_ms[len(frame_ms) // 2], 4),
         "frame_ms_p90_profiled": round(frame_ms[min(len(frame_ms) - 1, (9 * len(frame_ms)) // 10)], 4),
-        "host_submit_ms_per_step": round(host_t[0] / a.steps * 1e3, 4),
-        "host_gather_ms_per_step": round(host_t[1] / a.steps * 1e3, 4),
+        "host_submit_ms_per_step": round(host_submit / a.steps * 1e3, 4),
+        "host_gather_ms_per_step": round(host_gather / a.steps * 1e3, 4),
         "frame_alg_bytes": frame_bytes,
         "frame_gbps": round(frame_bytes / (ms_per_step * 1e-3) / 1e9, 1),
         "roofline": {"bound": "hbm", "kernel": dom, "achieved": achieved, "peak": HBM_PEAK_GBPS, "unit": "GB/s",
                      "frac": round(achieved / HBM_PEAK_GBPS, 4), "traffic": traffic,
-                     "peak_measured_copy": HBM_MEASURED_GBPS},
+                     "peak_source": "MI355X_MICROARCH.md measured float4 copy (SURVEY.md §8d)",
+                     "peak_spec": HBM_SPEC_GBPS, "frac_spec": round(achieved / HBM_SPEC_GBPS, 4),
+                     "alg_bytes_per_pair": BIN_ENTRY_BYTES + RECORD_BYTES,
+                     "survey_bytes_per_pair": SURVEY_PAIR_BYTES,
+                     "achieved_survey": achieved_survey,
+                     "frac_survey": round(achieved_survey / HBM_PEAK_GBPS, 4) if achieved_survey else None},
         "kernels": kernels,
         **({"emulated_shard": f"rank 0 of {shard_g} (diagnostic, no gather)"} if a.emulate_shard > 1 else {}),
         "bin_pairs": pairs,

@@ -1,6 +1,6 @@
 """bench.py's contract: the per-pass algorithmic bytes of SURVEY.md §8d and, on
 the GPU, the one JSON line the driver parses (keys, roofline and CPU-baseline
-objects, the --rotate input copies)."""
+objects, the cold-cache pass over rotated input copies)."""
 import json
 import os
 import subprocess
@@ -37,10 +37,10 @@ def test_algorithmic_bytes():
 
 @pytest.mark.gpu
 def test_bench_json_line():
-    """One short C1 run with two input copies, as a child process: stdout holds
-    exactly one JSON line with the contract's keys."""
+    """One short C1 run with a two-copy cold pass, as a child process: stdout holds
+    exactly one JSON line with the contract's keys (SURVEY.md §8d extras included)."""
     cmd = [sys.executable, os.path.join(ROOT, "bench.py"), "--config", "c1", "--steps", "4", "--warmup", "2",
-           "--rotate", "2", "--cpu-seconds", "0.5"]
+           "--cold-copies", "2", "--cpu-seconds", "0.5"]
     out = subprocess.run(cmd, cwd=ROOT, capture_output=True, text=True, timeout=110)
     assert out.returncode == 0, out.stderr[-2000:]
     lines = [ln for ln in out.stdout.splitlines() if ln.strip()]
@@ -50,11 +50,14 @@ def test_bench_json_line():
               "vs_baseline", "dtype", "data", "config", "roofline", "cpu_baseline", "kernels"):
         assert k in d, k
     assert d["unit"] == "Mtri/s" and d["n_gpus"] == 1 and d["steps"] == 4 and d["value"] > 0
-    assert d["config"]["input_copies"] == 2 and d["config"]["triangles"] == 100_000
+    assert d["config"]["input_copies"] == 1 and d["config"]["triangles"] == 100_000
+    assert d["cold_copies"] == 2 and d["value_cold"] > 0
     r = d["roofline"]
-    assert r["bound"] == "hbm" and r["unit"] == "GB/s" and r["peak"] == 8000.0
+    assert r["bound"] == "hbm" and r["unit"] == "GB/s" and r["peak"] == 6290.0 and r["peak_spec"] == 8000.0
     assert r["kernel"] in d["kernels"] and abs(r["frac"] - r["achieved"] / r["peak"]) < 1e-3
+    assert r["survey_bytes_per_pair"] == 68 and r["achieved_survey"] > d["kernels"]["tile"]["gbps"]
     assert r["traffic"] is None  # the committed PMC summary is C2's, not C1's
     cb = d["cpu_baseline"]
     assert cb["kind"] == "port" and cb["cores"] >= 1 and cb["value"] > 0
+    assert cb["nproc"] == cb["cores"] and cb["nproc_all"] >= cb["nproc"] and cb["cpu_model"]
     assert set(d["kernels"]) >= {"setup_bin", "tile"}

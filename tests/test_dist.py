@@ -131,3 +131,15 @@ def test_route_blocks_model():
     for d in range(world):
         recv = torch.stack([sends[s][d] for s in range(world)])
         assert shard.received_primitives(recv, n, world) == _expected(lo, hi, d, world)
+
+
+def test_route_model_matches_device_constants():
+    """The host route model uses the kernels' chunk size (zr_internal.h)."""
+    import re
+    from zenith_amd import shard
+    src = open(os.path.join(ROOT, "zenith_amd", "csrc", "zr_internal.h")).read()
+    assert int(re.search(r"kRouteChunk\s*=\s*(\d+)", src).group(1)) == shard.ROUTE_CHUNK
+    # 1M primitives over 8 ranks: span rounds ceil(N / G) up to whole chunks
+    chunks, span, bw = shard.route_geometry(1_000_000, 8)
+    assert span == 125_440 and bw == span + 1 and chunks == span // shard.ROUTE_CHUNK
+    assert shard.route_range(1_000_000, 7, 8) == (7 * 125_440, 1_000_000)

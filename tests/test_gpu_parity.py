@@ -363,6 +363,64 @@ def test_partitioned_paths():
     assert_partitioned_parity(scenes.triangle_scene(time=1.25), 3)
 
 
+def test_partitioned_ranks_without_rows():
+    """G=8 on a 160x120 target has 4 tile rows: ranks 4-7 own none, yet they still
+    route their ranges and join every exchange (nobody is left waiting)."""
+    assert_partitioned_parity(scenes.soup_scene(77, 4000, 160, 120, 8.0, scenes.PROGRAM_BLINN_PHONG), 8)
+
+
+def test_partitioned_beside_busy_stream():
+    """A partitioned draw while another stream keeps every CU busy (matmuls):
+    list-mode setup runs as two launches with no grid barrier, so it needs no
+    co-residency and cannot time out; the frame is exact."""
+    import threading
+    import torch
+    side = torch.cuda.Stream()
+    a = torch.randn(4096, 4096, device="cuda")
+    stop = threading.Event()
+
+    def busy():
+        with torch.cuda.stream(side):
+            while not stop.is_set():
+                for _ in range(8):
+                    a.matmul(a)
+                side.synchronize()
+
+    t = threading.Thread(target=busy)
+    t.start()
+    try:
+        assert_partitioned_parity(scenes.soup_scene(78, 300_000, 640, 480, 3.0, scenes.PROGRAM_FLAT_COLOR), 2)
+    finally:
+        stop.set()
+        t.join(timeout=60)
+
+
+def test_mixed_draw_sizes_no_sync(device):
+    """A draw above 2^18 primitives (persistent setup, scratch set 0, main stream)
+    followed by small draws (split setup on the setup stream, alternating sets)
+    with no host sync in between: every target equals its own oracle frame."""
+    big = scenes.soup_scene(79, 300_000, 640, 480, 3.0, scenes.PROGRAM_BLINN_PHONG)
+    small = [scenes.soup_scene(80 + i, 2000 + 1000 * i, 320, 240, 9.0, scenes.PROGRAM_FLAT_COLOR) for i in range(3)]
+    jobs = []
+    for s in [big] + small:
+        color = rhi.Texture(device, rhi.TextureDesc.new_color("rt", s.width, s.height, s.color_format))
+        depth = rhi.Texture(device, rhi.TextureDesc.new_depth("ds", s.width, s.height))
+        r = renderer.SceneRenderer(device, s)
+        enc = r.record(color, depth, encoder=rhi.CommandEncoder(device))
+        jobs.append((s, r, enc, color, depth))
+    for _ in range(2):
+        for _, _, enc, _, _ in jobs:
+            device.submit(enc)
+    device.wait_idle()
+    for s, _, enc, color, depth in jobs:
+        oc, od = oracle.render(s)
+        assert np.array_equal(color.read(), oc), s.name
+        assert np.array_equal(depth.read().view(np.uint32), od.view(np.uint32)), s.name
+        enc.destroy()
+        color.destroy()
+        depth.destroy()
+
+
 def test_partitioned_c2_full():
     """C2 (1M triangles, 1920x1080) as 8 partitioned ranks: union = oracle frame."""
     assert_partitioned_parity(scenes.config_scene("c2"), 8)

@@ -990,10 +990,25 @@ __global__ __launch_bounds__(kSetupThreads) void k_setup_bin(DrawParams P) {
     ZR_STAMP(3);
     if (P.debug & kDebugStopAfterScan) return;
 
-    // ---- phase 3: tile bases and this workgroup's cursors
-    for (uint32_t t = tid; t < nt; t += kSetupThreads) s_base[t] = ld_sc1(&P.tile_counts[t]);
+    // ---- phase 3: tile bases and this workgroup's cursors.  The pair total is
+    // also summed in 64 bits: a draw of 2^32 pairs or more would wrap the u32 tile
+    // offsets, so it reports a total past any bin capacity instead (spill path).
+    unsigned long long* s_total64 = reinterpret_cast<unsigned long long*>(s_misc + 26);
+    if (tid == 0) *s_total64 = 0ull;
     __syncthreads();
-    const uint32_t total = block_exclusive_scan(s_base, nt, s_misc + 8);
+    {
+        unsigned long long part = 0;
+        for (uint32_t t = tid; t < nt; t += kSetupThreads) {
+            const uint32_t c = ld_sc1(&P.tile_counts[t]);
+            s_base[t] = c;
+            part += c;
+        }
+        if (part) atomicAdd(s_total64, part);
+    }
+    __syncthreads();
+    const bool wrapped = *s_total64 > 0xFFFFFFFFull;
+    uint32_t total = block_exclusive_scan(s_base, nt, s_misc + 8);
+    if (wrapped) total = 0xFFFFFFFFu;
     if (w == 0) {
         for (uint32_t t = tid; t < nt; t += kSetupThreads) P.tile_offsets[t] = s_base[t];
         if (tid == 0) {

@@ -232,10 +232,6 @@ struct zr_device_t {
     ScratchSet sets[2];
     uint32_t cur_set = 0;
     hipStream_t setup_stream = nullptr;
-    // ZR_OVERLAP=1: overlap draws (measured slower on C2: the persistent setup's
-    // early workgroups hold CU slots at the grid barrier while the tile pass of the
-    // previous draw still needs them).  Default: one stream, set 0.
-    bool overlap = false;
     // k_setup_bin as two launches split at its grid barrier, on the setup stream,
     // so draw i+1's setup fills CUs draw i's tile pass frees.  Measured (1 GPU):
     // C1 (100k tris) 1180 -> 1274 Mtri/s, C2 7925 -> 8007, C3 equal, C4 (10M)
@@ -246,11 +242,7 @@ struct zr_device_t {
     int cu_count = 0;
     uint32_t occupancy_checked_tiles = 0;
     bool occupancy_checked_mesh = false;
-    uint32_t setup_sched = 1;  // k_setup_bin unit schedule (ZR_SETUP_SCHED: 0 contiguous, 1 interleaved)
-    uint32_t setup_batch = 2;  // k_setup_bin primitives per lane in flight (ZR_SETUP_BATCH: 1, 2, 4)
     uint32_t tile_threads = 0; // k_tile workgroup size override (ZR_TILE_NT: 256, 512; 0 = by tile count)
-    int tile_split = -1;       // k_tile workgroups per tile (ZR_TILE_SPLIT: 1, 2, 4, 8; -1 = tile_split_for)
-    uint64_t setup_per_wg = 0; // k_setup_bin primitives per workgroup at least (ZR_SETUP_PER_WG; 0 = threads x batch)
     uint32_t debug = 0;
     uint64_t initial_bins = 0;  // 0 = max(2^20, 2 * primitives of the first draw)
     uint64_t min_bins = 0;      // bin capacity an overflow asked for
@@ -448,7 +440,9 @@ zr_result device_sync(zr_device* d) {
         // Draws with more (tile, primitive) pairs than the bin buffer holds were
         // rasterized exactly by k_tile's scan of all records (slow); size the
         // buffer for the largest draw seen so later draws read tile lists again.
-        const uint64_t need = (uint64_t)st[kStMaxPairs] * 5 / 4 + 4096;
+        // (capped at 2^30 entries, 4 GiB: a larger draw -- k_setup_bin reports a
+        // wrapped 2^32 total as 0xFFFFFFFF -- keeps using the exact spill path)
+        const uint64_t need = std::min<uint64_t>((uint64_t)st[kStMaxPairs] * 5 / 4 + 4096, 1ull << 30);
         st[kStOverflow] = 0;
         d->min_bins = std::max(d->min_bins, need);  // also for a scratch set not allocated yet
         for (ScratchSet& S : d->sets) {
@@ -601,8 +595,17 @@ zr_result ensure_scratch(zr_device* d, ScratchSet& S, DrawParams& P) {
     return ZR_SUCCESS;
 }
 
+zr_result rccl_exchange(void* user, void* stream, const void* send, void* recv, uint64_t bytes_per_rank);
+
 zr_result exec_draw(zr_device* d, ExecState& s, const Cmd& c, bool indexed) {
     if (!s.rendering) return fail(ZR_ERROR_VALIDATION_FAILED, "draw outside begin_rendering/end_rendering");
+    // the runtime's own all-to-all sends one block to every communicator rank and
+    // takes bit d of a route mask for comm rank d: the shard must be that communicator
+    if (s.exchange == &rccl_exchange &&
+        (s.exchange_user != (void*)d || !d->comm_x || d->comm_size != (int)s.shard_count ||
+         d->comm_rank != (int)s.shard_rank))
+        return fail(ZR_ERROR_VALIDATION_FAILED,
+                    "tile shard (rank, count) differs from the device's RCCL communicator (zr_device_init_rccl)");
     const zr_pipeline* pp = s.pipe;
     if (!pp) return fail(ZR_ERROR_VALIDATION_FAILED, "draw without a bound pipeline");
     if (!s.vp_set || !s.sc_set)
@@ -616,7 +619,11 @@ zr_result exec_draw(zr_device* d, ExecState& s, const Cmd& c, bool indexed) {
     memset(&P, 0, sizeof P);
     zr_result rc = fill_target(s, P);
     if (rc) return rc;
-    if (P.ntiles == 0) return ZR_SUCCESS;  // a tile-row shard that owns no row of this target
+    // A tile-row shard that owns no row of this target draws nothing, but a
+    // partitioned one still routes its range and joins the exchange (every rank
+    // calls the collective once per draw, zenith_raster.h).
+    const bool no_tiles = P.ntiles == 0;
+    if (no_tiles && !s.exchange) return ZR_SUCCESS;
     if (!pp->has_fs) {
         P.color = nullptr;
         P.color_bpp = 0;
@@ -730,8 +737,7 @@ zr_result exec_draw(zr_device* d, ExecState& s, const Cmd& c, bool indexed) {
     // (every workgroup resident: it synchronises through grid barriers)
     if (P.ntiles > kMaxTilesPerPass)
         return fail(ZR_ERROR_FEATURE_NOT_PRESENT, "more than 16384 owned 32x32 tiles in one pass");
-    P.setup_batch = mesh ? 1u : d->setup_batch;  // the mesh instance is k_setup_bin<1, true>
-    P.setup_sched = d->setup_sched;
+    P.setup_batch = mesh ? 1u : 2u;  // k_setup_bin<2> (the mesh instance: <1, true>)
     if (d->occupancy_checked_tiles != P.ntiles || d->occupancy_checked_mesh != mesh) {
         int nb = 0;
         ZR_HIP(hipOccupancyMaxActiveBlocksPerMultiprocessor(&nb, setup_bin_kernel(P.setup_batch, mesh), kSetupThreads,
@@ -744,7 +750,7 @@ zr_result exec_draw(zr_device* d, ExecState& s, const Cmd& c, bool indexed) {
         // one workgroup per CU (fewer for small draws); a wave processes units of
         // 64 * batch * 2^k primitives, at most ~64 units per workgroup on average
         const uint64_t cus = (uint64_t)std::max(d->cu_count, 1);
-        const uint64_t per_wg = d->setup_per_wg ? d->setup_per_wg : (uint64_t)kSetupThreads * P.setup_batch;
+        const uint64_t per_wg = (uint64_t)kSetupThreads * P.setup_batch;
         P.setup_wgs = (uint32_t)std::max<uint64_t>(1, std::min<uint64_t>(cus, (positions + per_wg - 1) / per_wg));
         uint32_t shift = 6;
         while ((1u << shift) < 64u * P.setup_batch) ++shift;
@@ -762,16 +768,9 @@ zr_result exec_draw(zr_device* d, ExecState& s, const Cmd& c, bool indexed) {
     // split setup: default batch or the mesh instance, not list mode; bboxes and per-workgroup
     // offsets cross the launch boundary through global memory
     const bool split = (d->setup_split > 0 || (d->setup_split < 0 && (prims <= (1u << 18) || P.shard_count > 1))) &&
-                       !partitioned && !d->use_graphs && !d->debug && (mesh || P.setup_batch == 2);
+                       !partitioned && !d->use_graphs && !d->debug;
     if (split) P.bbox_lds = 0;
     P.tile_threads = d->tile_threads ? d->tile_threads : tile_threads_for(P.ntiles, (uint32_t)std::max(d->cu_count, 1), prims);
-#if ZR_TILE_SPLIT_BUILD
-    P.tile_split = d->tile_split >= 0 ? (uint32_t)d->tile_split
-                                      : tile_split_for(P.ntiles, (uint32_t)std::max(d->cu_count, 1), P.tile_threads);
-    if (P.tile_split < 1) P.tile_split = 1;
-#else
-    P.tile_split = 1;  // k_tile built without split tiles (zr_kernels.hip ZR_TILE_SPLIT_BUILD)
-#endif
     P.debug = d->debug;
     if (d->debug & kDebugStamps) {
         if (!d->dbg_ts) ZR_HIP(hipMalloc((void**)&d->dbg_ts, (8192 + kMaxTilesPerPass) * 8 * sizeof(unsigned long long)));
@@ -779,12 +778,12 @@ zr_result exec_draw(zr_device* d, ExecState& s, const Cmd& c, bool indexed) {
         d->dbg_wgs = P.setup_wgs;
         d->dbg_tiles = P.ntiles;
     }
-    // Draws alternate between the two scratch sets when overlapping (not while
+    // Split and partitioned draws alternate between the two scratch sets (not while
     // debugging or with graph replay, whose captures bake in set 0: one stream).
     // Partitioned draws always use both scratch sets and streams: the route and the
     // exchange of draw i+1 run on setup_stream while draw i's setup + tile pass
     // run on the main stream.
-    const bool overlap = (d->overlap && !d->debug && !d->use_graphs) || partitioned || split;
+    const bool overlap = partitioned || split;
     ScratchSet& S = d->sets[overlap ? d->cur_set : 0];
     if (overlap) d->cur_set ^= 1u;
     if ((rc = ensure_scratch(d, S, P))) return rc;
@@ -820,8 +819,22 @@ zr_result exec_draw(zr_device* d, ExecState& s, const Cmd& c, bool indexed) {
         if (xr != ZR_SUCCESS) return fail(xr, "tile-shard exchange callback failed: " + g_last_error);
         P.list = S.xrecv;
         ZR_HIP(hipEventRecord(S.setup_done, ss));
+        if (no_tiles) {  // routed and exchanged; nothing of this target to draw here
+            s.color_clear_pending = false;
+            s.depth_clear_pending = false;
+            return ZR_SUCCESS;
+        }
         ZR_HIP(hipStreamWaitEvent(d->stream, S.setup_done, 0));
-        timed_launch(d, "setup_bin", d->stream, [&] { launch_setup_bin(P, d->stream); });
+        // List mode runs as the two split launches (no grid barrier): a partitioned
+        // draw shares the GPU with the collectives' kernels on other streams, so a
+        // persistent launch could not count on every workgroup being resident.
+        if ((rc = grow(d, S.wg_offsets, S.wg_offsets_cap, (uint64_t)P.setup_wgs * P.ntiles, 4))) return rc;
+        P.wg_offsets = S.wg_offsets;
+        P.bbox_lds = 0;
+        timed_launch(d, "setup_bin", d->stream, [&] {
+            launch_setup_split(P, 1, d->stream);
+            launch_setup_split(P, 2, d->stream);
+        });
     } else if (split) {
         if ((rc = grow(d, S.wg_offsets, S.wg_offsets_cap, (uint64_t)P.setup_wgs * P.ntiles, 4))) return rc;
         P.wg_offsets = S.wg_offsets;
@@ -839,7 +852,11 @@ zr_result exec_draw(zr_device* d, ExecState& s, const Cmd& c, bool indexed) {
         }
     }
     timed_launch(d, "tile", d->stream, [&] { launch_tile(P, d->stream); });
-    if (overlap) {
+    // Every draw marks its set's last reader, overlapping or not: a later draw that
+    // sets up on setup_stream into this set waits for it (a draw on d->stream alone
+    // would otherwise leave the set's event stale for the next split draw).
+    // (A graph capture uses set 0 only; submit_graph_or_eager marks it after the replay.)
+    if (!d->capturing) {
         ZR_HIP(hipEventRecord(S.tile_done, d->stream));
         S.tile_done_valid = true;
     }
@@ -952,21 +969,10 @@ ZR_API zr_result zr_device_create(int32_t hip_device, zr_device** out) {
     if (const char* p = getenv("ZR_DEBUG_TS")) d->dbg_ts_path = p;
     if (const char* cap = getenv("ZR_BIN_CAPACITY")) d->initial_bins = std::max<uint64_t>(64, strtoull(cap, nullptr, 0));
     if (const char* g = getenv("ZR_GRAPH")) d->use_graphs = strtoul(g, nullptr, 0) != 0;
-    if (const char* o = getenv("ZR_OVERLAP")) d->overlap = strtoul(o, nullptr, 0) != 0;
     if (const char* o = getenv("ZR_SETUP_SPLIT")) d->setup_split = strtoul(o, nullptr, 0) != 0 ? 1 : 0;
-    if (const char* sc = getenv("ZR_SETUP_SCHED")) d->setup_sched = std::min<uint32_t>(1, (uint32_t)strtoul(sc, nullptr, 0));
     if (const char* nt = getenv("ZR_TILE_NT")) {
         const unsigned long v = strtoul(nt, nullptr, 0);
         d->tile_threads = v >= 512 ? 512u : v ? 256u : 0u;
-    }
-    if (const char* o = getenv("ZR_SETUP_PER_WG")) d->setup_per_wg = strtoull(o, nullptr, 0);
-    if (const char* o = getenv("ZR_TILE_SPLIT")) {
-        const unsigned long v = strtoul(o, nullptr, 0);
-        d->tile_split = v >= 8 ? 8 : v >= 4 ? 4 : v >= 2 ? 2 : 1;
-    }
-    if (const char* b = getenv("ZR_SETUP_BATCH")) {
-        const unsigned long v = strtoul(b, nullptr, 0);
-        d->setup_batch = v >= 4 ? 4u : (v >= 2 ? 2u : 1u);
     }
     ZR_HIP(hipSetDevice(hip_device));
     ZR_HIP(hipStreamCreateWithFlags(&d->stream, hipStreamNonBlocking));
@@ -1745,9 +1751,16 @@ static zr_result submit_graph_or_eager(zr_device* d, zr_cmd* c) {
         c->eager_runs++;
         return execute(d, c);
     }
+    // a replayed graph's draws read and write scratch set 0 on the main stream
+    auto mark_set0 = [d]() -> zr_result {
+        if (!d->sets[0].tile_done) return ZR_SUCCESS;
+        ZR_HIP(hipEventRecord(d->sets[0].tile_done, d->stream));
+        d->sets[0].tile_done_valid = true;
+        return ZR_SUCCESS;
+    };
     if (c->graph && c->graph_gen == d->scratch_gen) {
         ZR_HIP(hipGraphLaunch(c->graph, d->stream));
-        return ZR_SUCCESS;
+        return mark_set0();
     }
     c->drop_graph();
     const uint64_t gen = d->scratch_gen;
@@ -1763,7 +1776,7 @@ static zr_result submit_graph_or_eager(zr_device* d, zr_cmd* c) {
         if (ie == hipSuccess) {
             c->graph_gen = gen;
             ZR_HIP(hipGraphLaunch(c->graph, d->stream));
-            return ZR_SUCCESS;
+            return mark_set0();
         }
         c->graph = nullptr;
     } else if (g) {

@@ -53,53 +53,61 @@ class TileRowGather:
 #
 # zr_cmd_set_tile_shard_exchange (include/zenith_raster.h): each
 # rank routes 1/G of a draw's primitives to the ranks owning the tile rows they
-# touch; the routing lists travel in one all-to-all per draw.  Block layout per
-# destination (zr_internal.h): [chunks] u32 counts, then [chunks][ROUTE_CHUNK]
-# u32 primitive ids, each chunk's ids in primitive order.
+# touch; the routing lists travel in one all-to-all per draw.  Host model of the
+# device layout (zr_internal.h kRouteChunk, zr_runtime.cpp exec_draw): rank r
+# routes primitives [r * span, (r + 1) * span) with span = ceil(ceil(N / G) /
+# ROUTE_CHUNK) * ROUTE_CHUNK; its block for one destination is [1] u32 count, then
+# up to `span` u32 primitive ids in primitive order (block_words = span + 1).
 
-ROUTE_CHUNK = 4096  # zr::kRouteChunk
+ROUTE_CHUNK = 512  # zr::kRouteChunk (primitives per k_route workgroup)
 
 
 def route_geometry(n_prims: int, world: int):
     """(chunks, span, block_words) of a G-way partitioned draw of n primitives."""
     per_rank = -(-n_prims // world)
     chunks = max(1, -(-per_rank // ROUTE_CHUNK))
-    return chunks, chunks * ROUTE_CHUNK, chunks * (ROUTE_CHUNK + 1)
+    span = chunks * ROUTE_CHUNK
+    return chunks, span, span + 1
+
+
+def route_range(n_prims: int, rank: int, world: int):
+    """[lo, hi) of the primitives rank `rank` routes."""
+    _, span, _ = route_geometry(n_prims, world)
+    lo = min(n_prims, rank * span)
+    return lo, min(n_prims, lo + span)
 
 
 def route_blocks(row_lo, row_hi, rank: int, world: int) -> torch.Tensor:
-    """Host model of k_route for rank `rank`: row_lo/row_hi are each primitive's
-    first/last tile row (row_lo < 0: no sample).  Returns the send buffer,
-    [world][block_words] uint32 (as int64 for portability)."""
+    """Host model of k_route_count + k_route_scatter for rank `rank`: row_lo/row_hi
+    are each primitive's first/last tile row (row_lo < 0: no sample).  Returns the
+    send buffer, [world][block_words] uint32 (as int64 for portability)."""
     n = len(row_lo)
-    chunks, span, bw = route_geometry(n, world)
+    _, span, bw = route_geometry(n, world)
     send = torch.zeros((world, bw), dtype=torch.int64)
-    lo, hi = min(n, rank * span), min(n, rank * span + span)
-    for c in range(chunks):
-        fill = [0] * world
-        for p in range(lo + c * ROUTE_CHUNK, min(hi, lo + (c + 1) * ROUTE_CHUNK)):
-            a, b = int(row_lo[p]), int(row_hi[p])
-            if a < 0:
-                continue
-            dests = range(world) if b - a + 1 >= world else sorted({t % world for t in range(a, b + 1)})
-            for d in dests:
-                send[d, chunks + c * ROUTE_CHUNK + fill[d]] = p
-                fill[d] += 1
-        for d in range(world):
-            send[d, c] = fill[d]
+    lo, hi = route_range(n, rank, world)
+    fill = [0] * world
+    for p in range(lo, hi):
+        a, b = int(row_lo[p]), int(row_hi[p])
+        if a < 0:
+            continue
+        dests = range(world) if b - a + 1 >= world else sorted({t % world for t in range(a, b + 1)})
+        for d in dests:
+            send[d, 1 + fill[d]] = p
+            fill[d] += 1
+    for d in range(world):
+        send[d, 0] = fill[d]
     return send
 
 
 def received_primitives(recv: torch.Tensor, n_prims: int, world: int) -> list:
     """Primitive ids a rank's received blocks hold, in block-position order
     (= API order, the sequence the visibility keys use)."""
-    chunks, _, bw = route_geometry(n_prims, world)
+    _, _, bw = route_geometry(n_prims, world)
     recv = recv.reshape(world, bw)
     out = []
     for s in range(world):
-        for c in range(chunks):
-            k = int(recv[s, c])
-            out += recv[s, chunks + c * ROUTE_CHUNK: chunks + c * ROUTE_CHUNK + k].tolist()
+        k = int(recv[s, 0])
+        out += recv[s, 1:1 + k].tolist()
     return out
 
 
