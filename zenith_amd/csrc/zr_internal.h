@@ -180,10 +180,7 @@ struct DrawParams {
     // tiling / sharding
     uint32_t tiles_x, tiles_y, shard_rank, shard_count, owned_rows, ntiles;
     uint32_t tile_threads;    // k_tile workgroup size: 256 or 512 (tile_threads_for)
-    uint32_t tile_split;      // k_tile workgroups per tile (tile_split_for); > 1 uses the three below
-    unsigned long long* tile_keys;  // [ntiles][kTilePixels] merged visibility keys, ~0 between draws
-    uint32_t* tile_arrive;    // [ntiles] parts done, 0 between draws
-    uint32_t* tile_any;       // [ntiles] spill path: min primitive touching the tile, ~0 between draws
+    unsigned long long* tile_keys;  // [ntiles][kTilePixels] (ZR_SPLIT_RESOLVE): k_tile's keys for k_resolve, or nullptr
     // partitioned setup (list mode).  In list mode `prims` is the
     // capacity of the received blocks (shard_count * span); the setup pass runs
     // over the dense positions [0, sum of the blocks' counts).
@@ -233,24 +230,6 @@ constexpr uint32_t kSetupMiscWords = 96;
 inline uint32_t tile_threads_for(uint32_t ntiles, uint32_t cus, uint64_t prims) {
     const uint32_t per_cu = ntiles / (cus ? cus : 1u);
     return (per_cu >= 6u && prims >= 32ull * ntiles && prims < 256ull * ntiles) ? (uint32_t)kTileThreads : 512u;
-}
-
-#ifndef ZR_TILE_SPLIT_BUILD
-// Split tiles (DrawParams::tile_split) are built only on request: measured slower
-// on C2 shards (1 GPU, rank 0 of 8: tile pass 32.7 us at K = 1, 38.1 at 2, 42.1
-// at 4; with the setup overlap 74.6 vs 85.3 us per frame), because a tile's time
-// there is record-gather latency rather than raster work.
-#define ZR_TILE_SPLIT_BUILD 0
-#endif
-// k_tile workgroups per tile: the largest power of two <= 8 that keeps the pass
-// within the workgroups the CUs hold at once (4 per CU at 512 threads, 8 at 256),
-// so a pass of few tiles (tile-row shards) spreads each tile's list over K
-// workgroups instead of leaving CUs idle.
-inline uint32_t tile_split_for(uint32_t ntiles, uint32_t cus, uint32_t tile_threads) {
-    const uint64_t slots = (uint64_t)(cus ? cus : 1u) * (tile_threads >= 512u ? 4u : 8u);
-    uint32_t k = 1;
-    while (k < 8u && (uint64_t)ntiles * k * 2u <= slots) k *= 2u;
-    return k;
 }
 
 // Launchers (zr_kernels.hip).  All enqueue on `stream`; no host synchronisation.

@@ -61,11 +61,30 @@ namespace zr {
 #ifndef ZR_TILE_SUBLANE
 #define ZR_TILE_SUBLANE 1    // sparse segments: k lanes per entry split its bbox rows (0: one lane per entry)
 #endif
+#ifndef ZR_TILE_DEBUG
+#define ZR_TILE_DEBUG 0      // 1: k_tile honours the ZR_DEBUG timing switches and stamps (A/B builds only;
+                             // the checks cost the production kernel SGPRs)
+#endif
 #ifndef ZR_SETUP_LOAD_PROBE
 #define ZR_SETUP_LOAD_PROBE 0  // 1: ZR_DEBUG=16 makes phase 1 issue its loads only (timing probe)
 #endif
 
 __constant__ float c_srgbT[255] = ZR_SRGB_THRESHOLDS_INIT;
+
+// k_tile's view of DrawParams::debug: zero unless built with ZR_TILE_DEBUG.
+__device__ __forceinline__ uint32_t tile_debug(const DrawParams& P) { return ZR_TILE_DEBUG ? P.debug : 0u; }
+
+// The draw's parameters read through an opaque pointer to the kernel-argument
+// segment (every kernel here takes one DrawParams, at offset 0).  Each call starts
+// a fresh reference: fields read after it are loaded there (s_load, scalar cache)
+// instead of being hoisted to the kernel entry and held in SGPRs -- or spilled --
+// across the whole kernel.  Used at phase boundaries of the large kernels.
+typedef const __attribute__((address_space(4))) DrawParams* KernargParams;
+__device__ __forceinline__ const DrawParams& kernarg_params() {
+    KernargParams kp = (KernargParams)__builtin_amdgcn_kernarg_segment_ptr();
+    asm volatile("" : "+s"(kp));
+    return *(const DrawParams*)kp;
+}
 
 // ------------------------------------------------------------------ helpers
 
@@ -1003,7 +1022,9 @@ __global__ __launch_bounds__(kSetupThreads) void k_setup_bin(DrawParams P) {
             s_base[t] = c;
             part += c;
         }
-        if (part) atomicAdd(s_total64, part);
+#pragma unroll
+        for (int o = 32; o > 0; o >>= 1) part += __shfl_xor(part, o, 64);
+        if ((tid & 63u) == 0 && part) atomicAdd(s_total64, part);
     }
     __syncthreads();
     const bool wrapped = *s_total64 > 0xFFFFFFFFull;
@@ -1070,39 +1091,6 @@ __global__ __launch_bounds__(kSetupThreads) void k_setup_bin(DrawParams P) {
 }
 
 // ------------------------------------------------------------------- k_tile
-
-template <int PROG>
-__device__ __forceinline__ void shade_winner(const DrawParams& P, const TriRecord& r, const EdgeEvalF& e, float out[4]) {
-    if (PROG == kProgFlat) {
-        const float* c = attr_ptr(P, r.v0, 1);  // provoking vertex = first (flat)
-        out[0] = c[0]; out[1] = c[1]; out[2] = c[2]; out[3] = 1.0f;
-        return;
-    }
-    // perspective-correct weights b_i / w_i with w_i = 1 for every built-in vertex stage
-    const float pw0 = e.f0 * r.invA2, pw1 = e.f1 * r.invA2, pw2 = e.f2 * r.invA2;
-    const float inv = 1.0f / ((pw0 + pw1) + pw2);
-    const float* a0 = attr_ptr(P, r.v0, 1);
-    const float* a1 = attr_ptr(P, r.v1, 1);
-    const float* a2 = attr_ptr(P, r.v2, 1);
-    float f[3];
-#pragma unroll
-    for (int i = 0; i < 3; ++i) f[i] = ((pw0 * a0[i] + pw1 * a1[i]) + pw2 * a2[i]) * inv;
-    if (PROG == kProgTriangle) {
-        const float t3 = (P.time_ptr ? *P.time_ptr : 0.0f) * 3.0f;
-        out[0] = shade_triangle_channel(f[0], t3);
-        out[1] = shade_triangle_channel(f[1], t3);
-        out[2] = shade_triangle_channel(f[2], t3);
-        out[3] = 1.0f;
-        return;
-    }
-    const float* k0 = attr_ptr(P, r.v0, 2);
-    const float* k1 = attr_ptr(P, r.v1, 2);
-    const float* k2 = attr_ptr(P, r.v2, 2);
-    float kd[3];
-#pragma unroll
-    for (int i = 0; i < 3; ++i) kd[i] = ((pw0 * k0[i] + pw1 * k1[i]) + pw2 * k2[i]) * inv;
-    shade_blinn_phong(f[0], f[1], f[2], kd[0], kd[1], kd[2], out);
-}
 
 // T: the sRGB threshold table (LDS copy in k_tile).
 __device__ __forceinline__ void store_color(const DrawParams& P, int px, int py, bool have, const float c[4],
@@ -1259,16 +1247,20 @@ __device__ __forceinline__ void raster_lane(const DrawParams& P, const TriRecord
     const int b0 = (int)((flags >> 1) & 1u), b1 = (int)((flags >> 2) & 1u), b2 = (int)((flags >> 3) & 1u);
     // Sweep the bbox in row order, stepping the edge values: +sx per pixel, and at
     // the end of a row the jump back to the next row's first pixel, chosen with
-    // selects (no divergent branch).  The top-left bias is folded into the edge
-    // values, so coverage is one sign test; depth adds it back.  Fragment depth is
-    // never -0 here: setup canonicalised the vertex depths to +0 (the oracle's
-    // per-fragment -0 -> +0 rule therefore gives the same bits).
-    const int n = bw * ((bh - sub + k - 1) >> ksh);
+    // selects (no divergent branch: a nested row / column loop, or a wrap branch,
+    // idles the lanes of narrower primitives and measured slower).  The top-left
+    // bias is folded into the edge values, so coverage is one sign test; depth adds
+    // it back.  Fragment depth is never -0 here: setup canonicalised the vertex
+    // depths to +0 (the oracle's per-fragment -0 -> +0 rule therefore gives the
+    // same bits).  The sweep ends when the key address reaches the row after the
+    // last one (no separate step counter).
+    const int rows = (bh - sub + k - 1) >> ksh;
     const int j0 = k * sy0 - (bw - 1) * sx0, j1 = k * sy1 - (bw - 1) * sx1, j2 = k * sy2 - (bw - 1) * sx2;
     int w0 = r0 - b0, w1 = r1 - b1, w2 = r2 - b2;
     int ex = 0;
     uint32_t la = (uint32_t)(((by0 + sub - y0) * kTile + (bx0 - x0)) * 8);  // byte offset of the key
     const uint32_t lj = (uint32_t)((k * kTile - bw + 1) * 8);
+    const uint32_t la_end = la + (uint32_t)(rows * k * kTile * 8);
     // The depth-range test (fragments outside [dlo, dhi] are discarded, §3) is
     // dropped from the loop when every lane's vertex depths lie inside the range
     // by a margin far above the interpolation's rounding (a few ulp of 1): then
@@ -1276,7 +1268,7 @@ __device__ __forceinline__ void raster_lane(const DrawParams& P, const TriRecord
     const float z1v = z0 + dz1, z2v = z0 + dz2, zlo = P.dlo + 1e-4f, zhi = P.dhi - 1e-4f;
     const bool zsafe = z0 >= zlo && z0 <= zhi && z1v >= zlo && z1v <= zhi && z2v >= zlo && z2v <= zhi;
     auto sweep = [&](auto ztest) {
-        for (int q = 0; q < n; ++q) {
+        do {
             if ((w0 | w1 | w2) >= 0) {
                 const float fb1 = (float)(w1 + b1) * invA2, fb2 = (float)(w2 + b2) * invA2;
                 const float z = fmaf(fb2, dz2, fmaf(fb1, dz1, z0));
@@ -1291,7 +1283,7 @@ __device__ __forceinline__ void raster_lane(const DrawParams& P, const TriRecord
             w1 += wrap ? j1 : sx1;
             w2 += wrap ? j2 : sx2;
             la += wrap ? lj : 8u;
-        }
+        } while (la != la_end);
     };
     if (__ballot(!zsafe) == 0ull)
         sweep(std::false_type{});
@@ -1322,126 +1314,286 @@ __device__ __forceinline__ uint32_t record_prim(const DrawParams& P, uint32_t e)
     return (PROG == kProgMesh && e >= P.prims) ? (e - P.prims) >> 1 : e;
 }
 
-// mesh.slang psmain: perspective-correct barycentrics of the primitive (not of
-// its clipped fan triangle) from its homogeneous screen vertices
-// h_i = (x_i hw + w_i cx, y_i hh + w_i cy, w_i): b_i = E_i / sum E with
-// E_i = p . (h_j x h_k) at the pixel centre (the planes setup stored,
-// mesh_edge_planes); then normal and uv interpolated and lit like blinn_phong.slang with kd = (0.35 + 0.3 u, 0.35 + 0.3 v, 0.7)
-// (zr_oracle.c shade, same operation order).
-__device__ __forceinline__ void shade_mesh(const DrawParams& P, uint32_t prim, const uint32_t vid[3], int px, int py,
-                                           float out[4]) {
-    const float4* q = P.mesh_edges + (size_t)prim * 3u;
-    const float4 qa = q[0], qb = q[1], qc = q[2];
-    const float c[9] = {qa.x, qa.y, qa.z, qa.w, qb.x, qb.y, qb.z, qb.w, qc.x};
-    const float fx = (float)px + 0.5f, fy = (float)py + 0.5f;
-    float E[3];
-#pragma unroll
-    for (int i = 0; i < 3; ++i) E[i] = fmaf(c[3 * i], fx, fmaf(c[3 * i + 1], fy, c[3 * i + 2]));
-    const float einv = 1.0f / ((E[0] + E[1]) + E[2]);
-    const float b0 = E[0] * einv, b1 = E[1] * einv, b2 = E[2] * einv;
-    const float* n0 = attr_ptr(P, vid[0], 1);
-    const float* n1 = attr_ptr(P, vid[1], 1);
-    const float* n2 = attr_ptr(P, vid[2], 1);
-    const float* u0 = attr_ptr(P, vid[0], 2);
-    const float* u1 = attr_ptr(P, vid[1], 2);
-    const float* u2 = attr_ptr(P, vid[2], 2);
-    float n[3], uv[2];
-#pragma unroll
-    for (int i = 0; i < 3; ++i) n[i] = (b0 * n0[i] + b1 * n1[i]) + b2 * n2[i];
-#pragma unroll
-    for (int i = 0; i < 2; ++i) uv[i] = (b0 * u0[i] + b1 * u1[i]) + b2 * u2[i];
-    shade_blinn_phong(n[0], n[1], n[2], fmaf(uv[0], 0.3f, 0.35f), fmaf(uv[1], 0.3f, 0.35f), 0.7f, out);
+// ------------------------------------------------------------ tile resolve
+//
+// The resolve shades each pixel's winner once, but fetches each *distinct*
+// winner of the tile once (C2: ~280 winners for 1024 pixels): the pixels' winning
+// records go into an LDS hash table that hands out dense winner ids, then the
+// workgroup loads every winner's record, vertex ids and shading attributes with
+// one cooperative pass into an LDS array (AoS, WinLayout), and each pixel shades
+// from LDS.  A tile with more winners than the array holds runs it in batches.
+
+// Per-winner words in LDS, 16-B aligned records (zr_kernels.hip resolve):
+//   geometry  X0, Y0, (dx1 | dy1 << 16), (dx2 | dy2 << 16), |1/A2|   -- the compact
+//             record (vertex 1/2 in record order); a large primitive keeps dx1 ==
+//             kCompactLarge and its setup-record index in X0 (full record from HBM)
+//   depth     z0, dz1, dz2                      (last-wins modes only)
+//   attrs     flat: provoking colour (3); triangle: colour of v0..v2 (9); Blinn:
+//             normals then colours (18); mesh: barycentric planes (9), normals (9),
+//             uvs (6).  Triangle/Blinn in record order, mesh/flat in API order.
+template <int PROG, int MODE>
+struct WinLayout {
+    static constexpr bool kGeo = PROG == kProgTriangle || PROG == kProgBlinn || MODE == kDepthLastWins;
+    static constexpr bool kZ = MODE == kDepthLastWins;
+    static constexpr int kZOff = kGeo ? 5 : 0;
+    static constexpr int kAttrOff = kZOff + (kZ ? 3 : 0);
+    static constexpr int kAttrW = PROG == kProgFlat ? 3 : PROG == kProgTriangle ? 9 : PROG == kProgBlinn ? 18 : 24;
+    static constexpr int kWords = (kAttrOff + kAttrW + 3) & ~3;
+};
+
+// Resolve hash table: kWinSlots setup-record ids (kWinEmpty = free), then the
+// dense winner list (kWinSlots record ids); both live where the keys were.
+constexpr uint32_t kWinSlots = kTilePixels;
+constexpr uint32_t kWinEmpty = 0xFFFFFFFFu;
+__device__ __forceinline__ uint32_t win_hash(uint32_t rec) { return (rec * 0x9E3779B1u) >> 22; }  // 10 bits
+
+__device__ __forceinline__ void copy3(float* dst, const float* src) {
+    dst[0] = src[0]; dst[1] = src[1]; dst[2] = src[2];
 }
 
-// Vertex ids of a winning primitive; IDX32: u32 index buffer (one 12-B load).
-template <bool IDX32>
-__device__ __forceinline__ void resolve_vids(const DrawParams& P, uint32_t prim, uint32_t v[3]) {
-    if (IDX32) {
-        const uint32_t tri = tri_of(P, prim_gid(P, prim));
-        const uint3 ix = *reinterpret_cast<const uint3*>(P.ib + (uint64_t)(P.first + tri * 3u) * 4);
-        const uint32_t off = (uint32_t)P.vertex_offset;
-        v[0] = ix.x + off; v[1] = ix.y + off; v[2] = ix.z + off;
+// Loads winner `rec` (a setup record) into w[0 .. WinLayout::kWords).
+template <int PROG, int MODE, bool IDX32>
+__device__ __forceinline__ void fetch_winner(const DrawParams& P, uint32_t rec, float* w) {
+    using L = WinLayout<PROG, MODE>;
+    uint32_t v[3];
+    const uint32_t gp = record_prim<PROG>(P, rec);  // draw primitive (mesh: of the fan record)
+    {
+        const uint32_t tri = tri_of(P, prim_gid(P, gp));
+        const uint32_t e0 = P.first + tri * 3u;
+        if (IDX32) {
+            const uint3 ix = *reinterpret_cast<const uint3*>(P.ib + (uint64_t)e0 * 4);
+            const uint32_t off = (uint32_t)P.vertex_offset;  // two's complement: id + offset wraps to the valid id
+            v[0] = ix.x + off; v[1] = ix.y + off; v[2] = ix.z + off;
+        } else {
+            winner_vids(P, gp, v);
+        }
+    }
+    int4 q0 = make_int4(0, 0, 0, 0), q1 = q0;
+    if (L::kGeo) {
+        const int4* cp = reinterpret_cast<const int4*>(P.records + rec);
+        q0 = cp[0];
+        q1 = cp[1];
+    }
+    if (L::kGeo) {
+        int* wi = reinterpret_cast<int*>(w);
+        wi[0] = compact_is_large(q0) ? (int)rec : q0.x;
+        wi[1] = q0.y;
+        wi[2] = q0.z;
+        wi[3] = q0.w;
+        w[4] = fabsf(__int_as_float(q1.w));
+    }
+    if (L::kZ) {
+        w[L::kZOff + 0] = __int_as_float(q1.x);
+        w[L::kZOff + 1] = __int_as_float(q1.y);
+        w[L::kZOff + 2] = __int_as_float(q1.z);
+    }
+    float* a = w + L::kAttrOff;
+    if (PROG == kProgFlat) {
+        copy3(a, attr_ptr(P, v[0], 1));  // provoking vertex = first (flat)
+    } else if (PROG == kProgMesh) {
+        const float4* q = P.mesh_edges + (size_t)gp * 3u;
+        const float4 qa = q[0], qb = q[1], qc = q[2];
+        a[0] = qa.x; a[1] = qa.y; a[2] = qa.z; a[3] = qa.w;
+        a[4] = qb.x; a[5] = qb.y; a[6] = qb.z; a[7] = qb.w; a[8] = qc.x;
+#pragma unroll
+        for (int k = 0; k < 3; ++k) copy3(a + 9 + 3 * k, attr_ptr(P, v[k], 1));
+#pragma unroll
+        for (int k = 0; k < 3; ++k) {
+            const float* u = attr_ptr(P, v[k], 2);
+            a[18 + 2 * k] = u[0];
+            a[19 + 2 * k] = u[1];
+        }
     } else {
-        winner_vids(P, prim, v);
+        // record order: setup swapped v1 / v2 when it oriented the primitive (sign of 1/A2)
+        const bool sw = q1.w < 0;
+        const uint32_t r1 = sw ? v[2] : v[1], r2 = sw ? v[1] : v[2];
+        copy3(a + 0, attr_ptr(P, v[0], 1));
+        copy3(a + 3, attr_ptr(P, r1, 1));
+        copy3(a + 6, attr_ptr(P, r2, 1));
+        if (PROG == kProgBlinn) {
+            copy3(a + 9, attr_ptr(P, v[0], 2));
+            copy3(a + 12, attr_ptr(P, r1, 2));
+            copy3(a + 15, attr_ptr(P, r2, 2));
+        }
     }
 }
 
-// Resolve of one tile: per pixel the winning primitive is read from its key, its
-// compact record and vertex ids are gathered, its edges evaluated once and the
-// program shaded once (deferred shading); colour and depth are stored.  Two pixels
-// per batch: both pixels' record and index gathers are in flight together.
+// Colour (and for last-wins modes the depth) of pixel (px, py) from its winner's
+// LDS words; the same operations as the oracle's per-fragment shading
+// (zr_oracle.c shade), only fetched from LDS instead of the vertex buffer.
+template <int PROG, int MODE>
+__device__ __forceinline__ void shade_from_lds(const DrawParams& P, const float* w, int px, int py, float t3,
+                                               float out[4], float& zw) {
+    using L = WinLayout<PROG, MODE>;
+    TriRecord r;
+    EdgeEvalF e{0.0f, 0.0f, 0.0f};
+    if (L::kGeo) {
+        const int4 g = *reinterpret_cast<const int4*>(w);
+        const bool large = compact_is_large(g);
+        int4 q1 = make_int4(0, 0, 0, __float_as_int(w[4]));
+        if (L::kZ) {
+            q1.x = __float_as_int(w[L::kZOff + 0]);
+            q1.y = __float_as_int(w[L::kZOff + 1]);
+            q1.z = __float_as_int(w[L::kZOff + 2]);
+        }
+        r = decode_compact(P, g, q1, false);
+        if (__ballot(large)) {  // rare, wave-uniform: a winner too large for the compact form
+            if (large) r = P.records_big[g.x];
+        }
+        e = eval_edges_f(r, px, py);
+        if (L::kZ) zw = interp_depth_f(r, e.f1, e.f2);
+    }
+    const float* a = w + L::kAttrOff;
+    out[3] = 1.0f;
+    if (PROG == kProgFlat) {
+        out[0] = a[0]; out[1] = a[1]; out[2] = a[2];
+        return;
+    }
+    if (PROG == kProgMesh) {
+        // mesh.slang psmain: b_i = E_i / sum E with E_i = p . (h_j x h_k) at the pixel
+        // centre, from the planes setup stored (mesh_edge_planes); then normal and uv
+        // interpolated and lit like blinn_phong.slang, kd = (0.35 + 0.3 u, 0.35 + 0.3 v, 0.7)
+        const float fx = (float)px + 0.5f, fy = (float)py + 0.5f;
+        float E[3];
+#pragma unroll
+        for (int i = 0; i < 3; ++i) E[i] = fmaf(a[3 * i], fx, fmaf(a[3 * i + 1], fy, a[3 * i + 2]));
+        const float einv = 1.0f / ((E[0] + E[1]) + E[2]);
+        const float b0 = E[0] * einv, b1 = E[1] * einv, b2 = E[2] * einv;
+        float n[3], uv[2];
+#pragma unroll
+        for (int i = 0; i < 3; ++i) n[i] = (b0 * a[9 + i] + b1 * a[12 + i]) + b2 * a[15 + i];
+#pragma unroll
+        for (int i = 0; i < 2; ++i) uv[i] = (b0 * a[18 + i] + b1 * a[20 + i]) + b2 * a[22 + i];
+        shade_blinn_phong(n[0], n[1], n[2], fmaf(uv[0], 0.3f, 0.35f), fmaf(uv[1], 0.3f, 0.35f), 0.7f, out);
+        return;
+    }
+    // perspective-correct weights b_i / w_i with w_i = 1 for every built-in vertex stage
+    const float pw0 = e.f0 * r.invA2, pw1 = e.f1 * r.invA2, pw2 = e.f2 * r.invA2;
+    const float inv = 1.0f / ((pw0 + pw1) + pw2);
+    float f[3];
+#pragma unroll
+    for (int i = 0; i < 3; ++i) f[i] = ((pw0 * a[i] + pw1 * a[3 + i]) + pw2 * a[6 + i]) * inv;
+    if (PROG == kProgTriangle) {
+        out[0] = shade_triangle_channel(f[0], t3);
+        out[1] = shade_triangle_channel(f[1], t3);
+        out[2] = shade_triangle_channel(f[2], t3);
+        return;
+    }
+    float kd[3];
+#pragma unroll
+    for (int i = 0; i < 3; ++i) kd[i] = ((pw0 * a[9 + i] + pw1 * a[12 + i]) + pw2 * a[15 + i]) * inv;
+    shade_blinn_phong(f[0], f[1], f[2], kd[0], kd[1], kd[2], out);
+}
+
+// Resolve of one tile (after the raster phase; s_key holds the final keys).
+//   1  per pixel: key -> winning setup record; pixels no fragment won store the
+//      clear, and the key's depth is stored now (depth-writing min/max modes)
+//   2  winners into the hash table (LDS CAS); each new one gets a dense id
+//   3  per batch of <= cap winners: cooperative fetch into LDS, then every pixel
+//      whose winner is in the batch shades from LDS and stores its colour
+// s_tab: kWinSlots hash slots then kWinSlots dense-id -> record entries (the key
+// array's 8 KB, free once step 1 has read the keys); s_win: cap * kWords floats.
 template <int PROG, int MODE, bool IDX32, int NT>
-__device__ __forceinline__ void resolve_pixels(const DrawParams& P, int x0, int y0, uint32_t cnt, uint32_t fallback,
-                                               const unsigned long long* s_key, const float* s_srgb) {
+__device__ __forceinline__ void resolve_tile(const DrawParams& P, int x0, int y0, unsigned long long* s_key,
+                                             float* s_win, uint32_t cap, uint32_t* s_nwin, const float* s_srgb,
+                                             unsigned long long* ts = nullptr) {
+    using L = WinLayout<PROG, MODE>;
     constexpr int kPer = kTilePixels / NT;
-    constexpr int kB = kPer < ZR_RESOLVE_BATCH ? kPer : ZR_RESOLVE_BATCH;
     // recomputed here, not reused from the tile's init: a pixel coordinate kept
     // live across the raster loop spills at 64 VGPRs
     int tid = (int)threadIdx.x;
     asm volatile("" : "+v"(tid));
+    uint32_t rec[kPer];
+#pragma unroll
+    for (int k = 0; k < kPer; ++k) {
+        const int i = tid + k * NT;
+        const int px = x0 + (i & (kTile - 1)), py = y0 + (i >> kTileShift);
+        const bool inside = !(px < P.ra_x0 || px > P.ra_x1 || py < P.ra_y0 || py > P.ra_y1);
+        const unsigned long long key = s_key[i];
+        const uint32_t seq = inside ? winner_seq<MODE>(key) : 0u;
+        rec[k] = seq ? seq_record<PROG>(P, seq - 1u) : kWinEmpty;
+        if (!inside) continue;
+        if (!seq && P.color_bpp) {
+            const float c[4] = {0.f, 0.f, 0.f, 0.f};
+            store_color(P, px, py, false, c, s_srgb);
+        }
+        if (P.depth) {
+            float* dp = P.depth + (size_t)py * P.fb_w + px;
+            if (seq && P.depth_write_out) {
+                if (MODE != kDepthLastWins) *dp = key_depth<MODE>(key);  // last-wins: interpolated in step 3
+            } else if (P.clear_depth_enable) {
+                *dp = P.clear_depth;
+            }
+        }
+    }
+    __syncthreads();  // every key read: the key array becomes the hash table
+    uint32_t* s_tab = reinterpret_cast<uint32_t*>(s_key);
+    uint32_t* s_list = s_tab + kWinSlots;
+    for (uint32_t j = threadIdx.x; j < kWinSlots; j += NT) s_tab[j] = kWinEmpty;
+    if (threadIdx.x == 0) *s_nwin = 0u;
+    __syncthreads();
+    const uint32_t lane = threadIdx.x & 63u;
+    uint32_t hs[kPer], dnew[kPer];
+#pragma unroll
+    for (int k = 0; k < kPer; ++k) {
+        bool fresh = false;
+        uint32_t h = win_hash(rec[k]);
+        if (rec[k] != kWinEmpty) {
+            for (;;) {  // linear probing; at most kTilePixels distinct records, so it ends
+                const uint32_t old = atomicCAS(&s_tab[h], kWinEmpty, rec[k]);
+                if (old == kWinEmpty) { fresh = true; break; }
+                if (old == rec[k]) break;
+                h = (h + 1u) & (kWinSlots - 1u);
+            }
+        }
+        hs[k] = h;
+        dnew[k] = kWinEmpty;
+        const unsigned long long b = __ballot(fresh);
+        uint32_t base = 0;
+        if (lane == 0 && b) base = atomicAdd(s_nwin, (uint32_t)__popcll(b));
+        base = (uint32_t)__builtin_amdgcn_readfirstlane((int)base);
+        if (fresh) {
+            dnew[k] = base + (uint32_t)__popcll(b & ((1ull << lane) - 1ull));
+            s_list[dnew[k]] = rec[k];
+        }
+    }
+    __syncthreads();  // every insert done: the inserters replace their record ids by dense ids
+#pragma unroll
+    for (int k = 0; k < kPer; ++k)
+        if (dnew[k] != kWinEmpty) s_tab[hs[k]] = dnew[k];
+    __syncthreads();
+    uint32_t did[kPer];
+#pragma unroll
+    for (int k = 0; k < kPer; ++k) did[k] = rec[k] != kWinEmpty ? s_tab[hs[k]] : kWinEmpty;
+    __syncthreads();
+    // the table's slots now hold each pixel's dense winner id (kWinEmpty: none), so
+    // the shading loop below keeps no per-pixel state in registers
+#pragma unroll
+    for (int k = 0; k < kPer; ++k) s_tab[tid + k * NT] = did[k];
+    const uint32_t nwin = *s_nwin;
+    if (ts) ts[5] = __builtin_amdgcn_s_memrealtime();  // kDebugStamps: winners known
+    const float t3 = PROG == kProgTriangle ? (P.time_ptr ? *P.time_ptr : 0.0f) * 3.0f : 0.0f;
+    for (uint32_t base = 0; base < nwin; base += cap) {
+        const uint32_t nb = min(cap, nwin - base);
+        if (base) __syncthreads();  // the previous batch's pixels are done with s_win
+        for (uint32_t j = threadIdx.x; j < nb; j += NT)
+            fetch_winner<PROG, MODE, IDX32>(P, s_list[base + j], s_win + (size_t)j * L::kWords);
+        __syncthreads();
+        if (ts && !base) ts[6] = __builtin_amdgcn_s_memrealtime();  // first batch fetched
 #pragma unroll 1
-    for (int k0 = 0; k0 < kPer; k0 += kB) {
-        int px[kB], py[kB];
-        bool have[kB], inside[kB];
-        unsigned long long key[kB];
-        uint32_t prim[kB], gp[kB], vid[kB][3];  // setup record, draw primitive, its vertex ids
-        int4 c0[kB], c1[kB];
-#pragma unroll
-        for (int b = 0; b < kB; ++b) {
-            const int i = tid + (k0 + b) * NT;
-            px[b] = x0 + (i & (kTile - 1));
-            py[b] = y0 + (i >> kTileShift);
-            inside[b] = !(px[b] < P.ra_x0 || px[b] > P.ra_x1 || py[b] < P.ra_y0 || py[b] > P.ra_y1);
-            key[b] = s_key[i];
-            const uint32_t seq = inside[b] ? winner_seq<MODE>(key[b]) : 0u;
-            have[b] = seq != 0;
-            prim[b] = have[b] ? seq_record<PROG>(P, seq - 1u) : fallback;
-            gp[b] = have[b] ? seq_prim<PROG>(seq - 1u) : record_prim<PROG>(P, fallback);
-        }
-        float col[kB][4];
-        float zw[kB];
-        if (cnt) {
-#pragma unroll
-            for (int b = 0; b < kB; ++b) {  // gathers of the batch
-                const int4* cp = reinterpret_cast<const int4*>(P.records + prim[b]);
-                c0[b] = cp[0];
-                c1[b] = cp[1];
-                resolve_vids<IDX32>(P, gp[b], vid[b]);
-            }
-#pragma unroll
-            for (int b = 0; b < kB; ++b) {
-                TriRecord r = decode_compact(P, c0[b], c1[b], false);
-                if (__ballot(compact_is_large(c0[b]))) {  // rare, wave-uniform: a winner is a large primitive
-                    if (compact_is_large(c0[b])) r = P.records_big[prim[b]];
-                }
-                const bool sw = (r.flags & kFlagSwapped) != 0u;
-                r.v0 = vid[b][0];
-                r.v1 = sw ? vid[b][2] : vid[b][1];
-                r.v2 = sw ? vid[b][1] : vid[b][2];
-                const EdgeEvalF e = eval_edges_f(r, px[b], py[b]);
-                col[b][0] = col[b][1] = col[b][2] = col[b][3] = 0.0f;
-                if (P.color_bpp && !(P.debug & kDebugSkipShade)) {
-                    if constexpr (PROG == kProgMesh) shade_mesh(P, gp[b], vid[b], px[b], py[b], col[b]);
-                    else shade_winner<PROG>(P, r, e, col[b]);
-                }
-                zw[b] = (MODE == kDepthLastWins) ? interp_depth_f(r, e.f1, e.f2) : key_depth<MODE>(key[b]);
-            }
-        } else {
-#pragma unroll
-            for (int b = 0; b < kB; ++b) {
-                col[b][0] = col[b][1] = col[b][2] = col[b][3] = 0.0f;
-                zw[b] = 0.0f;
-            }
-        }
-#pragma unroll
-        for (int b = 0; b < kB; ++b) {
-            if (!inside[b]) continue;
-            if (P.color_bpp) store_color(P, px[b], py[b], have[b], col[b], s_srgb);
-            if (P.depth) {
-                float* dp = P.depth + (size_t)py[b] * P.fb_w + px[b];
-                if (have[b] && P.depth_write_out) *dp = zw[b];
-                else if (P.clear_depth_enable) *dp = P.clear_depth;
-            }
+        for (int k = 0; k < kPer; ++k) {
+            const int i = tid + k * NT;
+            const uint32_t dk = s_tab[i];
+            const uint32_t j = dk - base;
+            if (dk == kWinEmpty || j >= nb) continue;
+            const int px = x0 + (i & (kTile - 1)), py = y0 + (i >> kTileShift);
+            float col[4] = {0.f, 0.f, 0.f, 0.f};
+            float zw = 0.0f;
+            if (!(tile_debug(P) & kDebugSkipShade))
+                shade_from_lds<PROG, MODE>(P, s_win + (size_t)j * L::kWords, px, py, t3, col, zw);
+            if (P.color_bpp) store_color(P, px, py, true, col, s_srgb);
+            if (MODE == kDepthLastWins && P.depth && P.depth_write_out)
+                P.depth[(size_t)py * P.fb_w + px] = zw;
         }
     }
 }
@@ -1453,39 +1605,45 @@ template <int PROG, int MODE, bool INITD, int NT>
 // (launch bounds: the second argument is the minimum waves per SIMD -- 8, i.e.
 // 64 VGPRs, for both sizes; 8 x 256 or 4 x 512 threads per CU)
 __global__ __launch_bounds__(NT, ZR_TILE_WGS * kTileThreads / 256) void k_tile(DrawParams P) {
+    // LDS: a workgroup's share of the CU's 160 KiB at the occupancy the launch
+    // bounds ask for (8 x 256 or 4 x 512 threads: 20 or 40 KiB).  The keys (8 KiB)
+    // become the resolve's hash table; one union holds the raster scratch (sorted
+    // segment, wave-path queue, bucket counts, initial depths) and then the
+    // resolve's per-winner array.
+    constexpr uint32_t kWgsPerCu = (uint32_t)ZR_TILE_WGS * (uint32_t)kTileThreads / (uint32_t)NT;
+#ifdef ZR_TILE_LDS_BYTES
+    constexpr uint32_t kBudget = ZR_TILE_LDS_BYTES * 512u / NT < 160u * 1024u / kWgsPerCu
+                                     ? ZR_TILE_LDS_BYTES * 512u / NT : 160u * 1024u / kWgsPerCu;  // A/B knob
+#else
+    constexpr uint32_t kBudget = 160u * 1024u / kWgsPerCu;
+#endif
+    constexpr uint32_t kMiscWords = 16;
+    constexpr uint32_t kUnionWords = (kBudget - kTilePixels * 8u - 256u * 4u - kMiscWords * 4u) / 4u;
+    static_assert(kSortCap + kBigQueue + kSortBuckets + (INITD ? kTilePixels : 0u) <= kUnionWords,
+                  "k_tile raster scratch exceeds the workgroup's LDS share");
+    using WL = WinLayout<PROG, MODE>;
+    constexpr uint32_t kWinCap = kUnionWords / WL::kWords < kTilePixels ? kUnionWords / WL::kWords : kTilePixels;
     __shared__ unsigned long long s_key[kTilePixels];
-    __shared__ float s_initd[INITD ? kTilePixels : 1];
-    __shared__ uint32_t s_sorted[kSortCap];
-    __shared__ uint32_t s_bucket[kSortBuckets];
     __shared__ float s_srgb[256];
-    __shared__ uint32_t s_any;  // spill path: some primitive touching the tile (resolve's in-bounds fallback)
-    __shared__ uint32_t s_claim;  // next 64-entry chunk of the segment to rasterize
+    __shared__ __attribute__((aligned(16))) uint32_t s_u[kUnionWords];
+    __shared__ uint32_t s_misc[kMiscWords];
+    uint32_t* s_sorted = s_u;                       // [kSortCap]
     // wave-path primitives of the segment (large / wide), rasterized after its
     // chunks by whichever wave claims them next: the area sort groups them, so the
     // wave owning their chunk would otherwise sweep them all alone
-    __shared__ uint32_t s_big[kBigQueue];
-    __shared__ uint32_t s_nbig, s_bclaim;
-    __shared__ uint32_t s_dbg[2];  // kDebugStamps: lane-walk steps of the chunks, wave-path sweeps
-    __shared__ uint32_t s_last;  // split tiles: this workgroup arrived last and resolves
-    // Split tiles (P.tile_split = K > 1, passes with few tiles per CU): K workgroups
-    // share a tile, each rasterizing a K-th of its list into LDS keys of its own;
-    // they merge them into the tile's global keys with 64-bit atomic mins, and the
-    // last to arrive resolves.  Workgroups b with equal b % 8 take the K parts of a
-    // tile, so they usually run on one XCD (correctness never depends on it).
-    const uint32_t K = ZR_TILE_SPLIT_BUILD ? P.tile_split : 1u;
-    uint32_t t, ks = 0;
-    if (K <= 1) {
-        t = (P.debug & kDebugReverseTiles) ? P.ntiles - 1u - blockIdx.x : blockIdx.x;
-    } else {
-        const uint32_t grp = blockIdx.x / (8u * K), r = blockIdx.x - grp * 8u * K;
-        t = grp * 8u + (r & 7u);
-        ks = r >> 3;
-        if (t >= P.ntiles) return;
-    }
+    uint32_t* s_big = s_u + kSortCap;               // [kBigQueue]
+    uint32_t* s_bucket = s_big + kBigQueue;         // [kSortBuckets]
+    float* s_initd = reinterpret_cast<float*>(s_bucket + kSortBuckets);  // [kTilePixels] (INITD)
+    uint32_t& s_claim = s_misc[0];   // next 64-entry chunk of the segment to rasterize
+    uint32_t& s_nbig = s_misc[1];
+    uint32_t& s_bclaim = s_misc[2];
+    uint32_t* s_dbg = s_misc + 3;    // [2] kDebugStamps: lane-walk steps of the chunks, wave-path sweeps
+    uint32_t* s_nwin = s_misc + 5;   // resolve: distinct winners of the tile
+    const uint32_t t = (tile_debug(P) & kDebugReverseTiles) ? P.ntiles - 1u - blockIdx.x : blockIdx.x;
     const uint32_t oy = t / P.tiles_x, tx = t - oy * P.tiles_x;
     const uint32_t ty = oy * P.shard_count + P.shard_rank;
     const int x0 = (int)tx * kTile, y0 = (int)ty * kTile;
-    const bool stamp = (P.debug & kDebugStamps) && threadIdx.x == 0 && t < kMaxTilesPerPass && ks == 0;
+    const bool stamp = (tile_debug(P) & kDebugStamps) && threadIdx.x == 0 && t < kMaxTilesPerPass;
     unsigned long long* ts = P.dbg_ts + 8192 * 8 + (size_t)t * 8;
     if (stamp) ts[0] = __builtin_amdgcn_s_memrealtime();
 
@@ -1497,21 +1655,23 @@ __global__ __launch_bounds__(NT, ZR_TILE_WGS * kTileThreads / 256) void k_tile(D
     // later draws) is rasterized exactly but slowly: every tile scans all records'
     // bboxes (k_setup_bin stored them) instead of reading its list.
     const bool spill = P.tile_offsets[P.ntiles] > P.bin_capacity;
-    const uint32_t cnt_all = spill ? 0u : end - begin;
-    // this workgroup's part of the list (all of it unless split)
-    const uint32_t lbeg = begin + (uint32_t)(((uint64_t)cnt_all * ks) / max(K, 1u));
-    const uint32_t cnt = begin + (uint32_t)(((uint64_t)cnt_all * (ks + 1u)) / max(K, 1u)) - lbeg;
+    const uint32_t cnt = spill ? 0u : end - begin;
+    const uint32_t lbeg = begin;
     constexpr uint32_t kPerThread = kSortCap / NT;
     uint32_t ent[kPerThread];
     auto load_segment = [&](uint32_t seg) {
         const uint32_t n = min(kSortCap, cnt - seg);
+        // the segment's base as a uniform (scalar) pointer: lane addresses then come
+        // from threadIdx alone instead of per-lane bases held (spilled) across the pass
+        const uint32_t* bp = P.bins + lbeg + seg;
+        asm volatile("" : "+s"(bp));
 #pragma unroll
         for (uint32_t k = 0; k < kPerThread; ++k) {
             const uint32_t i = threadIdx.x + k * NT;
-            ent[k] = i < n ? P.bins[lbeg + seg + i] : 0u;  // prim | area bucket (k_setup_bin phase 4)
+            ent[k] = i < n ? bp[i] : 0u;  // prim | area bucket (k_setup_bin phase 4)
         }
     };
-    if (cnt && !(P.debug & kDebugSkipRaster)) load_segment(0);
+    if (cnt && !(tile_debug(P) & kDebugSkipRaster)) load_segment(0);
 
     for (int i = threadIdx.x; i < kTilePixels; i += NT) {
         const int px = x0 + (i & (kTile - 1)), py = y0 + (i >> kTileShift);
@@ -1521,25 +1681,24 @@ __global__ __launch_bounds__(NT, ZR_TILE_WGS * kTileThreads / 256) void k_tile(D
         if (INITD) s_initd[i] = d;
     }
     if (threadIdx.x < 255) s_srgb[threadIdx.x] = c_srgbT[threadIdx.x];
-    if (threadIdx.x == 0) s_any = 0xFFFFFFFFu;
     if (threadIdx.x < 2) s_dbg[threadIdx.x] = 0u;
     // k_setup_bin's counters back to zero for the next draw on this scratch set
     // (the tile lists live in tile_offsets / bins): each tile its own count,
     // tile 0 the grid counters, after reporting the draw's primitive stats
-    if (threadIdx.x == 0 && ks == 0) P.tile_counts[t] = 0u;
-    if (t == 0 && ks == 0 && threadIdx.x == 0) {
+    if (threadIdx.x == 0) P.tile_counts[t] = 0u;
+    if (t == 0 && threadIdx.x == 0) {
         volatile uint32_t* st = P.status;
         st[kStTrianglesSetup] = P.counters[kCtSetup];
         st[kStDroppedClip] = P.counters[kCtDropped];
     }
     __syncthreads();
-    if (t == 0 && ks == 0)
+    if (t == 0)
         for (uint32_t i = threadIdx.x; i < kCtWords; i += NT) P.counters[i] = 0u;
 
     const uint32_t wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
     const int lane = threadIdx.x & 63;
     if (stamp) ts[1] = __builtin_amdgcn_s_memrealtime();
-    if (!(P.debug & kDebugSkipRaster)) {
+    if (!(tile_debug(P) & kDebugSkipRaster)) {
         // The list is processed in segments of kSortCap entries.  Each segment is
         // counting-sorted in LDS by the primitive's bbox ∩ tile area (lane-path cost)
         // so that a 64-lane chunk holds primitives of similar cost (the lane loop runs
@@ -1548,6 +1707,7 @@ __global__ __launch_bounds__(NT, ZR_TILE_WGS * kTileThreads / 256) void k_tile(D
         for (uint32_t seg = 0; seg < cnt; seg += kSortCap) {
             const uint32_t n = min(kSortCap, cnt - seg);
             if (seg) load_segment(seg);
+            const DrawParams& P = kernarg_params();  // re-loaded per segment, not held across the pass
             if (threadIdx.x < kSortBuckets) s_bucket[threadIdx.x] = 0u;
             if (threadIdx.x == 0) s_claim = s_nbig = s_bclaim = 0u;
             __syncthreads();
@@ -1632,17 +1792,17 @@ __global__ __launch_bounds__(NT, ZR_TILE_WGS * kTileThreads / 256) void k_tile(D
                     q0 = rp[0];
                     q1 = rp[1];
                 }
-                const bool valid = j < n && !(P.debug & kDebugLoadOnly);
-                if (P.debug & kDebugLoadOnly) asm volatile("" ::"v"(q0.x), "v"(q1.x), "v"(my_prim));
+                const bool valid = j < n && !(tile_debug(P) & kDebugLoadOnly);
+                if (tile_debug(P) & kDebugLoadOnly) asm volatile("" ::"v"(q0.x), "v"(q1.x), "v"(my_prim));
                 const bool large = compact_is_large(q0);
                 // wide: bbox ∩ tile of 253+ pixels (the last sort bucket, which lumps
                 // 253..1024); one lane would walk them for up to 1024 steps
                 const bool wide = ZR_TILE_WIDE && j >= off63;
-                if (valid && !large && !wide && !(P.debug & kDebugSkipLanePath)) {
+                if (valid && !large && !wide && !(tile_debug(P) & kDebugSkipLanePath)) {
                     const TriRecord r = decode_compact(P, q0, q1, true);
                     raster_lane<MODE, INITD>(P, r, entry_seq<PROG>(P, my_prim), x0, y0, s_key, s_initd, sub, (int)ksh);
                 }
-                if (ZR_TILE_WORK_STATS && (P.debug & kDebugStamps)) {  // work of the chunk: its longest lane walk
+                if (ZR_TILE_WORK_STATS && (tile_debug(P) & kDebugStamps)) {  // work of the chunk: its longest lane walk
                     int steps = 0;
                     if (valid && !large && !wide) {
                         const TriRecord r = decode_compact(P, q0, q1, true);
@@ -1682,7 +1842,7 @@ __global__ __launch_bounds__(NT, ZR_TILE_WGS * kTileThreads / 256) void k_tile(D
                         r = decode_compact(P, a, b, true);
                     }
                     raster_prim<MODE, INITD>(P, r, entry_seq<PROG>(P, prim), x0, y0, lane, s_key, s_initd);
-                    if (ZR_TILE_WORK_STATS && (P.debug & kDebugStamps) && lane == 0) atomicAdd(&s_dbg[1], prim_sweeps(r, x0, y0));
+                    if (ZR_TILE_WORK_STATS && (tile_debug(P) & kDebugStamps) && lane == 0) atomicAdd(&s_dbg[1], prim_sweeps(r, x0, y0));
                 }
             }
             __syncthreads();
@@ -1691,7 +1851,7 @@ __global__ __launch_bounds__(NT, ZR_TILE_WGS * kTileThreads / 256) void k_tile(D
                 uint32_t i = 0;
                 if (lane == 0) i = atomicAdd(&s_bclaim, 2u);
                 i = (uint32_t)__builtin_amdgcn_readfirstlane((int)i);
-                if (i >= nbig || (P.debug & kDebugSkipWavePath)) break;
+                if (i >= nbig || (tile_debug(P) & kDebugSkipWavePath)) break;
                 const bool two = i + 1u < nbig;
                 const uint32_t e0 = s_big[i], e1 = two ? s_big[i + 1u] : e0;
                 if (!((e0 | e1) & kBigWide)) {
@@ -1722,9 +1882,7 @@ __global__ __launch_bounds__(NT, ZR_TILE_WGS * kTileThreads / 256) void k_tile(D
             __syncthreads();
         }
         if (spill) {
-            const uint32_t n_all = P.tile_offsets[P.ntiles + 1];  // setup records of the draw
-            const uint32_t r0 = (uint32_t)(((uint64_t)n_all * ks) / max(K, 1u));
-            const uint32_t n_rec = (uint32_t)(((uint64_t)n_all * (ks + 1u)) / max(K, 1u));
+            const uint32_t r0 = 0u, n_rec = P.tile_offsets[P.ntiles + 1];  // setup records of the draw
             for (uint32_t cb = r0 + wave * 64u; cb < n_rec; cb += NT) {
                 const uint32_t j = cb + (uint32_t)lane;
                 bool hit = false;
@@ -1738,7 +1896,6 @@ __global__ __launch_bounds__(NT, ZR_TILE_WGS * kTileThreads / 256) void k_tile(D
                     const int4* rp = reinterpret_cast<const int4*>(P.records + j);
                     q0 = rp[0];
                     q1 = rp[1];
-                    s_any = j;
                 }
                 const bool large = compact_is_large(q0);
                 if (hit && !large)
@@ -1757,68 +1914,49 @@ __global__ __launch_bounds__(NT, ZR_TILE_WGS * kTileThreads / 256) void k_tile(D
     }
     __syncthreads();
     if (stamp) ts[3] = __builtin_amdgcn_s_memrealtime();
-
-    uint32_t any = s_any;  // spill path: a primitive touching the tile, or ~0
-    if (K > 1) {
-        // merge into the tile's global keys: agent-scope atomics (coherent across
-        // XCDs), drained before arriving; pixels no fragment reached are skipped
-        // when every pixel starts from the clear depth
+    if (P.tile_keys) {  // resolve in k_resolve: hand the tile's keys over through HBM
         unsigned long long* gk = P.tile_keys + (size_t)t * kTilePixels;
-        const unsigned long long ik = init_key<MODE>(P.clear_depth);
-        for (int i = threadIdx.x; i < kTilePixels; i += NT) {
-            const unsigned long long k = s_key[i];
-            if (P.load_depth || k != ik)
-                __hip_atomic_fetch_min(&gk[i], k, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-        }
-        if (spill && threadIdx.x == 0 && any != 0xFFFFFFFFu)
-            __hip_atomic_fetch_min(&P.tile_any[t], any, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-        __syncthreads();
-        if (threadIdx.x == 0) {
-            const uint32_t prev = __hip_atomic_fetch_add(&P.tile_arrive[t], 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-            s_last = prev + 1u == K;
-        }
-        __syncthreads();
-        if (!s_last) return;
-        // the resolver: every part's keys, then the tile's merge state back to
-        // neutral for the next draw (~0 keys, zero arrivals)
-        for (int i = threadIdx.x; i < kTilePixels; i += NT) {
-            const unsigned long long g = __hip_atomic_load(&gk[i], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-            if (g < s_key[i]) s_key[i] = g;
-            __hip_atomic_store(&gk[i], ~0ull, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-        }
-        if (threadIdx.x == 0) {
-            __hip_atomic_store(&P.tile_arrive[t], 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-            if (spill) {
-                s_any = __hip_atomic_load(&P.tile_any[t], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-                __hip_atomic_store(&P.tile_any[t], 0xFFFFFFFFu, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-            }
-        }
-        __syncthreads();
-        any = s_any;
+        for (int i = threadIdx.x; i < kTilePixels; i += NT) gk[i] = s_key[i];
+        return;
     }
 
-    // Resolve: four pixels per thread in two batches of two (the index width is a
-    // template parameter so the batch's gathers are issued back to back).
-    uint32_t fallback = cnt_all ? (P.bins[begin] & kBinPrimMask) : 0u;  // any binned primitive: loads in bounds
-    uint32_t rcnt = cnt_all;
-    if (spill) {
-        rcnt = any != 0xFFFFFFFFu ? 1u : 0u;
-        fallback = rcnt ? any : 0u;
-    }
+    // Resolve (the index width is a template parameter so a winner's record and
+    // index loads are issued back to back).
     if (P.index_size == 4)
-        resolve_pixels<PROG, MODE, true, NT>(P, x0, y0, rcnt, fallback, s_key, s_srgb);
+        resolve_tile<PROG, MODE, true, NT>(kernarg_params(), x0, y0, s_key, reinterpret_cast<float*>(s_u), kWinCap,
+                                          s_nwin, s_srgb, stamp ? ts : nullptr);
     else
-        resolve_pixels<PROG, MODE, false, NT>(P, x0, y0, rcnt, fallback, s_key, s_srgb);
+        resolve_tile<PROG, MODE, false, NT>(kernarg_params(), x0, y0, s_key, reinterpret_cast<float*>(s_u), kWinCap,
+                                           s_nwin, s_srgb, stamp ? ts : nullptr);
     if (stamp) {
         ts[4] = __builtin_amdgcn_s_memrealtime();
-        uint32_t hw, xcc;
-        asm volatile("s_getreg_b32 %0, hwreg(HW_REG_HW_ID)" : "=s"(hw));
-        asm volatile("s_getreg_b32 %0, hwreg(HW_REG_XCC_ID)" : "=s"(xcc));
-        ts[5] = ((unsigned long long)xcc << 32) | hw;
-        ts[6] = cnt_all;
         ts[7] = ((unsigned long long)s_dbg[1] << 32) | s_dbg[0];
     }
+}
+
+// The resolve as a launch of its own (DrawParams::tile_keys set): one workgroup per
+// tile reads the keys k_tile stored and runs resolve_tile.
+template <int PROG, int MODE, int NT>
+__global__ __launch_bounds__(NT) void k_resolve(DrawParams P) {
+    constexpr uint32_t kUnionWords = (40u * 1024u - kTilePixels * 8u - 256u * 4u - 64u) / 4u;
+    using WL = WinLayout<PROG, MODE>;
+    constexpr uint32_t kWinCap = kUnionWords / WL::kWords < kTilePixels ? kUnionWords / WL::kWords : kTilePixels;
+    __shared__ unsigned long long s_key[kTilePixels];
+    __shared__ float s_srgb[256];
+    __shared__ __attribute__((aligned(16))) uint32_t s_u[kUnionWords];
+    __shared__ uint32_t s_misc[16];
+    const uint32_t t = blockIdx.x;
+    const uint32_t oy = t / P.tiles_x, tx = t - oy * P.tiles_x;
+    const uint32_t ty = oy * P.shard_count + P.shard_rank;
+    const int x0 = (int)tx * kTile, y0 = (int)ty * kTile;
+    const unsigned long long* gk = P.tile_keys + (size_t)t * kTilePixels;
+    for (int i = threadIdx.x; i < kTilePixels; i += NT) s_key[i] = gk[i];
+    if (threadIdx.x < 255) s_srgb[threadIdx.x] = c_srgbT[threadIdx.x];
+    __syncthreads();
+    if (P.index_size == 4)
+        resolve_tile<PROG, MODE, true, NT>(P, x0, y0, s_key, reinterpret_cast<float*>(s_u), kWinCap, s_misc + 5, s_srgb);
+    else
+        resolve_tile<PROG, MODE, false, NT>(P, x0, y0, s_key, reinterpret_cast<float*>(s_u), kWinCap, s_misc + 5, s_srgb);
 }
 
 __global__ __launch_bounds__(kTileThreads) void k_clear(DrawParams P) {
@@ -1890,17 +2028,20 @@ void launch_setup_bin(const DrawParams& p, void* stream) {
     }
 }
 
-// k_tile's grid: one workgroup per tile, or K per tile in groups of 8 tiles
-static inline uint32_t tile_grid(const DrawParams& p) {
-    return p.tile_split <= 1 ? p.ntiles : blocks_for(p.ntiles, 8u) * 8u * p.tile_split;
-}
-
 template <int PROG, int MODE, int NT>
 static void launch_tile_pmt(const DrawParams& p, hipStream_t s, bool initd) {
+    if (p.tile_keys) {
+        if (initd)
+            hipLaunchKernelGGL((k_tile<PROG, MODE, true, NT>), dim3(p.ntiles), dim3(NT), 0, s, p);
+        else
+            hipLaunchKernelGGL((k_tile<PROG, MODE, false, NT>), dim3(p.ntiles), dim3(NT), 0, s, p);
+        hipLaunchKernelGGL((k_resolve<PROG, MODE, 512>), dim3(p.ntiles), dim3(512), 0, s, p);
+        return;
+    }
     if (initd)
-        hipLaunchKernelGGL((k_tile<PROG, MODE, true, NT>), dim3(tile_grid(p)), dim3(NT), 0, s, p);
+        hipLaunchKernelGGL((k_tile<PROG, MODE, true, NT>), dim3(p.ntiles), dim3(NT), 0, s, p);
     else
-        hipLaunchKernelGGL((k_tile<PROG, MODE, false, NT>), dim3(tile_grid(p)), dim3(NT), 0, s, p);
+        hipLaunchKernelGGL((k_tile<PROG, MODE, false, NT>), dim3(p.ntiles), dim3(NT), 0, s, p);
 }
 
 template <int PROG, int MODE>

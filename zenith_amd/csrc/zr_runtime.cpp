@@ -193,10 +193,6 @@ struct ScratchSet {
     uint64_t tiles_cap = 0;
     uint32_t* tile_offsets = nullptr;
     uint64_t tiles_cap2 = 0;
-    unsigned long long* tile_keys = nullptr;  // split tiles (DrawParams::tile_split)
-    uint32_t* tile_arrive = nullptr;
-    uint32_t* tile_any = nullptr;
-    uint64_t split_tiles_cap = 0;
     uint32_t* counters = nullptr;
     uint64_t counters_cap = 0;
     uint32_t* bins = nullptr;
@@ -244,6 +240,9 @@ struct zr_device_t {
     bool occupancy_checked_mesh = false;
     uint32_t tile_threads = 0; // k_tile workgroup size override (ZR_TILE_NT: 256, 512; 0 = by tile count)
     uint32_t debug = 0;
+    bool split_resolve = false;           // ZR_SPLIT_RESOLVE=1 (A/B): k_resolve as its own launch
+    unsigned long long* keys = nullptr;   // its tile keys
+    uint64_t keys_cap = 0;
     uint64_t initial_bins = 0;  // 0 = max(2^20, 2 * primitives of the first draw)
     uint64_t min_bins = 0;      // bin capacity an overflow asked for
     unsigned long long* dbg_ts = nullptr;  // kDebugStamps
@@ -380,12 +379,15 @@ void dump_stamps(zr_device* d) {
             unsigned long long t1 = ~0ull;
             for (uint32_t w = 0; w < d->dbg_tiles; ++w) t1 = std::min(t1, tt[w * 8]);
             fprintf(f, "\n  tile(us from first tile start; dur = per-tile phase length):");
-            for (int i = 0; i <= 4; ++i) {
+            // t0 start, t1 init, t2 first segment sorted, t3 raster done, t5 resolve
+            // winners known, t6 first batch fetched, t4 resolve done
+            for (int i : {0, 1, 2, 3, 5, 6, 4}) {
                 double mn = 1e30, mx = 0, sum = 0, dsum = 0, dmx = 0;
                 for (uint32_t w = 0; w < d->dbg_tiles; ++w) {
                     const double v = (double)(tt[w * 8 + i] - t1) * 0.01;
                     mn = std::min(mn, v); mx = std::max(mx, v); sum += v;
-                    if (i) { const double dd = (double)(tt[w * 8 + i] - tt[w * 8 + i - 1]) * 0.01; dsum += dd; dmx = std::max(dmx, dd); }
+                    const int prev = i == 5 ? 3 : i == 6 ? 5 : i == 4 ? 6 : i - 1;
+                    if (i) { const double dd = (double)(tt[w * 8 + i] - tt[w * 8 + prev]) * 0.01; dsum += dd; dmx = std::max(dmx, dd); }
                 }
                 fprintf(f, " t%d[min %.1f avg %.1f max %.1f dur avg %.1f max %.1f]", i, mn, sum / d->dbg_tiles, mx,
                         dsum / d->dbg_tiles, dmx);
@@ -555,18 +557,6 @@ zr_result ensure_scratch(zr_device* d, ScratchSet& S, DrawParams& P) {
         if (S.tiles_cap != cap) ZR_HIP(hipMemset(S.tile_counts, 0, S.tiles_cap * 4));
     }
     if ((rc = grow(d, S.tile_offsets, S.tiles_cap2, P.ntiles + 2, 4))) return rc;
-    if (P.tile_split > 1 && (S.split_tiles_cap < P.ntiles || !S.tile_keys)) {
-        // merge state of split tiles: neutral (~0 keys, 0 arrivals, ~0 any) between
-        // draws; k_tile's resolvers put it back after every draw
-        uint64_t cap = 0, cap2 = 0, cap3 = 0;
-        if ((rc = grow(d, S.tile_keys, cap, (uint64_t)P.ntiles * kTilePixels, 8))) return rc;
-        if ((rc = grow(d, S.tile_arrive, cap2, P.ntiles, 4))) return rc;
-        if ((rc = grow(d, S.tile_any, cap3, P.ntiles, 4))) return rc;
-        ZR_HIP(hipMemset(S.tile_keys, 0xFF, cap * 8));
-        ZR_HIP(hipMemset(S.tile_arrive, 0, cap2 * 4));
-        ZR_HIP(hipMemset(S.tile_any, 0xFF, cap3 * 4));
-        S.split_tiles_cap = cap / kTilePixels;
-    }
     if (!S.counters) {  // zeroed once; k_setup_bin leaves them zero after every draw
         if ((rc = grow(d, S.counters, S.counters_cap, kCtWords, 4))) return rc;
         ZR_HIP(hipMemset(S.counters, 0, S.counters_cap * 4));
@@ -585,9 +575,6 @@ zr_result ensure_scratch(zr_device* d, ScratchSet& S, DrawParams& P) {
     P.bboxes = S.bboxes;
     P.tile_counts = S.tile_counts;
     P.tile_offsets = S.tile_offsets;
-    P.tile_keys = S.tile_keys;
-    P.tile_arrive = S.tile_arrive;
-    P.tile_any = S.tile_any;
     P.counters = S.counters;
     P.bins = S.bins;
     P.bin_capacity = (uint32_t)std::min<uint64_t>(S.bins_cap, 0xFFFFFFFFull);
@@ -772,6 +759,12 @@ zr_result exec_draw(zr_device* d, ExecState& s, const Cmd& c, bool indexed) {
     if (split) P.bbox_lds = 0;
     P.tile_threads = d->tile_threads ? d->tile_threads : tile_threads_for(P.ntiles, (uint32_t)std::max(d->cu_count, 1), prims);
     P.debug = d->debug;
+    if (d->split_resolve) {
+        uint64_t cap = d->keys_cap;
+        if ((rc = grow(d, d->keys, cap, (uint64_t)P.ntiles * kTilePixels, 8))) return rc;
+        d->keys_cap = cap;
+        P.tile_keys = d->keys;
+    }
     if (d->debug & kDebugStamps) {
         if (!d->dbg_ts) ZR_HIP(hipMalloc((void**)&d->dbg_ts, (8192 + kMaxTilesPerPass) * 8 * sizeof(unsigned long long)));
         P.dbg_ts = d->dbg_ts;
@@ -966,6 +959,7 @@ ZR_API zr_result zr_device_create(int32_t hip_device, zr_device** out) {
     if (!d) return fail(ZR_ERROR_OUT_OF_HOST_MEMORY, "device alloc");
     d->hip_device = hip_device;
     if (const char* dbg = getenv("ZR_DEBUG")) d->debug = (uint32_t)strtoul(dbg, nullptr, 0);
+    if (const char* sr = getenv("ZR_SPLIT_RESOLVE")) d->split_resolve = strtoul(sr, nullptr, 0) != 0;
     if (const char* p = getenv("ZR_DEBUG_TS")) d->dbg_ts_path = p;
     if (const char* cap = getenv("ZR_BIN_CAPACITY")) d->initial_bins = std::max<uint64_t>(64, strtoull(cap, nullptr, 0));
     if (const char* g = getenv("ZR_GRAPH")) d->use_graphs = strtoul(g, nullptr, 0) != 0;
@@ -1007,9 +1001,10 @@ ZR_API void zr_device_destroy(zr_device* d) {
     collect_timings(d);
     for (hipEvent_t e : d->event_pool) (void)hipEventDestroy(e);
     if (d->dbg_ts) (void)hipFree(d->dbg_ts);
+    if (d->keys) (void)hipFree(d->keys);
     for (ScratchSet& S : d->sets) {
         for (void* p : {(void*)S.records, (void*)S.records_big, (void*)S.mesh_edges, (void*)S.bboxes, (void*)S.tile_counts,
-                        (void*)S.tile_offsets, (void*)S.tile_keys, (void*)S.tile_arrive, (void*)S.tile_any, (void*)S.counters, (void*)S.bins, (void*)S.xsend, (void*)S.xrecv,
+                        (void*)S.tile_offsets, (void*)S.counters, (void*)S.bins, (void*)S.xsend, (void*)S.xrecv,
                         (void*)S.gids, (void*)S.rmasks, (void*)S.rcounts, (void*)S.wg_offsets})
             if (p) (void)hipFree(p);
         if (S.setup_done) (void)hipEventDestroy(S.setup_done);
