@@ -180,7 +180,6 @@ struct DrawParams {
     // tiling / sharding
     uint32_t tiles_x, tiles_y, shard_rank, shard_count, owned_rows, ntiles;
     uint32_t tile_threads;    // k_tile workgroup size: 256 or 512 (tile_threads_for)
-    unsigned long long* tile_keys;  // [ntiles][kTilePixels] (ZR_SPLIT_RESOLVE): k_tile's keys for k_resolve, or nullptr
     // partitioned setup (list mode).  In list mode `prims` is the
     // capacity of the received blocks (shard_count * span); the setup pass runs
     // over the dense positions [0, sum of the blocks' counts).

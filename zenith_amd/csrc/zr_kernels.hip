@@ -61,6 +61,9 @@ namespace zr {
 #ifndef ZR_TILE_SUBLANE
 #define ZR_TILE_SUBLANE 1    // sparse segments: k lanes per entry split its bbox rows (0: one lane per entry)
 #endif
+#ifndef ZR_LANE_PREDICATED
+#define ZR_LANE_PREDICATED 0  // A/B: lane-walk step without the coverage branch
+#endif
 #ifndef ZR_TILE_DEBUG
 #define ZR_TILE_DEBUG 0      // 1: k_tile honours the ZR_DEBUG timing switches and stamps (A/B builds only;
                              // the checks cost the production kernel SGPRs)
@@ -1269,6 +1272,16 @@ __device__ __forceinline__ void raster_lane(const DrawParams& P, const TriRecord
     const bool zsafe = z0 >= zlo && z0 <= zhi && z1v >= zlo && z1v <= zhi && z2v >= zlo && z2v <= zhi;
     auto sweep = [&](auto ztest) {
         do {
+#if ZR_LANE_PREDICATED
+            {  // branch-free step: uncovered lanes issue a no-op min (~0)
+                const float fb1 = (float)(w1 + b1) * invA2, fb2 = (float)(w2 + b2) * invA2;
+                const float z = fmaf(fb2, dz2, fmaf(fb1, dz1, z0));
+                const bool ok = ((w0 | w1 | w2) >= 0) && (!decltype(ztest)::value || (z >= P.dlo && z <= P.dhi)) &&
+                                (!INITD || depth_pass(P.depth_op, z, s_initd[la >> 3]));
+                atomicMin(reinterpret_cast<unsigned long long*>(reinterpret_cast<char*>(s_key) + la),
+                          ok ? frag_key<MODE>(z, seq) : ~0ull);
+            }
+#else
             if ((w0 | w1 | w2) >= 0) {
                 const float fb1 = (float)(w1 + b1) * invA2, fb2 = (float)(w2 + b2) * invA2;
                 const float z = fmaf(fb2, dz2, fmaf(fb1, dz1, z0));
@@ -1277,6 +1290,7 @@ __device__ __forceinline__ void raster_lane(const DrawParams& P, const TriRecord
                     atomicMin(reinterpret_cast<unsigned long long*>(reinterpret_cast<char*>(s_key) + la),
                               frag_key<MODE>(z, seq));
             }
+#endif
             const bool wrap = ++ex == bw;
             ex = wrap ? 0 : ex;
             w0 += wrap ? j0 : sx0;
@@ -1313,6 +1327,187 @@ template <int PROG>
 __device__ __forceinline__ uint32_t record_prim(const DrawParams& P, uint32_t e) {
     return (PROG == kProgMesh && e >= P.prims) ? (e - P.prims) >> 1 : e;
 }
+
+template <int PROG>
+__device__ __forceinline__ void shade_winner(const DrawParams& P, const TriRecord& r, const EdgeEvalF& e, float out[4]) {
+    if (PROG == kProgFlat) {
+        const float* c = attr_ptr(P, r.v0, 1);  // provoking vertex = first (flat)
+        out[0] = c[0]; out[1] = c[1]; out[2] = c[2]; out[3] = 1.0f;
+        return;
+    }
+    // perspective-correct weights b_i / w_i with w_i = 1 for every built-in vertex stage
+    const float pw0 = e.f0 * r.invA2, pw1 = e.f1 * r.invA2, pw2 = e.f2 * r.invA2;
+    const float inv = 1.0f / ((pw0 + pw1) + pw2);
+    const float* a0 = attr_ptr(P, r.v0, 1);
+    const float* a1 = attr_ptr(P, r.v1, 1);
+    const float* a2 = attr_ptr(P, r.v2, 1);
+    float f[3];
+#pragma unroll
+    for (int i = 0; i < 3; ++i) f[i] = ((pw0 * a0[i] + pw1 * a1[i]) + pw2 * a2[i]) * inv;
+    if (PROG == kProgTriangle) {
+        const float t3 = (P.time_ptr ? *P.time_ptr : 0.0f) * 3.0f;
+        out[0] = shade_triangle_channel(f[0], t3);
+        out[1] = shade_triangle_channel(f[1], t3);
+        out[2] = shade_triangle_channel(f[2], t3);
+        out[3] = 1.0f;
+        return;
+    }
+    const float* k0 = attr_ptr(P, r.v0, 2);
+    const float* k1 = attr_ptr(P, r.v1, 2);
+    const float* k2 = attr_ptr(P, r.v2, 2);
+    float kd[3];
+#pragma unroll
+    for (int i = 0; i < 3; ++i) kd[i] = ((pw0 * k0[i] + pw1 * k1[i]) + pw2 * k2[i]) * inv;
+    shade_blinn_phong(f[0], f[1], f[2], kd[0], kd[1], kd[2], out);
+}
+
+// mesh.slang psmain: perspective-correct barycentrics of the primitive (not of
+// its clipped fan triangle) from its homogeneous screen vertices
+// h_i = (x_i hw + w_i cx, y_i hh + w_i cy, w_i): b_i = E_i / sum E with
+// E_i = p . (h_j x h_k) at the pixel centre (the planes setup stored,
+// mesh_edge_planes); then normal and uv interpolated and lit like blinn_phong.slang with kd = (0.35 + 0.3 u, 0.35 + 0.3 v, 0.7)
+// (zr_oracle.c shade, same operation order).
+__device__ __forceinline__ void shade_mesh(const DrawParams& P, uint32_t prim, const uint32_t vid[3], int px, int py,
+                                           float out[4]) {
+    const float4* q = P.mesh_edges + (size_t)prim * 3u;
+    const float4 qa = q[0], qb = q[1], qc = q[2];
+    const float c[9] = {qa.x, qa.y, qa.z, qa.w, qb.x, qb.y, qb.z, qb.w, qc.x};
+    const float fx = (float)px + 0.5f, fy = (float)py + 0.5f;
+    float E[3];
+#pragma unroll
+    for (int i = 0; i < 3; ++i) E[i] = fmaf(c[3 * i], fx, fmaf(c[3 * i + 1], fy, c[3 * i + 2]));
+    const float einv = 1.0f / ((E[0] + E[1]) + E[2]);
+    const float b0 = E[0] * einv, b1 = E[1] * einv, b2 = E[2] * einv;
+    const float* n0 = attr_ptr(P, vid[0], 1);
+    const float* n1 = attr_ptr(P, vid[1], 1);
+    const float* n2 = attr_ptr(P, vid[2], 1);
+    const float* u0 = attr_ptr(P, vid[0], 2);
+    const float* u1 = attr_ptr(P, vid[1], 2);
+    const float* u2 = attr_ptr(P, vid[2], 2);
+    float n[3], uv[2];
+#pragma unroll
+    for (int i = 0; i < 3; ++i) n[i] = (b0 * n0[i] + b1 * n1[i]) + b2 * n2[i];
+#pragma unroll
+    for (int i = 0; i < 2; ++i) uv[i] = (b0 * u0[i] + b1 * u1[i]) + b2 * u2[i];
+    shade_blinn_phong(n[0], n[1], n[2], fmaf(uv[0], 0.3f, 0.35f), fmaf(uv[1], 0.3f, 0.35f), 0.7f, out);
+}
+
+// Vertex ids of a winning primitive; IDX32: u32 index buffer (one 12-B load).
+template <bool IDX32>
+__device__ __forceinline__ void resolve_vids(const DrawParams& P, uint32_t prim, uint32_t v[3]) {
+    if (IDX32) {
+        const uint32_t tri = tri_of(P, prim_gid(P, prim));
+        const uint3 ix = *reinterpret_cast<const uint3*>(P.ib + (uint64_t)(P.first + tri * 3u) * 4);
+        const uint32_t off = (uint32_t)P.vertex_offset;
+        v[0] = ix.x + off; v[1] = ix.y + off; v[2] = ix.z + off;
+    } else {
+        winner_vids(P, prim, v);
+    }
+}
+
+// Per-pixel resolve (512-thread tiles: two pixels per thread, one batch): per
+// pixel the winning primitive is read from its key, its compact record and vertex
+// ids are gathered, its edges evaluated once and the program shaded once
+// (deferred shading); colour and depth are stored.  The batch's gathers are in
+// flight together, and a tile's records are still L2-resident from its raster
+// phase.  Measured faster than resolve_tile at 512 threads (C2: ~78 vs 80-84 us:
+// no barriers, two dependent round trips), slower at 256 threads (4 pixels per
+// thread in two batches; C1 49 vs 44 us, C3 223 vs 204 us).  A wave with no
+// winner skips the gathers; other pixels without a winner load the wave's first
+// winner (in-bounds addresses) and discard it.
+template <int PROG, int MODE, bool IDX32, int NT>
+__device__ __forceinline__ void resolve_pixels(const DrawParams& P, int x0, int y0, const unsigned long long* s_key,
+                                               const float* s_srgb) {
+    constexpr int kPer = kTilePixels / NT;
+    constexpr int kB = kPer < ZR_RESOLVE_BATCH ? kPer : ZR_RESOLVE_BATCH;
+    // recomputed here, not reused from the tile's init: a pixel coordinate kept
+    // live across the raster loop spills at 64 VGPRs
+    int tid = (int)threadIdx.x;
+    asm volatile("" : "+v"(tid));
+#pragma unroll 1
+    for (int k0 = 0; k0 < kPer; k0 += kB) {
+        int px[kB], py[kB];
+        bool have[kB], inside[kB];
+        unsigned long long key[kB];
+        uint32_t prim[kB], gp[kB], vid[kB][3];  // setup record, draw primitive, its vertex ids
+        int4 c0[kB], c1[kB];
+#pragma unroll
+        for (int b = 0; b < kB; ++b) {
+            const int i = tid + (k0 + b) * NT;
+            px[b] = x0 + (i & (kTile - 1));
+            py[b] = y0 + (i >> kTileShift);
+            inside[b] = !(px[b] < P.ra_x0 || px[b] > P.ra_x1 || py[b] < P.ra_y0 || py[b] > P.ra_y1);
+            key[b] = s_key[i];
+            const uint32_t seq = inside[b] ? winner_seq<MODE>(key[b]) : 0u;
+            have[b] = seq != 0;
+            prim[b] = have[b] ? seq_record<PROG>(P, seq - 1u) : 0u;
+            gp[b] = have[b] ? seq_prim<PROG>(seq - 1u) : 0u;
+        }
+        unsigned long long anyw = 0;
+#pragma unroll
+        for (int b = 0; b < kB; ++b) anyw |= __ballot(have[b]);
+        if (anyw) {  // wave-uniform: some pixel of the wave has a winner, lend it to the others
+            const int src = (int)__builtin_ctzll(anyw);
+            uint32_t fb = 0, fg = 0;
+#pragma unroll
+            for (int b = 0; b < kB; ++b) {
+                const unsigned long long hb = __ballot(have[b]);
+                const uint32_t pb = (uint32_t)__builtin_amdgcn_readlane((int)prim[b], src);
+                const uint32_t gb = (uint32_t)__builtin_amdgcn_readlane((int)gp[b], src);
+                if (!fb && ((hb >> src) & 1ull)) { fb = pb + 1u; fg = gb; }
+            }
+#pragma unroll
+            for (int b = 0; b < kB; ++b)
+                if (!have[b]) { prim[b] = fb - 1u; gp[b] = fg; }
+        }
+        float col[kB][4];
+        float zw[kB];
+        if (anyw) {
+#pragma unroll
+            for (int b = 0; b < kB; ++b) {  // gathers of the batch
+                const int4* cp = reinterpret_cast<const int4*>(P.records + prim[b]);
+                c0[b] = cp[0];
+                c1[b] = cp[1];
+                resolve_vids<IDX32>(P, gp[b], vid[b]);
+            }
+#pragma unroll
+            for (int b = 0; b < kB; ++b) {
+                TriRecord r = decode_compact(P, c0[b], c1[b], false);
+                if (__ballot(compact_is_large(c0[b]))) {  // rare, wave-uniform: a winner is a large primitive
+                    if (compact_is_large(c0[b])) r = P.records_big[prim[b]];
+                }
+                const bool sw = (r.flags & kFlagSwapped) != 0u;
+                r.v0 = vid[b][0];
+                r.v1 = sw ? vid[b][2] : vid[b][1];
+                r.v2 = sw ? vid[b][1] : vid[b][2];
+                const EdgeEvalF e = eval_edges_f(r, px[b], py[b]);
+                col[b][0] = col[b][1] = col[b][2] = col[b][3] = 0.0f;
+                if (P.color_bpp && !(tile_debug(P) & kDebugSkipShade)) {
+                    if constexpr (PROG == kProgMesh) shade_mesh(P, gp[b], vid[b], px[b], py[b], col[b]);
+                    else shade_winner<PROG>(P, r, e, col[b]);
+                }
+                zw[b] = (MODE == kDepthLastWins) ? interp_depth_f(r, e.f1, e.f2) : key_depth<MODE>(key[b]);
+            }
+        } else {
+#pragma unroll
+            for (int b = 0; b < kB; ++b) {
+                col[b][0] = col[b][1] = col[b][2] = col[b][3] = 0.0f;
+                zw[b] = 0.0f;
+            }
+        }
+#pragma unroll
+        for (int b = 0; b < kB; ++b) {
+            if (!inside[b]) continue;
+            if (P.color_bpp) store_color(P, px[b], py[b], have[b], col[b], s_srgb);
+            if (P.depth) {
+                float* dp = P.depth + (size_t)py[b] * P.fb_w + px[b];
+                if (have[b] && P.depth_write_out) *dp = zw[b];
+                else if (P.clear_depth_enable) *dp = P.clear_depth;
+            }
+        }
+    }
+}
+
 
 // ------------------------------------------------------------ tile resolve
 //
@@ -1487,18 +1682,29 @@ __device__ __forceinline__ void shade_from_lds(const DrawParams& P, const float*
 
 // Resolve of one tile (after the raster phase; s_key holds the final keys).
 //   1  per pixel: key -> winning setup record; pixels no fragment won store the
-//      clear, and the key's depth is stored now (depth-writing min/max modes)
-//   2  winners into the hash table (LDS CAS); each new one gets a dense id
+//      clear, and the key's depth is stored now (depth-writing min/max modes).
+//      The key array's upper half becomes the hash table: each thread empties the
+//      slots lying over the keys it owns (so no barrier is needed before that).
+//   2  winners into the hash table (LDS CAS, linear probing); the inserting lane
+//      takes a dense id (one LDS add per wave) and records it beside the slot and
+//      the winner in the dense list (the key array's lower half)
 //   3  per batch of <= cap winners: cooperative fetch into LDS, then every pixel
 //      whose winner is in the batch shades from LDS and stores its colour
-// s_tab: kWinSlots hash slots then kWinSlots dense-id -> record entries (the key
-// array's 8 KB, free once step 1 has read the keys); s_win: cap * kWords floats.
+// Three barriers in all.  s_u: the dense-id map (u16 per slot), then (kPer > 2)
+// each pixel's dense id (u16), then the per-winner words (cap * kWords floats).
 template <int PROG, int MODE, bool IDX32, int NT>
 __device__ __forceinline__ void resolve_tile(const DrawParams& P, int x0, int y0, unsigned long long* s_key,
-                                             float* s_win, uint32_t cap, uint32_t* s_nwin, const float* s_srgb,
-                                             unsigned long long* ts = nullptr) {
+                                             uint32_t* s_u, uint32_t u_words, uint32_t* s_nwin,
+                                             const float* s_srgb, unsigned long long* ts = nullptr) {
     using L = WinLayout<PROG, MODE>;
     constexpr int kPer = kTilePixels / NT;
+    constexpr bool kPixLds = kPer > 2;  // per-pixel ids in LDS (registers at 512 threads)
+    uint32_t* s_list = reinterpret_cast<uint32_t*>(s_key);              // [kWinSlots] over keys 0..511
+    uint32_t* s_tab = s_list + kWinSlots;                               // [kWinSlots] over keys 512..1023
+    uint16_t* s_dmap = reinterpret_cast<uint16_t*>(s_u);                // [kWinSlots]
+    uint32_t* s_pix = s_tab;  // [kTilePixels] (kPixLds): the table is free once every dense id is known
+    float* s_win = reinterpret_cast<float*>(s_u + kWinSlots / 2u);
+    const uint32_t cap = min((u_words - kWinSlots / 2u) / (uint32_t)L::kWords, kWinSlots);
     // recomputed here, not reused from the tile's init: a pixel coordinate kept
     // live across the raster loop spills at 64 VGPRs
     int tid = (int)threadIdx.x;
@@ -1510,6 +1716,10 @@ __device__ __forceinline__ void resolve_tile(const DrawParams& P, int x0, int y0
         const int px = x0 + (i & (kTile - 1)), py = y0 + (i >> kTileShift);
         const bool inside = !(px < P.ra_x0 || px > P.ra_x1 || py < P.ra_y0 || py > P.ra_y1);
         const unsigned long long key = s_key[i];
+        if (i >= (int)(kTilePixels / 2)) {  // this key's bytes hold hash slots 2(i - 512) and 2(i - 512) + 1
+            s_tab[2 * (i - kTilePixels / 2)] = kWinEmpty;
+            s_tab[2 * (i - kTilePixels / 2) + 1] = kWinEmpty;
+        }
         const uint32_t seq = inside ? winner_seq<MODE>(key) : 0u;
         rec[k] = seq ? seq_record<PROG>(P, seq - 1u) : kWinEmpty;
         if (!inside) continue;
@@ -1526,14 +1736,10 @@ __device__ __forceinline__ void resolve_tile(const DrawParams& P, int x0, int y0
             }
         }
     }
-    __syncthreads();  // every key read: the key array becomes the hash table
-    uint32_t* s_tab = reinterpret_cast<uint32_t*>(s_key);
-    uint32_t* s_list = s_tab + kWinSlots;
-    for (uint32_t j = threadIdx.x; j < kWinSlots; j += NT) s_tab[j] = kWinEmpty;
     if (threadIdx.x == 0) *s_nwin = 0u;
-    __syncthreads();
+    __syncthreads();  // every key read, every slot empty
     const uint32_t lane = threadIdx.x & 63u;
-    uint32_t hs[kPer], dnew[kPer];
+    uint32_t hs[kPer];
 #pragma unroll
     for (int k = 0; k < kPer; ++k) {
         bool fresh = false;
@@ -1547,29 +1753,27 @@ __device__ __forceinline__ void resolve_tile(const DrawParams& P, int x0, int y0
             }
         }
         hs[k] = h;
-        dnew[k] = kWinEmpty;
         const unsigned long long b = __ballot(fresh);
         uint32_t base = 0;
         if (lane == 0 && b) base = atomicAdd(s_nwin, (uint32_t)__popcll(b));
         base = (uint32_t)__builtin_amdgcn_readfirstlane((int)base);
         if (fresh) {
-            dnew[k] = base + (uint32_t)__popcll(b & ((1ull << lane) - 1ull));
-            s_list[dnew[k]] = rec[k];
+            const uint32_t d = base + (uint32_t)__popcll(b & ((1ull << lane) - 1ull));
+            s_list[d] = rec[k];
+            s_dmap[h] = (uint16_t)d;
         }
     }
-    __syncthreads();  // every insert done: the inserters replace their record ids by dense ids
-#pragma unroll
-    for (int k = 0; k < kPer; ++k)
-        if (dnew[k] != kWinEmpty) s_tab[hs[k]] = dnew[k];
-    __syncthreads();
+    __syncthreads();  // every winner has its dense id
     uint32_t did[kPer];
 #pragma unroll
-    for (int k = 0; k < kPer; ++k) did[k] = rec[k] != kWinEmpty ? s_tab[hs[k]] : kWinEmpty;
-    __syncthreads();
-    // the table's slots now hold each pixel's dense winner id (kWinEmpty: none), so
-    // the shading loop below keeps no per-pixel state in registers
+    for (int k = 0; k < kPer; ++k) {
+        did[k] = rec[k] != kWinEmpty ? (uint32_t)s_dmap[hs[k]] : kWinEmpty;
+    }
+    if (kPixLds) {
+        __syncthreads();  // every lookup of the table done before it holds pixel ids
 #pragma unroll
-    for (int k = 0; k < kPer; ++k) s_tab[tid + k * NT] = did[k];
+        for (int k = 0; k < kPer; ++k) s_pix[tid + k * NT] = did[k];  // read back by this thread only
+    }
     const uint32_t nwin = *s_nwin;
     if (ts) ts[5] = __builtin_amdgcn_s_memrealtime();  // kDebugStamps: winners known
     const float t3 = PROG == kProgTriangle ? (P.time_ptr ? *P.time_ptr : 0.0f) * 3.0f : 0.0f;
@@ -1580,20 +1784,24 @@ __device__ __forceinline__ void resolve_tile(const DrawParams& P, int x0, int y0
             fetch_winner<PROG, MODE, IDX32>(P, s_list[base + j], s_win + (size_t)j * L::kWords);
         __syncthreads();
         if (ts && !base) ts[6] = __builtin_amdgcn_s_memrealtime();  // first batch fetched
-#pragma unroll 1
-        for (int k = 0; k < kPer; ++k) {
-            const int i = tid + k * NT;
-            const uint32_t dk = s_tab[i];
+        auto shade_pixel = [&](int k, uint32_t dk) {
             const uint32_t j = dk - base;
-            if (dk == kWinEmpty || j >= nb) continue;
+            if (dk == kWinEmpty || j >= nb) return;
+            const int i = tid + k * NT;
             const int px = x0 + (i & (kTile - 1)), py = y0 + (i >> kTileShift);
             float col[4] = {0.f, 0.f, 0.f, 0.f};
             float zw = 0.0f;
             if (!(tile_debug(P) & kDebugSkipShade))
                 shade_from_lds<PROG, MODE>(P, s_win + (size_t)j * L::kWords, px, py, t3, col, zw);
             if (P.color_bpp) store_color(P, px, py, true, col, s_srgb);
-            if (MODE == kDepthLastWins && P.depth && P.depth_write_out)
-                P.depth[(size_t)py * P.fb_w + px] = zw;
+            if (MODE == kDepthLastWins && P.depth && P.depth_write_out) P.depth[(size_t)py * P.fb_w + px] = zw;
+        };
+        if (kPixLds) {
+#pragma unroll 1
+            for (int k = 0; k < kPer; ++k) shade_pixel(k, s_pix[tid + k * NT]);
+        } else {
+#pragma unroll
+            for (int k = 0; k < kPer; ++k) shade_pixel(k, did[k]);
         }
     }
 }
@@ -1621,8 +1829,6 @@ __global__ __launch_bounds__(NT, ZR_TILE_WGS * kTileThreads / 256) void k_tile(D
     constexpr uint32_t kUnionWords = (kBudget - kTilePixels * 8u - 256u * 4u - kMiscWords * 4u) / 4u;
     static_assert(kSortCap + kBigQueue + kSortBuckets + (INITD ? kTilePixels : 0u) <= kUnionWords,
                   "k_tile raster scratch exceeds the workgroup's LDS share");
-    using WL = WinLayout<PROG, MODE>;
-    constexpr uint32_t kWinCap = kUnionWords / WL::kWords < kTilePixels ? kUnionWords / WL::kWords : kTilePixels;
     __shared__ unsigned long long s_key[kTilePixels];
     __shared__ float s_srgb[256];
     __shared__ __attribute__((aligned(16))) uint32_t s_u[kUnionWords];
@@ -1914,49 +2120,25 @@ __global__ __launch_bounds__(NT, ZR_TILE_WGS * kTileThreads / 256) void k_tile(D
     }
     __syncthreads();
     if (stamp) ts[3] = __builtin_amdgcn_s_memrealtime();
-    if (P.tile_keys) {  // resolve in k_resolve: hand the tile's keys over through HBM
-        unsigned long long* gk = P.tile_keys + (size_t)t * kTilePixels;
-        for (int i = threadIdx.x; i < kTilePixels; i += NT) gk[i] = s_key[i];
-        return;
-    }
 
     // Resolve (the index width is a template parameter so a winner's record and
     // index loads are issued back to back).
-    if (P.index_size == 4)
-        resolve_tile<PROG, MODE, true, NT>(kernarg_params(), x0, y0, s_key, reinterpret_cast<float*>(s_u), kWinCap,
-                                          s_nwin, s_srgb, stamp ? ts : nullptr);
-    else
-        resolve_tile<PROG, MODE, false, NT>(kernarg_params(), x0, y0, s_key, reinterpret_cast<float*>(s_u), kWinCap,
-                                           s_nwin, s_srgb, stamp ? ts : nullptr);
+    if (NT >= 512) {
+        if (P.index_size == 4)
+            resolve_pixels<PROG, MODE, true, NT>(kernarg_params(), x0, y0, s_key, s_srgb);
+        else
+            resolve_pixels<PROG, MODE, false, NT>(kernarg_params(), x0, y0, s_key, s_srgb);
+    } else if (P.index_size == 4) {
+        resolve_tile<PROG, MODE, true, NT>(kernarg_params(), x0, y0, s_key, s_u, kUnionWords, s_nwin, s_srgb,
+                                          stamp ? ts : nullptr);
+    } else {
+        resolve_tile<PROG, MODE, false, NT>(kernarg_params(), x0, y0, s_key, s_u, kUnionWords, s_nwin, s_srgb,
+                                           stamp ? ts : nullptr);
+    }
     if (stamp) {
         ts[4] = __builtin_amdgcn_s_memrealtime();
         ts[7] = ((unsigned long long)s_dbg[1] << 32) | s_dbg[0];
     }
-}
-
-// The resolve as a launch of its own (DrawParams::tile_keys set): one workgroup per
-// tile reads the keys k_tile stored and runs resolve_tile.
-template <int PROG, int MODE, int NT>
-__global__ __launch_bounds__(NT) void k_resolve(DrawParams P) {
-    constexpr uint32_t kUnionWords = (40u * 1024u - kTilePixels * 8u - 256u * 4u - 64u) / 4u;
-    using WL = WinLayout<PROG, MODE>;
-    constexpr uint32_t kWinCap = kUnionWords / WL::kWords < kTilePixels ? kUnionWords / WL::kWords : kTilePixels;
-    __shared__ unsigned long long s_key[kTilePixels];
-    __shared__ float s_srgb[256];
-    __shared__ __attribute__((aligned(16))) uint32_t s_u[kUnionWords];
-    __shared__ uint32_t s_misc[16];
-    const uint32_t t = blockIdx.x;
-    const uint32_t oy = t / P.tiles_x, tx = t - oy * P.tiles_x;
-    const uint32_t ty = oy * P.shard_count + P.shard_rank;
-    const int x0 = (int)tx * kTile, y0 = (int)ty * kTile;
-    const unsigned long long* gk = P.tile_keys + (size_t)t * kTilePixels;
-    for (int i = threadIdx.x; i < kTilePixels; i += NT) s_key[i] = gk[i];
-    if (threadIdx.x < 255) s_srgb[threadIdx.x] = c_srgbT[threadIdx.x];
-    __syncthreads();
-    if (P.index_size == 4)
-        resolve_tile<PROG, MODE, true, NT>(P, x0, y0, s_key, reinterpret_cast<float*>(s_u), kWinCap, s_misc + 5, s_srgb);
-    else
-        resolve_tile<PROG, MODE, false, NT>(P, x0, y0, s_key, reinterpret_cast<float*>(s_u), kWinCap, s_misc + 5, s_srgb);
 }
 
 __global__ __launch_bounds__(kTileThreads) void k_clear(DrawParams P) {
@@ -2030,14 +2212,6 @@ void launch_setup_bin(const DrawParams& p, void* stream) {
 
 template <int PROG, int MODE, int NT>
 static void launch_tile_pmt(const DrawParams& p, hipStream_t s, bool initd) {
-    if (p.tile_keys) {
-        if (initd)
-            hipLaunchKernelGGL((k_tile<PROG, MODE, true, NT>), dim3(p.ntiles), dim3(NT), 0, s, p);
-        else
-            hipLaunchKernelGGL((k_tile<PROG, MODE, false, NT>), dim3(p.ntiles), dim3(NT), 0, s, p);
-        hipLaunchKernelGGL((k_resolve<PROG, MODE, 512>), dim3(p.ntiles), dim3(512), 0, s, p);
-        return;
-    }
     if (initd)
         hipLaunchKernelGGL((k_tile<PROG, MODE, true, NT>), dim3(p.ntiles), dim3(NT), 0, s, p);
     else

@@ -240,9 +240,6 @@ struct zr_device_t {
     bool occupancy_checked_mesh = false;
     uint32_t tile_threads = 0; // k_tile workgroup size override (ZR_TILE_NT: 256, 512; 0 = by tile count)
     uint32_t debug = 0;
-    bool split_resolve = false;           // ZR_SPLIT_RESOLVE=1 (A/B): k_resolve as its own launch
-    unsigned long long* keys = nullptr;   // its tile keys
-    uint64_t keys_cap = 0;
     uint64_t initial_bins = 0;  // 0 = max(2^20, 2 * primitives of the first draw)
     uint64_t min_bins = 0;      // bin capacity an overflow asked for
     unsigned long long* dbg_ts = nullptr;  // kDebugStamps
@@ -759,12 +756,6 @@ zr_result exec_draw(zr_device* d, ExecState& s, const Cmd& c, bool indexed) {
     if (split) P.bbox_lds = 0;
     P.tile_threads = d->tile_threads ? d->tile_threads : tile_threads_for(P.ntiles, (uint32_t)std::max(d->cu_count, 1), prims);
     P.debug = d->debug;
-    if (d->split_resolve) {
-        uint64_t cap = d->keys_cap;
-        if ((rc = grow(d, d->keys, cap, (uint64_t)P.ntiles * kTilePixels, 8))) return rc;
-        d->keys_cap = cap;
-        P.tile_keys = d->keys;
-    }
     if (d->debug & kDebugStamps) {
         if (!d->dbg_ts) ZR_HIP(hipMalloc((void**)&d->dbg_ts, (8192 + kMaxTilesPerPass) * 8 * sizeof(unsigned long long)));
         P.dbg_ts = d->dbg_ts;
@@ -959,7 +950,6 @@ ZR_API zr_result zr_device_create(int32_t hip_device, zr_device** out) {
     if (!d) return fail(ZR_ERROR_OUT_OF_HOST_MEMORY, "device alloc");
     d->hip_device = hip_device;
     if (const char* dbg = getenv("ZR_DEBUG")) d->debug = (uint32_t)strtoul(dbg, nullptr, 0);
-    if (const char* sr = getenv("ZR_SPLIT_RESOLVE")) d->split_resolve = strtoul(sr, nullptr, 0) != 0;
     if (const char* p = getenv("ZR_DEBUG_TS")) d->dbg_ts_path = p;
     if (const char* cap = getenv("ZR_BIN_CAPACITY")) d->initial_bins = std::max<uint64_t>(64, strtoull(cap, nullptr, 0));
     if (const char* g = getenv("ZR_GRAPH")) d->use_graphs = strtoul(g, nullptr, 0) != 0;
@@ -1001,7 +991,6 @@ ZR_API void zr_device_destroy(zr_device* d) {
     collect_timings(d);
     for (hipEvent_t e : d->event_pool) (void)hipEventDestroy(e);
     if (d->dbg_ts) (void)hipFree(d->dbg_ts);
-    if (d->keys) (void)hipFree(d->keys);
     for (ScratchSet& S : d->sets) {
         for (void* p : {(void*)S.records, (void*)S.records_big, (void*)S.mesh_edges, (void*)S.bboxes, (void*)S.tile_counts,
                         (void*)S.tile_offsets, (void*)S.counters, (void*)S.bins, (void*)S.xsend, (void*)S.xrecv,
