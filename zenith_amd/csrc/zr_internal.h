@@ -205,7 +205,6 @@ struct DrawParams {
     uint32_t unit_shift;      // log2 primitives per claim unit (64 lanes * batch * rounds)
     uint32_t units;           // claim units of the draw: ceil(prims / unit size)
     uint32_t setup_batch;     // primitives per lane in flight (template instance of k_setup_bin)
-    uint32_t setup_sched;     // unit schedule: 0 contiguous per workgroup, 1 interleaved (u % G)
     uint32_t bbox_lds;        // 0: bboxes in global memory; else LDS entries per workgroup (own units * unit size)
     uint32_t* wg_offsets;     // split setup: [setup_wgs][ntiles] each workgroup's offsets in the tile lists
     uint32_t debug;           // kDebug* bits (timing experiments only)
