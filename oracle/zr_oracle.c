@@ -404,6 +404,35 @@ static void interp3(const float *f0, const float *f1, const float *f2, const flo
     for (int i = 0; i < 3; ++i) out[i] = ((pw[0] * f0[i] + pw[1] * f1[i]) + pw[2] * f2[i]) * inv;
 }
 
+/* mesh.slang barycentric planes E_i(p) = p . (h_j x h_k) of the primitive's
+ * homogeneous screen vertices h = (x hw + w cx, y hh + w cy, w).
+ * The plane constants are formed in double, relative to a reference pixel r =
+ * floor(vertex 0's screen position) (clamped to the guard band), and rounded
+ * once to float: E_i = c0 (px - rx) + c1 (py - ry) + c2r, c2r = E_i at r's
+ * centre.  Evaluated per fragment in float with two fmaf. */
+static void mesh_planes_eval(const zro_draw_state *s, const float clip[3][4], int32_t px, int32_t py, float E[3]) {
+    const float hw = s->viewport[2] * 0.5f, hh = s->viewport[3] * 0.5f;
+    const float cx = s->viewport[0] + hw, cy = s->viewport[1] + hh;
+    double hX[3], hY[3], hW[3];
+    for (int k = 0; k < 3; ++k) {
+        hX[k] = (double)clip[k][0] * (double)hw + (double)clip[k][3] * (double)cx;
+        hY[k] = (double)clip[k][1] * (double)hh + (double)clip[k][3] * (double)cy;
+        hW[k] = (double)clip[k][3];
+    }
+    double rx = hW[0] > 0.0 ? floor(hX[0] / hW[0]) : 0.0, ry = hW[0] > 0.0 ? floor(hY[0] / hW[0]) : 0.0;
+    rx = fmin(fmax(rx, -4194304.0), 4194304.0);
+    ry = fmin(fmax(ry, -4194304.0), 4194304.0);
+    const float dx = (float)px - (float)rx, dy = (float)py - (float)ry;
+    for (int i = 0; i < 3; ++i) {
+        const int j = (i + 1) % 3, k = (i + 2) % 3;
+        const double c0 = hY[j] * hW[k] - hW[j] * hY[k];
+        const double c1 = hW[j] * hX[k] - hX[j] * hW[k];
+        const double c2 = hX[j] * hY[k] - hY[j] * hX[k];
+        const float c2r = (float)((c0 * (rx + 0.5) + c1 * (ry + 0.5)) + c2);
+        E[i] = fmaf((float)c0, dx, fmaf((float)c1, dy, c2r));
+    }
+}
+
 /* blinn_phong.slang / mesh.slang lighting: ks = 0.5, n = 32, ambient 0.05 */
 static void blinn_phong(const float n[3], const float kd[3], float out[4]) {
     static const float L[3] = {0x1.3651a0p-2f, 0x1.02995cp-1f, 0x1.9dc22cp-1f}; /* norm(.3,.5,.8) */
@@ -450,23 +479,8 @@ static void shade(const zro_draw_state *s, const zro_vertex_input *vi, const tri
          * its clipped fan triangle) from its homogeneous screen vertices
          * h_i = (x_i*hw + w_i*cx, y_i*hh + w_i*cy, w_i): b_i = E_i / sum E, with
          * E_i = p . (h_j x h_k) at the pixel centre p = (px + .5, py + .5, 1). */
-        const float hw = s->viewport[2] * 0.5f, hh = s->viewport[3] * 0.5f;
-        const float cx = s->viewport[0] + hw, cy = s->viewport[1] + hh;
-        float hX[3], hY[3], hW[3];
-        for (int k = 0; k < 3; ++k) {
-            hX[k] = fmaf(o->clip[k][0], hw, o->clip[k][3] * cx);
-            hY[k] = fmaf(o->clip[k][1], hh, o->clip[k][3] * cy);
-            hW[k] = o->clip[k][3];
-        }
-        const float fx = (float)pxl + 0.5f, fy = (float)pyl + 0.5f;
         float E[3];
-        for (int i = 0; i < 3; ++i) {
-            const int j = (i + 1) % 3, k = (i + 2) % 3;
-            const float c0 = hY[j] * hW[k] - hW[j] * hY[k];
-            const float c1 = hW[j] * hX[k] - hX[j] * hW[k];
-            const float c2 = hX[j] * hY[k] - hY[j] * hX[k];
-            E[i] = fmaf(c0, fx, fmaf(c1, fy, c2));
-        }
+        mesh_planes_eval(s, o->clip, pxl, pyl, E);
         const float einv = 1.0f / ((E[0] + E[1]) + E[2]);
         const float bb[3] = {E[0] * einv, E[1] * einv, E[2] * einv};
         float nrm[3], uv[2];

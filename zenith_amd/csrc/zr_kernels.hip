@@ -576,28 +576,50 @@ __device__ __forceinline__ BBox write_record(const DrawParams& P, uint32_t rec, 
     return box;
 }
 
-// The mesh program's barycentric planes: with the homogeneous screen vertices
-// h_i = (x_i hw + w_i cx, y_i hh + w_i cy, w_i) of the primitive (not of its
-// clipped fans), E_i(p) = p . (h_j x h_k) = c0 fx + c1 fy + c2; e[3 i + n] = c_n
-// (zr_oracle.c shade, same operations).  Stored once per primitive by setup so the
-// resolve neither re-reads positions nor re-runs the vertex stage per pixel.
-__device__ __forceinline__ void mesh_edge_planes(const DrawParams& P, const float3 p[3], float e[9]) {
-    float hX[3], hY[3], hW[3];
+// The mesh program's barycentric planes: with the homogeneous
+// screen vertices h_i = (x_i hw + w_i cx, y_i hh + w_i cy, w_i) of the primitive
+// (not of its clipped fans), E_i(p) = p . (h_j x h_k) = c0 fx + c1 fy + c2.
+// Evaluated relative to a reference pixel r near the primitive (r = floor of
+// vertex 0's screen position), E_i = c0 (px - rx) + c1 (py - ry) + c2r with c2r
+// = E_i at r's centre: the plane constants are formed in double and rounded once,
+// so the resolve's float32 evaluation has no cancellation between large terms.
+// e = {c0_0, c1_0, c2r_0, c0_1, c1_1, c2r_1, c0_2, c1_2, c2r_2, rx, ry, 0}
+// (zr_oracle.c mesh_planes, same operations).
+__device__ __forceinline__ void mesh_edge_planes(const DrawParams& P, const float3 p[3], float e[12]) {
+    double hX[3], hY[3], hW[3];
 #pragma unroll
     for (int k = 0; k < 3; ++k) {
         float c[4];
         mesh_transform(P.view_proj, p[k], c);
-        hX[k] = fmaf(c[0], P.hw, c[3] * P.cx);
-        hY[k] = fmaf(c[1], P.hh, c[3] * P.cy);
-        hW[k] = c[3];
+        hX[k] = (double)c[0] * (double)P.hw + (double)c[3] * (double)P.cx;
+        hY[k] = (double)c[1] * (double)P.hh + (double)c[3] * (double)P.cy;
+        hW[k] = (double)c[3];
     }
+    // (a primitive reaching here has w > 0 at vertex 0 unless it was clipped; the
+    // reference pixel only has to be finite: clamped to the guard band)
+    double rx = hW[0] > 0.0 ? floor(hX[0] / hW[0]) : 0.0, ry = hW[0] > 0.0 ? floor(hY[0] / hW[0]) : 0.0;
+    rx = fmin(fmax(rx, -4194304.0), 4194304.0);
+    ry = fmin(fmax(ry, -4194304.0), 4194304.0);
 #pragma unroll
     for (int i = 0; i < 3; ++i) {
         const int j = (i + 1) % 3, k = (i + 2) % 3;
-        e[3 * i + 0] = hY[j] * hW[k] - hW[j] * hY[k];
-        e[3 * i + 1] = hW[j] * hX[k] - hX[j] * hW[k];
-        e[3 * i + 2] = hX[j] * hY[k] - hY[j] * hX[k];
+        const double c0 = hY[j] * hW[k] - hW[j] * hY[k];
+        const double c1 = hW[j] * hX[k] - hX[j] * hW[k];
+        const double c2 = hX[j] * hY[k] - hY[j] * hX[k];
+        e[3 * i + 0] = (float)c0;
+        e[3 * i + 1] = (float)c1;
+        e[3 * i + 2] = (float)((c0 * (rx + 0.5) + c1 * (ry + 0.5)) + c2);
     }
+    e[9] = (float)rx;
+    e[10] = (float)ry;
+    e[11] = 0.0f;
+}
+
+// E_i of pixel (px, py) from the stored planes (float32, see mesh_edge_planes).
+__device__ __forceinline__ void mesh_plane_eval(const float* e, int px, int py, float E[3]) {
+    const float dx = (float)px - e[9], dy = (float)py - e[10];  // exact: integers below 2^24
+#pragma unroll
+    for (int i = 0; i < 3; ++i) E[i] = fmaf(e[3 * i], dx, fmaf(e[3 * i + 1], dy, e[3 * i + 2]));
 }
 
 // Setup record index of fan k of mesh primitive p (zr_internal.h kMeshFans).
@@ -627,12 +649,12 @@ __device__ __forceinline__ void setup_finish_mesh(const DrawParams& P, uint32_t 
             ++nvalid;
             if (count_owned(P, g, s_hist)) {
                 box[0] = write_record(P, prim, g);
-                float e[9];
+                float e[12];
                 mesh_edge_planes(P, in.p, e);
                 float4* q = P.mesh_edges + (size_t)prim * 3u;
                 q[0] = make_float4(e[0], e[1], e[2], e[3]);
                 q[1] = make_float4(e[4], e[5], e[6], e[7]);
-                q[2] = make_float4(e[8], 0.0f, 0.0f, 0.0f);
+                q[2] = make_float4(e[8], e[9], e[10], e[11]);
             }
         }
     } else {  // clipped (or invalid): the general path
@@ -648,12 +670,12 @@ __device__ __forceinline__ void setup_finish_mesh(const DrawParams& P, uint32_t 
                 }
             }
             if (owned) {  // the resolve's barycentric planes (shade_mesh)
-                float e[9];
+                float e[12];
                 mesh_edge_planes(P, in.p, e);
                 float4* q = P.mesh_edges + (size_t)prim * 3u;
                 q[0] = make_float4(e[0], e[1], e[2], e[3]);
                 q[1] = make_float4(e[4], e[5], e[6], e[7]);
-                q[2] = make_float4(e[8], 0.0f, 0.0f, 0.0f);
+                q[2] = make_float4(e[8], e[9], e[10], e[11]);
             }
         }
     }
@@ -1370,11 +1392,9 @@ __device__ __forceinline__ void shade_mesh(const DrawParams& P, uint32_t prim, c
                                            float out[4]) {
     const float4* q = P.mesh_edges + (size_t)prim * 3u;
     const float4 qa = q[0], qb = q[1], qc = q[2];
-    const float c[9] = {qa.x, qa.y, qa.z, qa.w, qb.x, qb.y, qb.z, qb.w, qc.x};
-    const float fx = (float)px + 0.5f, fy = (float)py + 0.5f;
+    const float c[12] = {qa.x, qa.y, qa.z, qa.w, qb.x, qb.y, qb.z, qb.w, qc.x, qc.y, qc.z, qc.w};
     float E[3];
-#pragma unroll
-    for (int i = 0; i < 3; ++i) E[i] = fmaf(c[3 * i], fx, fmaf(c[3 * i + 1], fy, c[3 * i + 2]));
+    mesh_plane_eval(c, px, py, E);
     const float einv = 1.0f / ((E[0] + E[1]) + E[2]);
     const float b0 = E[0] * einv, b1 = E[1] * einv, b2 = E[2] * einv;
     const float* n0 = attr_ptr(P, vid[0], 1);
@@ -1523,15 +1543,15 @@ __device__ __forceinline__ void resolve_pixels(const DrawParams& P, int x0, int 
 //             kCompactLarge and its setup-record index in X0 (full record from HBM)
 //   depth     z0, dz1, dz2                      (last-wins modes only)
 //   attrs     flat: provoking colour (3); triangle: colour of v0..v2 (9); Blinn:
-//             normals then colours (18); mesh: barycentric planes (9), normals (9),
-//             uvs (6).  Triangle/Blinn in record order, mesh/flat in API order.
+//             normals then colours (18); mesh: barycentric planes and their
+//             reference pixel (12), normals (9), uvs (6).  Triangle/Blinn in record order, mesh/flat in API order.
 template <int PROG, int MODE>
 struct WinLayout {
     static constexpr bool kGeo = PROG == kProgTriangle || PROG == kProgBlinn || MODE == kDepthLastWins;
     static constexpr bool kZ = MODE == kDepthLastWins;
     static constexpr int kZOff = kGeo ? 5 : 0;
     static constexpr int kAttrOff = kZOff + (kZ ? 3 : 0);
-    static constexpr int kAttrW = PROG == kProgFlat ? 3 : PROG == kProgTriangle ? 9 : PROG == kProgBlinn ? 18 : 24;
+    static constexpr int kAttrW = PROG == kProgFlat ? 3 : PROG == kProgTriangle ? 9 : PROG == kProgBlinn ? 18 : 27;
     static constexpr int kWords = (kAttrOff + kAttrW + 3) & ~3;
 };
 
@@ -1588,14 +1608,15 @@ __device__ __forceinline__ void fetch_winner(const DrawParams& P, uint32_t rec, 
         const float4* q = P.mesh_edges + (size_t)gp * 3u;
         const float4 qa = q[0], qb = q[1], qc = q[2];
         a[0] = qa.x; a[1] = qa.y; a[2] = qa.z; a[3] = qa.w;
-        a[4] = qb.x; a[5] = qb.y; a[6] = qb.z; a[7] = qb.w; a[8] = qc.x;
+        a[4] = qb.x; a[5] = qb.y; a[6] = qb.z; a[7] = qb.w;
+        a[8] = qc.x; a[9] = qc.y; a[10] = qc.z; a[11] = qc.w;
 #pragma unroll
-        for (int k = 0; k < 3; ++k) copy3(a + 9 + 3 * k, attr_ptr(P, v[k], 1));
+        for (int k = 0; k < 3; ++k) copy3(a + 12 + 3 * k, attr_ptr(P, v[k], 1));
 #pragma unroll
         for (int k = 0; k < 3; ++k) {
             const float* u = attr_ptr(P, v[k], 2);
-            a[18 + 2 * k] = u[0];
-            a[19 + 2 * k] = u[1];
+            a[21 + 2 * k] = u[0];
+            a[22 + 2 * k] = u[1];
         }
     } else {
         // record order: setup swapped v1 / v2 when it oriented the primitive (sign of 1/A2)
@@ -1647,17 +1668,15 @@ __device__ __forceinline__ void shade_from_lds(const DrawParams& P, const float*
         // mesh.slang psmain: b_i = E_i / sum E with E_i = p . (h_j x h_k) at the pixel
         // centre, from the planes setup stored (mesh_edge_planes); then normal and uv
         // interpolated and lit like blinn_phong.slang, kd = (0.35 + 0.3 u, 0.35 + 0.3 v, 0.7)
-        const float fx = (float)px + 0.5f, fy = (float)py + 0.5f;
         float E[3];
-#pragma unroll
-        for (int i = 0; i < 3; ++i) E[i] = fmaf(a[3 * i], fx, fmaf(a[3 * i + 1], fy, a[3 * i + 2]));
+        mesh_plane_eval(a, px, py, E);
         const float einv = 1.0f / ((E[0] + E[1]) + E[2]);
         const float b0 = E[0] * einv, b1 = E[1] * einv, b2 = E[2] * einv;
         float n[3], uv[2];
 #pragma unroll
-        for (int i = 0; i < 3; ++i) n[i] = (b0 * a[9 + i] + b1 * a[12 + i]) + b2 * a[15 + i];
+        for (int i = 0; i < 3; ++i) n[i] = (b0 * a[12 + i] + b1 * a[15 + i]) + b2 * a[18 + i];
 #pragma unroll
-        for (int i = 0; i < 2; ++i) uv[i] = (b0 * a[18 + i] + b1 * a[20 + i]) + b2 * a[22 + i];
+        for (int i = 0; i < 2; ++i) uv[i] = (b0 * a[21 + i] + b1 * a[23 + i]) + b2 * a[25 + i];
         shade_blinn_phong(n[0], n[1], n[2], fmaf(uv[0], 0.3f, 0.35f), fmaf(uv[1], 0.3f, 0.35f), 0.7f, out);
         return;
     }
