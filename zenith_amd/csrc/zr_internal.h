@@ -94,13 +94,12 @@ constexpr uint32_t kMaxTilesPerPass = 16384;  // LDS histogram of the setup pass
 
 // Partitioned setup for tile-row shards.  Rank r routes the
 // primitives of its range [r * span, (r + 1) * span) to the ranks owning the tile
-// rows they touch, in chunks of kRouteChunk (one workgroup of k_route_count and
-// k_route_scatter each).  Exchange block for one destination = [1] u32 count,
-// then up to `span` u32 primitive ids in primitive order.  After the all-to-all a
-// receiver's blocks, in source order, list its primitives in API order, so the
-// dense position over the concatenated blocks is an order-preserving sequence.
+// rows they touch, kRouteChunk per workgroup of k_route.  Exchange block for one
+// destination = [1] u32 count, then up to `span` u32 primitive ids in no
+// particular order: the receiver's setup records are indexed by primitive id, so
+// visibility sequences are the API order whatever order the ids arrive in.
 constexpr uint32_t kRouteChunk = 512;
-constexpr int kRouteThreads = 256;   // 2 primitives per thread
+constexpr int kRouteThreads = 512;   // 1 primitive per thread (a latency chain: index -> positions)
 constexpr uint32_t kMaxShards = 32;  // destination masks are u32
 
 // Timing-experiment switches (ZR_DEBUG env var); never set in production runs.
@@ -182,14 +181,14 @@ struct DrawParams {
     uint32_t tile_threads;    // k_tile workgroup size: 256 or 512 (tile_threads_for)
     // partitioned setup (list mode).  In list mode `prims` is the
     // capacity of the received blocks (shard_count * span); the setup pass runs
-    // over the dense positions [0, sum of the blocks' counts).
+    // over the dense positions [0, sum of the blocks' counts) and writes the
+    // record of position j at its primitive id gids[j] (< draw_prims <= prims).
     uint32_t draw_prims;      // primitives of the draw (instances * triangles per instance)
     const uint32_t* list;     // received exchange blocks ([shard_count][list_block_words]), or nullptr
     uint32_t list_block_words;// 1 + span
-    uint32_t* gids;           // list mode: the draw primitive of each setup record (resolve's index fetch)
-    uint32_t* route_out;      // k_route_*: this rank's send blocks ([shard_count][list_block_words])
-    uint32_t* route_masks;    // [span] destination mask of each primitive of the range
-    uint32_t* route_counts;   // [route_chunks][shard_count] ids per chunk and destination
+    uint32_t* gids;           // list mode: the draw primitive at each dense position
+    uint32_t* route_out;      // k_route: this rank's send blocks ([shard_count][list_block_words])
+    uint32_t* route_counts;   // [shard_count + 1] ids per destination, finished workgroups (zero between routes)
     uint32_t route_lo, route_hi, route_chunks;
     // scratch (binning without contended global atomics)
     TriCompact* records;      // [prims] compact records (every binned primitive)

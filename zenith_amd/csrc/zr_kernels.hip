@@ -15,7 +15,7 @@
 //                resolve that shades each pixel's winner once, encodes to the
 //                attachment format and writes colour + depth with coalesced
 //                stores.  The attachment CLEAR is fused into the resolve.
-//   k_route_*    partitioned multi-GPU setup: route primitives to the ranks
+//   k_route      partitioned multi-GPU setup: route primitives to the ranks
 //                owning the tile rows they touch.
 //   k_clear      a render pass without draws.
 //
@@ -109,14 +109,8 @@ __device__ __forceinline__ uint32_t tri_of(const DrawParams& P, uint32_t gid) {
     return (P.tris_per_instance == P.draw_prims) ? gid : gid % P.tris_per_instance;
 }
 
-// Draw primitive of a setup record index: the index itself, or in list mode the
-// primitive k_setup_bin recorded for that dense position.
-__device__ __forceinline__ uint32_t prim_gid(const DrawParams& P, uint32_t pos) {
-    return P.list ? P.gids[pos] : pos;
-}
-
 __device__ __forceinline__ void winner_vids(const DrawParams& P, uint32_t prim, uint32_t v[3]) {
-    const uint32_t tri = tri_of(P, prim_gid(P, prim));
+    const uint32_t tri = tri_of(P, prim);
     const uint32_t e0 = P.first + tri * 3u;
     if (P.index_size == 4) {
         const uint3 ix = *reinterpret_cast<const uint3*>(P.ib + (uint64_t)e0 * 4);
@@ -690,28 +684,31 @@ __device__ __forceinline__ void setup_finish(const DrawParams& P, uint32_t prim,
     if (prim >= n_pos) return;
     BBox box{kEmptyBox, 0u};
     PrimGeom g;
+    // List mode: the record is indexed by the draw primitive (records are sized
+    // for every primitive of the draw), so bins, keys and the resolve all use
+    // global primitive ids -- the visibility sequence is the API order whatever
+    // order the exchange delivered the primitives in.  gids maps the dense
+    // position back for phase 4 and the spill scan.
+    if (P.list) P.gids[prim] = gid;
     if (prim_geometry(P, in, g, ndropped)) {
         ++nvalid;
-        if (count_owned(P, g, s_hist)) {
-            box = write_record(P, prim, g);
-            if (P.list) P.gids[prim] = gid;
-        }
+        if (count_owned(P, g, s_hist)) box = write_record(P, P.list ? gid : prim, g);
     }
     *bbox_out = box;
 }
 
 // ----------------------------------------------------------------- k_route
 //
-// Partitioned setup, step 1 (tile-row shards).  Workgroup c of
-// both kernels owns primitives [route_lo + c * kRouteChunk, ...) of this rank's
-// range, thread t the primitives base + t and base + t + 256 (coalesced).
-//   k_route_count    setup geometry -> the set of ranks owning a tile row the
-//                    bbox touches (ty % G == rank) as a mask per primitive, and
-//                    the chunk's id count per destination
-//   k_route_scatter  prefix of the counts of earlier chunks, then the chunk's ids
-//                    in primitive order into each destination's block (ballot
-//                    ranks within a wave, per-wave offsets in LDS); the last
-//                    chunk stores the block totals.
+// Partitioned setup, step 1 (tile-row shards): one pass over this
+// rank's primitive range [route_lo, route_hi).  Workgroup c owns primitives
+// route_lo + c * kRouteChunk + t (kRouteThreads per pass, coalesced): setup geometry ->
+// the set of ranks owning a tile row the bbox touches (ty % G == rank), then the
+// ids appended to each destination's block.  A workgroup reserves its run in a
+// block with one returning atomic per destination (route_counts[d]), so runs
+// land in any order: the receiver keys everything by the primitive id (setup
+// records are indexed by it in list mode), so block order carries no meaning.
+// The last workgroup to finish stores the block totals and re-zeroes the
+// counters for the next draw (they start zeroed when allocated).
 __device__ __forceinline__ uint32_t dest_mask(const DrawParams& P, const PrimGeom& g) {
     const uint32_t G = P.shard_count;
     const int ty0 = g.py0 >> kTileShift, ty1 = g.py1 >> kTileShift;
@@ -721,83 +718,63 @@ __device__ __forceinline__ uint32_t dest_mask(const DrawParams& P, const PrimGeo
     return m;
 }
 
-__global__ __launch_bounds__(kRouteThreads) void k_route_count(DrawParams P) {
-    __shared__ uint32_t s_cnt[kMaxShards];
-    const uint32_t G = P.shard_count, c = blockIdx.x, tid = threadIdx.x, lane = tid & 63u;
-    if (tid < kMaxShards) s_cnt[tid] = 0;
+__global__ __launch_bounds__(kRouteThreads) void k_route(DrawParams P) {
+    constexpr uint32_t kPer = kRouteChunk / kRouteThreads, kWaves = kRouteThreads / 64, kSlots = kPer * kWaves;
+    __shared__ uint32_t s_off[kSlots][kMaxShards];  // ids per (part, wave) and destination -> run offsets
+    __shared__ uint32_t s_base[kMaxShards];
+    __shared__ uint32_t s_last;
+    const uint32_t G = P.shard_count, c = blockIdx.x, tid = threadIdx.x;
+    const uint32_t lane = tid & 63u, wave = tid >> 6;
     const uint32_t p0 = P.route_lo + c * kRouteChunk + tid;
-    PrimIn in[2];
+    PrimIn in[kPer];
 #pragma unroll
-    for (int k = 0; k < 2; ++k) {
+    for (uint32_t k = 0; k < kPer; ++k) {
         in[k].ok = p0 + k * kRouteThreads < P.route_hi;
         if (in[k].ok) fetch_indices_gid(P, p0 + k * kRouteThreads, in[k]);
     }
 #pragma unroll
-    for (int k = 0; k < 2; ++k) fetch_positions(P, in[k]);
-    uint32_t m[2];
+    for (uint32_t k = 0; k < kPer; ++k) fetch_positions(P, in[k]);
+    uint32_t m[kPer];
     int ndropped = 0;
 #pragma unroll
-    for (int k = 0; k < 2; ++k) {
+    for (uint32_t k = 0; k < kPer; ++k) {
         PrimGeom g;
         m[k] = prim_geometry(P, in[k], g, ndropped) ? dest_mask(P, g) : 0u;
-        if (p0 + k * kRouteThreads < P.route_hi) P.route_masks[p0 + k * kRouteThreads - P.route_lo] = m[k];
-    }
-    __syncthreads();
-    for (uint32_t d = 0; d < G; ++d) {
-        const uint32_t n = (uint32_t)(__popcll(__ballot((m[0] >> d) & 1u)) + __popcll(__ballot((m[1] >> d) & 1u)));
-        if (lane == 0 && n) atomicAdd(&s_cnt[d], n);
-    }
-    __syncthreads();
-    if (tid < G) P.route_counts[(size_t)c * G + tid] = s_cnt[tid];
-}
-
-__global__ __launch_bounds__(kRouteThreads) void k_route_scatter(DrawParams P) {
-    constexpr uint32_t kWaves = kRouteThreads / 64;
-    __shared__ uint32_t s_pre[kMaxShards];
-    __shared__ uint32_t s_off[2][kWaves][kMaxShards];
-    const uint32_t G = P.shard_count, c = blockIdx.x, tid = threadIdx.x;
-    const uint32_t lane = tid & 63u, wave = tid >> 6;
-    if (tid < kMaxShards) s_pre[tid] = 0;
-    const uint32_t p0 = P.route_lo + c * kRouteChunk + tid;
-    uint32_t m[2];
-#pragma unroll
-    for (int k = 0; k < 2; ++k) {
-        const uint32_t p = p0 + k * kRouteThreads;
-        m[k] = p < P.route_hi ? P.route_masks[p - P.route_lo] : 0u;
-    }
-    __syncthreads();
-    for (uint32_t i = tid; i < c * G; i += kRouteThreads) {  // ids of earlier chunks, per destination
-        const uint32_t n = P.route_counts[i];
-        if (n) atomicAdd(&s_pre[i % G], n);
     }
     for (uint32_t d = 0; d < G; ++d) {
 #pragma unroll
-        for (int k = 0; k < 2; ++k) {
+        for (uint32_t k = 0; k < kPer; ++k) {
             const uint32_t n = (uint32_t)__popcll(__ballot((m[k] >> d) & 1u));
-            if (lane == 0) s_off[k][wave][d] = n;
+            if (lane == 0) s_off[k * kWaves + wave][d] = n;
         }
     }
     __syncthreads();
-    if (tid < G) {  // primitive order: first half (k = 0) wave by wave, then the second half
-        uint32_t run = s_pre[tid];
-        for (int k = 0; k < 2; ++k)
-            for (uint32_t w = 0; w < kWaves; ++w) {
-                const uint32_t n = s_off[k][w][tid];
-                s_off[k][w][tid] = run;
-                run += n;
-            }
-        if (c + 1u == P.route_chunks) P.route_out[(size_t)tid * P.list_block_words] = run;  // block total
+    if (tid < G) {
+        uint32_t run = 0;
+        for (uint32_t i = 0; i < kSlots; ++i) {
+            const uint32_t n = s_off[i][tid];
+            s_off[i][tid] = run;
+            run += n;
+        }
+        s_base[tid] = run ? atomicAdd(&P.route_counts[tid], run) : 0u;
     }
     __syncthreads();
     const unsigned long long below = (1ull << lane) - 1ull;
     for (uint32_t d = 0; d < G; ++d) {
-        uint32_t* ids = P.route_out + (size_t)d * P.list_block_words + 1u;
+        uint32_t* ids = P.route_out + (size_t)d * P.list_block_words + 1u + s_base[d];
 #pragma unroll
-        for (int k = 0; k < 2; ++k) {
+        for (uint32_t k = 0; k < kPer; ++k) {
             const bool on = (m[k] >> d) & 1u;
             const unsigned long long b = __ballot(on);
-            if (on) ids[s_off[k][wave][d] + (uint32_t)__popcll(b & below)] = p0 + k * kRouteThreads;
+            if (on) ids[s_off[k * kWaves + wave][d] + (uint32_t)__popcll(b & below)] = p0 + k * kRouteThreads;
         }
+    }
+    // every reservation of this workgroup has returned (s_base) before its arrival
+    if (tid == 0) s_last = atomicAdd(&P.route_counts[G], 1u) + 1u == gridDim.x;
+    __syncthreads();
+    if (s_last && tid < G) {
+        P.route_out[(size_t)tid * P.list_block_words] = atomicExch(&P.route_counts[tid], 0u);
+        if (tid == 0) atomicExch(&P.route_counts[G], 0u);
     }
 }
 
@@ -1101,7 +1078,7 @@ __global__ __launch_bounds__(kSetupThreads) void k_setup_bin(DrawParams P) {
             const BBox bb = P.bbox_lds ? s_bbox[j] : P.bboxes[prim];
             // overflowed draw: k_tile rasterizes by scanning every record's bbox
             if (P.bbox_lds && total > P.bin_capacity) P.bboxes[prim] = bb;
-            scatter(prim, bb);
+            scatter(P.list && bb.bb0 != kEmptyBox ? P.gids[prim] : prim, bb);
             if (MESH) {  // fans 1 and 2 (bboxes stored by this workgroup in phase 1)
                 scatter(mesh_record(P, prim, 1), P.bboxes[mesh_record(P, prim, 1)]);
                 scatter(mesh_record(P, prim, 2), P.bboxes[mesh_record(P, prim, 2)]);
@@ -1415,7 +1392,7 @@ __device__ __forceinline__ void shade_mesh(const DrawParams& P, uint32_t prim, c
 template <bool IDX32>
 __device__ __forceinline__ void resolve_vids(const DrawParams& P, uint32_t prim, uint32_t v[3]) {
     if (IDX32) {
-        const uint32_t tri = tri_of(P, prim_gid(P, prim));
+        const uint32_t tri = tri_of(P, prim);
         const uint3 ix = *reinterpret_cast<const uint3*>(P.ib + (uint64_t)(P.first + tri * 3u) * 4);
         const uint32_t off = (uint32_t)P.vertex_offset;
         v[0] = ix.x + off; v[1] = ix.y + off; v[2] = ix.z + off;
@@ -1572,7 +1549,7 @@ __device__ __forceinline__ void fetch_winner(const DrawParams& P, uint32_t rec, 
     uint32_t v[3];
     const uint32_t gp = record_prim<PROG>(P, rec);  // draw primitive (mesh: of the fan record)
     {
-        const uint32_t tri = tri_of(P, prim_gid(P, gp));
+        const uint32_t tri = tri_of(P, gp);
         const uint32_t e0 = P.first + tri * 3u;
         if (IDX32) {
             const uint3 ix = *reinterpret_cast<const uint3*>(P.ib + (uint64_t)e0 * 4);
@@ -2116,20 +2093,22 @@ __global__ __launch_bounds__(NT, ZR_TILE_WGS * kTileThreads / 256) void k_tile(D
                     hit = bb.bb0 != kEmptyBox && (int)(bb.bb0 & 0xFFFFu) < x0 + kTile && (int)(bb.bb1 & 0xFFFFu) >= x0 &&
                           (int)(bb.bb0 >> 16) < y0 + kTile && (int)(bb.bb1 >> 16) >= y0;
                 }
+                uint32_t rec = j;  // bboxes by position; records by primitive in list mode
                 if (hit) {
-                    const int4* rp = reinterpret_cast<const int4*>(P.records + j);
+                    if (P.list) rec = P.gids[j];
+                    const int4* rp = reinterpret_cast<const int4*>(P.records + rec);
                     q0 = rp[0];
                     q1 = rp[1];
                 }
                 const bool large = compact_is_large(q0);
                 if (hit && !large)
-                    raster_lane<MODE, INITD>(P, decode_compact(P, q0, q1, true), entry_seq<PROG>(P, j), x0, y0, s_key, s_initd,
-                                             0, 0);
+                    raster_lane<MODE, INITD>(P, decode_compact(P, q0, q1, true), entry_seq<PROG>(P, rec), x0, y0, s_key,
+                                             s_initd, 0, 0);
                 unsigned long long big = __ballot(hit && large);
                 while (big) {
                     const uint32_t i = (uint32_t)__builtin_ctzll(big);
                     big &= big - 1ull;
-                    const uint32_t prim = (uint32_t)rl((int)j, i);
+                    const uint32_t prim = (uint32_t)rl((int)rec, i);
                     raster_prim<MODE, INITD>(P, load_uniform_record(P.records_big + prim), entry_seq<PROG>(P, prim), x0, y0, lane,
                                              s_key, s_initd);
                 }
@@ -2268,8 +2247,7 @@ void launch_tile(const DrawParams& p, void* stream) {
 }
 
 void launch_route(const DrawParams& p, void* stream) {
-    hipLaunchKernelGGL(k_route_count, dim3(p.route_chunks), dim3(kRouteThreads), 0, (hipStream_t)stream, p);
-    hipLaunchKernelGGL(k_route_scatter, dim3(p.route_chunks), dim3(kRouteThreads), 0, (hipStream_t)stream, p);
+    hipLaunchKernelGGL(k_route, dim3(p.route_chunks), dim3(kRouteThreads), 0, (hipStream_t)stream, p);
 }
 
 void launch_clear(const DrawParams& p, void* stream) {

@@ -203,9 +203,7 @@ struct ScratchSet {
     uint64_t xrecv_cap = 0;
     uint32_t* gids = nullptr;   // draw primitive per setup record (list mode)
     uint64_t gids_cap = 0;
-    uint32_t* rmasks = nullptr; // route: destination mask per primitive of the range
-    uint64_t rmasks_cap = 0;
-    uint32_t* rcounts = nullptr;// route: ids per chunk and destination
+    uint32_t* rcounts = nullptr;// route: ids per destination block + finished workgroups
     uint64_t rcounts_cap = 0;
     uint32_t* wg_offsets = nullptr;  // split setup: per-workgroup tile offsets
     uint64_t wg_offsets_cap = 0;
@@ -788,10 +786,11 @@ zr_result exec_draw(zr_device* d, ExecState& s, const Cmd& c, bool indexed) {
         if ((rc = grow(d, S.xsend, S.xsend_cap, words, 4))) return rc;
         if ((rc = grow(d, S.xrecv, S.xrecv_cap, words, 4))) return rc;
         if ((rc = grow(d, S.gids, S.gids_cap, positions, 4))) return rc;
-        if ((rc = grow(d, S.rmasks, S.rmasks_cap, span, 4))) return rc;
-        if ((rc = grow(d, S.rcounts, S.rcounts_cap, (uint64_t)P.route_chunks * s.shard_count, 4))) return rc;
+        if (!S.rcounts) {  // k_route's block counters: zeroed once, re-zeroed by every route
+            if ((rc = grow(d, S.rcounts, S.rcounts_cap, kMaxShards + 1, 4))) return rc;
+            ZR_HIP(hipMemsetAsync(S.rcounts, 0, (kMaxShards + 1) * 4, ss));
+        }
         P.route_out = S.xsend;
-        P.route_masks = S.rmasks;
         P.route_counts = S.rcounts;
         P.gids = S.gids;
         timed_launch(d, "route", ss, [&] { launch_route(P, ss); });
@@ -802,23 +801,27 @@ zr_result exec_draw(zr_device* d, ExecState& s, const Cmd& c, bool indexed) {
         });
         if (xr != ZR_SUCCESS) return fail(xr, "tile-shard exchange callback failed: " + g_last_error);
         P.list = S.xrecv;
-        ZR_HIP(hipEventRecord(S.setup_done, ss));
         if (no_tiles) {  // routed and exchanged; nothing of this target to draw here
+            ZR_HIP(hipEventRecord(S.setup_done, ss));
             s.color_clear_pending = false;
             s.depth_clear_pending = false;
             return ZR_SUCCESS;
         }
-        ZR_HIP(hipStreamWaitEvent(d->stream, S.setup_done, 0));
         // List mode runs as the two split launches (no grid barrier): a partitioned
         // draw shares the GPU with the collectives' kernels on other streams, so a
         // persistent launch could not count on every workgroup being resident.
+        // They run on the setup stream behind the exchange, so draw i+1's route,
+        // exchange and setup overlap draw i's tile pass (the main stream only
+        // runs tile passes).
         if ((rc = grow(d, S.wg_offsets, S.wg_offsets_cap, (uint64_t)P.setup_wgs * P.ntiles, 4))) return rc;
         P.wg_offsets = S.wg_offsets;
         P.bbox_lds = 0;
-        timed_launch(d, "setup_bin", d->stream, [&] {
-            launch_setup_split(P, 1, d->stream);
-            launch_setup_split(P, 2, d->stream);
+        timed_launch(d, "setup_bin", ss, [&] {
+            launch_setup_split(P, 1, ss);
+            launch_setup_split(P, 2, ss);
         });
+        ZR_HIP(hipEventRecord(S.setup_done, ss));
+        ZR_HIP(hipStreamWaitEvent(d->stream, S.setup_done, 0));
     } else if (split) {
         if ((rc = grow(d, S.wg_offsets, S.wg_offsets_cap, (uint64_t)P.setup_wgs * P.ntiles, 4))) return rc;
         P.wg_offsets = S.wg_offsets;
@@ -994,7 +997,7 @@ ZR_API void zr_device_destroy(zr_device* d) {
     for (ScratchSet& S : d->sets) {
         for (void* p : {(void*)S.records, (void*)S.records_big, (void*)S.mesh_edges, (void*)S.bboxes, (void*)S.tile_counts,
                         (void*)S.tile_offsets, (void*)S.counters, (void*)S.bins, (void*)S.xsend, (void*)S.xrecv,
-                        (void*)S.gids, (void*)S.rmasks, (void*)S.rcounts, (void*)S.wg_offsets})
+                        (void*)S.gids, (void*)S.rcounts, (void*)S.wg_offsets})
             if (p) (void)hipFree(p);
         if (S.setup_done) (void)hipEventDestroy(S.setup_done);
         if (S.tile_done) (void)hipEventDestroy(S.tile_done);

@@ -57,7 +57,9 @@ class TileRowGather:
 # device layout (zr_internal.h kRouteChunk, zr_runtime.cpp exec_draw): rank r
 # routes primitives [r * span, (r + 1) * span) with span = ceil(ceil(N / G) /
 # ROUTE_CHUNK) * ROUTE_CHUNK; its block for one destination is [1] u32 count, then
-# up to `span` u32 primitive ids in primitive order (block_words = span + 1).
+# up to `span` u32 primitive ids (block_words = span + 1).  The device appends a
+# workgroup's run of ids at an atomically reserved offset, so the order of the ids
+# in a block is unspecified: the receiver keys its setup records by primitive id.
 
 ROUTE_CHUNK = 512  # zr::kRouteChunk (primitives per k_route workgroup)
 
@@ -78,9 +80,10 @@ def route_range(n_prims: int, rank: int, world: int):
 
 
 def route_blocks(row_lo, row_hi, rank: int, world: int) -> torch.Tensor:
-    """Host model of k_route_count + k_route_scatter for rank `rank`: row_lo/row_hi
-    are each primitive's first/last tile row (row_lo < 0: no sample).  Returns the
-    send buffer, [world][block_words] uint32 (as int64 for portability)."""
+    """Host model of k_route for rank `rank`: row_lo/row_hi are each primitive's
+    first/last tile row (row_lo < 0: no sample).  Returns the send buffer,
+    [world][block_words] uint32 (as int64 for portability), ids in primitive order
+    (one of the orders the device may produce)."""
     n = len(row_lo)
     _, span, bw = route_geometry(n, world)
     send = torch.zeros((world, bw), dtype=torch.int64)
@@ -100,8 +103,8 @@ def route_blocks(row_lo, row_hi, rank: int, world: int) -> torch.Tensor:
 
 
 def received_primitives(recv: torch.Tensor, n_prims: int, world: int) -> list:
-    """Primitive ids a rank's received blocks hold, in block-position order
-    (= API order, the sequence the visibility keys use)."""
+    """Primitive ids a rank's received blocks hold, in block-position order (the
+    device's dense setup positions; the visibility keys use the ids themselves)."""
     _, _, bw = route_geometry(n_prims, world)
     recv = recv.reshape(world, bw)
     out = []
