@@ -1,7 +1,7 @@
 # Round deliverables on the GPU box for the current tree (run via gpurun):
 #   gpurun --timeout 1200 -- 'bash tools/gpu_round.sh v35 [quick]'
 # Full GPU parity, bench C2 with CPU baseline, C1/C3/C4/cerberus bench lines, C2
-# tile-row shard emulation (rank 0 of 2/4/8 on one GPU), kernel-trace
+# tile-row shard emulation (rank 0 of 2/4/8 on one GPU; C2/C3 partitioned at 8), kernel-trace
 # stats, PMC FETCH/WRITE passes + counter calibration.  "quick" stops after the
 # bench lines.  Every GPU step has its own time limit; the first failure ends the run.
 set -o pipefail
@@ -13,6 +13,8 @@ timeout -k 10 700 python -u -m pytest tests -m gpu -x -q --timeout 120 --timeout
 timeout -k 10 300 python bench.py > $O/bench_c2.json 2> $O/bench.err || exit 2
 for c in c1 c3 c4 cerberus; do timeout -k 10 200 python bench.py --config $c --no-cpu-baseline > $O/bench_$c.json 2>> $O/bench.err || exit 3; done
 for g in 2 4 8; do timeout -k 10 200 python bench.py --emulate-shard $g --no-cpu-baseline > $O/bench_c2_shard$g.json 2>> $O/bench.err || exit 3; done
+for c in c2 c3; do timeout -k 10 200 python bench.py --config $c --emulate-shard 8 --setup partitioned --no-cpu-baseline > $O/bench_${c}_shard8_part.json 2>> $O/bench.err || exit 3; done
+timeout -k 10 200 python bench.py --config c3 --emulate-shard 8 --no-cpu-baseline > $O/bench_c3_shard8.json 2>> $O/bench.err || exit 3
 [ "$2" = quick ] && { echo done; exit 0; }
 timeout -k 10 200 rocprofv3 --kernel-trace --stats -d $O/kt -o run --output-format csv -- python3 bench.py --steps 50 --warmup 5 --no-cpu-baseline > $O/kt.log 2>&1 || exit 4
 timeout -k 10 200 rocprofv3 --pmc FETCH_SIZE -d $O/pf -o run --output-format csv -- python3 bench.py --steps 5 --warmup 2 --no-cpu-baseline > $O/pf.log 2>&1 || exit 5

@@ -4,7 +4,7 @@ bench.py reads for ``roofline.traffic``.
 
   python tools/pmc_summary.py --fetch DIR/run_counter_collection.csv \
       --write DIR2/run_counter_collection.csv --calib CALIB_FETCH.csv CALIB_WRITE.csv \
-      --config c2 -o profiles/r01_pmc_c2.json
+      --config c2 -o profiles/r02_pmc_c2.json
 
 FETCH_SIZE / WRITE_SIZE are in KiB per dispatch.  MI355X_MICROARCH.md §HBM: on
 gfx950 FETCH_SIZE reports half the bytes of 16-B/lane streaming reads; other
