@@ -61,8 +61,8 @@ namespace zr {
 #ifndef ZR_TILE_SUBLANE
 #define ZR_TILE_SUBLANE 1    // sparse segments: k lanes per entry split its bbox rows (0: one lane per entry)
 #endif
-#ifndef ZR_LANE_PREDICATED
-#define ZR_LANE_PREDICATED 0  // A/B: lane-walk step without the coverage branch
+#ifndef ZR_LANE_PAIR
+#define ZR_LANE_PAIR 1  // lane walk: two pixels of a row per step (0: one pixel per step, A/B)
 #endif
 #ifndef ZR_TILE_DEBUG
 #define ZR_TILE_DEBUG 0      // 1: k_tile honours the ZR_DEBUG timing switches and stamps (A/B builds only;
@@ -1268,27 +1268,40 @@ __device__ __forceinline__ void raster_lane(const DrawParams& P, const TriRecord
     // no fragment can fall outside.  NaN depths fail the comparisons, so keep it.
     const float z1v = z0 + dz1, z2v = z0 + dz2, zlo = P.dlo + 1e-4f, zhi = P.dhi - 1e-4f;
     const bool zsafe = z0 >= zlo && z0 <= zhi && z1v >= zlo && z1v <= zhi && z2v >= zlo && z2v <= zhi;
+    // one covered sample: depth from the (un-biased) edge values, test, key
+    auto frag = [&](auto ztest, int e1, int e2, uint32_t a) {
+        const float fb1 = (float)(e1 + b1) * invA2, fb2 = (float)(e2 + b2) * invA2;
+        const float z = fmaf(fb2, dz2, fmaf(fb1, dz1, z0));
+        if ((!decltype(ztest)::value || (z >= P.dlo && z <= P.dhi)) &&
+            (!INITD || depth_pass(P.depth_op, z, s_initd[a >> 3])))
+            atomicMin(reinterpret_cast<unsigned long long*>(reinterpret_cast<char*>(s_key) + a), frag_key<MODE>(z, seq));
+    };
+#if ZR_LANE_PAIR
+    // Two pixels of a row per step (VALU and loop-control SALU are what the lane
+    // walk spends: one step's wrap selects and branch bookkeeping now serve two
+    // samples).  The second pixel of a row's last pair lies past an odd-width
+    // bbox and is skipped (pair index lastB).
+    const int hw = (bw + 1) >> 1, lastB = (bw & 1) ? hw - 1 : hw;
+    const int t0 = 2 * sx0, t1 = 2 * sx1, t2 = 2 * sx2;
+    const int q0 = k * sy0 - 2 * (hw - 1) * sx0, q1 = k * sy1 - 2 * (hw - 1) * sx1, q2 = k * sy2 - 2 * (hw - 1) * sx2;
+    const uint32_t lq = (uint32_t)((k * kTile - 2 * (hw - 1)) * 8);
     auto sweep = [&](auto ztest) {
         do {
-#if ZR_LANE_PREDICATED
-            {  // branch-free step: uncovered lanes issue a no-op min (~0)
-                const float fb1 = (float)(w1 + b1) * invA2, fb2 = (float)(w2 + b2) * invA2;
-                const float z = fmaf(fb2, dz2, fmaf(fb1, dz1, z0));
-                const bool ok = ((w0 | w1 | w2) >= 0) && (!decltype(ztest)::value || (z >= P.dlo && z <= P.dhi)) &&
-                                (!INITD || depth_pass(P.depth_op, z, s_initd[la >> 3]));
-                atomicMin(reinterpret_cast<unsigned long long*>(reinterpret_cast<char*>(s_key) + la),
-                          ok ? frag_key<MODE>(z, seq) : ~0ull);
-            }
+            if ((w0 | w1 | w2) >= 0) frag(ztest, w1, w2, la);
+            const int v0 = w0 + sx0, v1 = w1 + sx1, v2 = w2 + sx2;
+            if (ex != lastB && (v0 | v1 | v2) >= 0) frag(ztest, v1, v2, la + 8u);
+            const bool wrap = ++ex == hw;
+            ex = wrap ? 0 : ex;
+            w0 += wrap ? q0 : t0;
+            w1 += wrap ? q1 : t1;
+            w2 += wrap ? q2 : t2;
+            la += wrap ? lq : 16u;
+        } while (la != la_end);
+    };
 #else
-            if ((w0 | w1 | w2) >= 0) {
-                const float fb1 = (float)(w1 + b1) * invA2, fb2 = (float)(w2 + b2) * invA2;
-                const float z = fmaf(fb2, dz2, fmaf(fb1, dz1, z0));
-                if ((!decltype(ztest)::value || (z >= P.dlo && z <= P.dhi)) &&
-                    (!INITD || depth_pass(P.depth_op, z, s_initd[la >> 3])))
-                    atomicMin(reinterpret_cast<unsigned long long*>(reinterpret_cast<char*>(s_key) + la),
-                              frag_key<MODE>(z, seq));
-            }
-#endif
+    auto sweep = [&](auto ztest) {
+        do {
+            if ((w0 | w1 | w2) >= 0) frag(ztest, w1, w2, la);
             const bool wrap = ++ex == bw;
             ex = wrap ? 0 : ex;
             w0 += wrap ? j0 : sx0;
@@ -1297,6 +1310,7 @@ __device__ __forceinline__ void raster_lane(const DrawParams& P, const TriRecord
             la += wrap ? lj : 8u;
         } while (la != la_end);
     };
+#endif
     if (__ballot(!zsafe) == 0ull)
         sweep(std::false_type{});
     else
