@@ -507,6 +507,10 @@ static void raster_rows(const zro_target *t, const zro_draw_state *s, const zro_
     const int32_t dx1 = o->X[0] - o->X[2], dy1 = o->Y[0] - o->Y[2];
     const int32_t dx2 = o->X[1] - o->X[0], dy2 = o->Y[1] - o->Y[0];
     const float dz1 = o->z[1] - o->z[0], dz2 = o->z[2] - o->z[0];
+    /* depth is a plane in the biased edge values w_i - bias_i,
+     * z = fmaf(w2', C2, fmaf(w1', C1, Z0)), C_i = dz_i * invA2, Z0 its value at w' = 0 */
+    const float C1 = dz1 * o->invA2, C2 = dz2 * o->invA2;
+    const float Z0 = fmaf((float)o->bias[2], C2, fmaf((float)o->bias[1], C1, o->z[0]));
     const float dlo = s->viewport[4] < s->viewport[5] ? s->viewport[4] : s->viewport[5];
     const float dhi = s->viewport[4] < s->viewport[5] ? s->viewport[5] : s->viewport[4];
     const int test = s->depth_test && t->depth;
@@ -520,8 +524,7 @@ static void raster_rows(const zro_target *t, const zro_draw_state *s, const zro_
             const int64_t w2 = (int64_t)dx2 * (Sy - o->Y[0]) - (int64_t)dy2 * (Sx - o->X[0]);
             if (w0 < o->bias[0] || w1 < o->bias[1] || w2 < o->bias[2]) continue;
             if (st) st->fragments_covered++;
-            const float b1 = (float)w1 * o->invA2, b2 = (float)w2 * o->invA2;
-            float z = fmaf(b2, dz2, fmaf(b1, dz1, o->z[0]));
+            float z = fmaf((float)(w2 - o->bias[2]), C2, fmaf((float)(w1 - o->bias[1]), C1, Z0));
             if (z == 0.0f) z = 0.0f; /* canonical +0 */
             if (!(z >= dlo && z <= dhi)) continue; /* depth clip == 0<=z<=w clip for w>0 */
             const size_t idx = (size_t)py * t->width + (size_t)px;

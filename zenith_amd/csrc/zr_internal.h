@@ -104,32 +104,28 @@ constexpr uint32_t kMaxShards = 32;  // destination masks are u32
 
 // Timing-experiment switches (ZR_DEBUG env var); never set in production runs.
 enum : uint32_t { kDebugSkipRaster = 1u, kDebugSkipShade = 2u, kDebugLoadOnly = 16u,
-                  kDebugPhase1Only = 32u, kDebugStopAfterScan = 64u, kDebugStamps = 128u,
+                  kDebugPhase1Only = 32u, kDebugStamps = 128u,
                   kDebugReverseTiles = 256u, kDebugSkipLanePath = 512u, kDebugSkipWavePath = 1024u };
 
 // Status words in host-mapped pinned memory (read by the runtime at sync points).
 enum StatusWord : uint32_t {
-    kStTotalPairs = 0,
-    kStOverflow = 1,
-    kStMaxPairs = 2,
+    kStTotalPairs = 0,      // (tile, primitive) pairs of the last draw (saturating)
+    kStOverflow = 1,        // draws with a tile list longer than its slab (since the last sync)
+    kStMaxPairs = 2,        // bin entries (ntiles * longest list) the largest such draw needs
     kStTrianglesSetup = 3,
     kStDroppedClip = 4,
-    kStBarrierTimeout = 5,
     kStWords = 16,
 };
-// Device counters of k_setup_bin.  Zero between draws: the draw's k_tile resets
-// them (and the tile counts), so a draw needs no memset launch.
-// The grid barrier is two-level (arrivals on 8 group counters, blockIdx % 8, then
-// one top counter; release through 8 group flags), each word on a 128-B line of
-// its own: 256 workgroups on one counter cost ~10 us after the last arrival.
-constexpr uint32_t kBarrierGroups = 8;
+// Device counters of k_setup_bin, read by the draw's k_tile (tile 0 reports them
+// and resets them, as every tile resets its count, so a draw needs no memset).
 enum CounterWord : uint32_t {
     kCtSetup = 0, kCtDropped = 1,
-    kCtGroup = 32,                            // + 32 * group: arrivals of the group
-    kCtTop = 32 * (1 + kBarrierGroups),       // groups complete
-    kCtRelease = 32 * (2 + kBarrierGroups),   // + 32 * group: barrier open
-    kCtWords = 32 * (2 + 2 * kBarrierGroups),
+    kCtMaxTile = 2,   // the largest tile list of the draw (pairs, including any past the slab)
+    kCtPairs = 4,     // u64 (words 4-5): (tile, primitive) pairs of the draw
+    kCtWords = 32,
 };
+// draw_info words (written by k_setup_bin for k_tile)
+enum DrawInfoWord : uint32_t { kInfoRecords = 0, kInfoWords = 4 };
 
 struct DrawParams {
     // vertex input (binding 0) and index buffer
@@ -195,17 +191,16 @@ struct DrawParams {
     TriRecord* records_big;   // [prims] full records, written for large primitives only
     float4* mesh_edges;       // mesh program: [prims][3] homogeneous edge coefficients (shade_mesh)
     BBox* bboxes;             // [prims]; bb0 == kEmptyBox when culled / no owned tile
-    uint32_t* tile_counts;    // [ntiles]
-    uint32_t* tile_offsets;   // [ntiles] exclusive scan (list starts)
+    uint32_t* tile_counts;    // [ntiles] pairs per tile (zero between draws)
+    uint32_t* draw_info;      // [kInfoWords] (DrawInfoWord)
     uint32_t* counters;       // [kCtWords] (CounterWord)
-    uint32_t* bins;           // [bin_capacity] primitive ids grouped by tile
-    uint32_t bin_capacity;
-    uint32_t setup_wgs;       // workgroups of k_setup_bin (<= CUs: all resident)
+    uint32_t* bins;           // [ntiles * slab] tile t's list at [t * slab, t * slab + count): id | area bucket
+    uint32_t slab;            // list capacity per tile (host: bin buffer / ntiles)
+    uint32_t setup_wgs;       // workgroups of k_setup_bin (one per CU at most)
     uint32_t unit_shift;      // log2 primitives per claim unit (64 lanes * batch * rounds)
     uint32_t units;           // claim units of the draw: ceil(prims / unit size)
     uint32_t setup_batch;     // primitives per lane in flight (template instance of k_setup_bin)
     uint32_t bbox_lds;        // 0: bboxes in global memory; else LDS entries per workgroup (own units * unit size)
-    uint32_t* wg_offsets;     // split setup: [setup_wgs][ntiles] each workgroup's offsets in the tile lists
     uint32_t debug;           // kDebug* bits (timing experiments only)
     unsigned long long* dbg_ts; // [setup_wgs][8] s_memrealtime stamps (kDebugStamps only)
     uint32_t* status;         // host-mapped
@@ -230,13 +225,12 @@ inline uint32_t tile_threads_for(uint32_t ntiles, uint32_t cus, uint64_t prims) 
 }
 
 // Launchers (zr_kernels.hip).  All enqueue on `stream`; no host synchronisation.
-void launch_setup_bin(const DrawParams& p, void* stream);  // persistent: setup + scan + scatter
+void launch_setup_bin(const DrawParams& p, void* stream);  // setup + bin, one launch
 size_t setup_bin_lds_bytes(uint32_t ntiles, uint32_t bbox_entries);
 const void* setup_bin_kernel(uint32_t batch, bool mesh);
 void launch_tile(const DrawParams& p, void* stream);
 void launch_clear(const DrawParams& p, void* stream);
 void launch_route(const DrawParams& p, void* stream);
-void launch_setup_split(const DrawParams& p, int pass, void* stream);  // k_setup_bin's halves, 2 launches
-const void* setup_split_kernel(int pass, bool mesh);     // partitioned setup: route own range (2 kernels)
+
 
 }  // namespace zr

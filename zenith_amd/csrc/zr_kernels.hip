@@ -201,14 +201,35 @@ __device__ __forceinline__ EdgeEval eval_edges(const TriRecord& r, int px, int p
     return e;
 }
 
-__device__ __forceinline__ float interp_depth_f(const TriRecord& r, float fw1, float fw2) {
-    const float b1 = fw1 * r.invA2, b2 = fw2 * r.invA2;
-    float z = fmaf(b2, r.dz2, fmaf(b1, r.dz1, r.z0));
-    return z == 0.0f ? 0.0f : z;
+// Depth: a plane in the biased edge values w_i' = w_i - bias_i,
+// z = fmaf(w2', C2, fmaf(w1', C1, Z0)) with C_i = dz_i * invA2 and Z0 = the plane
+// at w' = 0, fmaf(bias2, C2, fmaf(bias1, C1, z0)).  The lane walk steps the
+// biased values, so a sample costs two conversions and two FMAs.  Never -0 (z0
+// is canonical +0 and a sum of nonzero terms that cancels rounds to +0).
+struct DepthPlane {
+    float C1, C2, Z0;
+};
+__device__ __forceinline__ DepthPlane depth_plane(float z0, float dz1, float dz2, float invA2, int b1, int b2) {
+    DepthPlane d;
+    d.C1 = dz1 * invA2;
+    d.C2 = dz2 * invA2;
+    d.Z0 = fmaf((float)b2, d.C2, fmaf((float)b1, d.C1, z0));
+    return d;
 }
+__device__ __forceinline__ float plane_z(const DepthPlane& d, float w1b, float w2b) {
+    return fmaf(w2b, d.C2, fmaf(w1b, d.C1, d.Z0));
+}
+// The top-left bias of the edge from vertex a to vertex b (y-down: an edge is
+// top-left iff dy < 0 || (dy == 0 && dx > 0)); edge i is opposite vertex i.
+__device__ __forceinline__ int edge_bias(int dx, int dy) { return ((dy < 0) || (dy == 0 && dx > 0)) ? 0 : 1; }
 
-__device__ __forceinline__ float interp_depth(const TriRecord& r, long long w1, long long w2) {
-    return interp_depth_f(r, (float)w1, (float)w2);
+// The contract depth of record r at pixel (px, py) (last-wins resolve: no key
+// carries it), from the record's vertices alone.
+__device__ __forceinline__ float winner_depth(const TriRecord& r, int px, int py) {
+    const EdgeEval e = eval_edges(r, px, py);
+    const int b1 = edge_bias(r.X0 - r.X2, r.Y0 - r.Y2), b2 = edge_bias(r.X1 - r.X0, r.Y1 - r.Y0);
+    const DepthPlane d = depth_plane(r.z0, r.dz1, r.dz2, r.invA2, b1, b2);
+    return plane_z(d, (float)(e.w1 - b1), (float)(e.w2 - b2));
 }
 
 // Edge values at a pixel centre as floats (resolve: the winner's barycentrics).
@@ -621,11 +642,10 @@ __device__ __forceinline__ uint32_t mesh_record(const DrawParams& P, uint32_t p,
     return k ? P.prims + 2u * p + k - 1u : p;
 }
 
-// The mesh program's setup of primitive `prim`: fan 0's bbox to *bbox_out, fans
-// 1 and 2's to their global slots (empty when absent).
-__device__ __forceinline__ void setup_finish_mesh(const DrawParams& P, uint32_t prim, uint32_t n_pos, const PrimIn& in,
-                                                  uint32_t* s_hist, BBox* bbox_out, int& nvalid, int& ndropped) {
-    if (prim >= n_pos) return;
+// The mesh program's setup of primitive `prim`: returns fan 0's bbox, stores fans
+// 1 and 2's in their global slots (empty when absent).
+__device__ __forceinline__ BBox setup_finish_mesh(const DrawParams& P, uint32_t prim, const PrimIn& in,
+                                                  uint32_t* s_hist, int& nvalid, int& ndropped) {
     BBox box[kMeshFans];
 #pragma unroll
     for (uint32_t k = 0; k < kMeshFans; ++k) box[k] = BBox{kEmptyBox, 0u};
@@ -673,15 +693,15 @@ __device__ __forceinline__ void setup_finish_mesh(const DrawParams& P, uint32_t 
             }
         }
     }
-    *bbox_out = box[0];
     P.bboxes[mesh_record(P, prim, 1)] = box[1];
     P.bboxes[mesh_record(P, prim, 2)] = box[2];
+    return box[0];
 }
 
-__device__ __forceinline__ void setup_finish(const DrawParams& P, uint32_t prim, uint32_t n_pos, uint32_t gid,
-                                             const PrimIn& in, uint32_t* s_hist, BBox* bbox_out,
-                                             int& nvalid, int& ndropped) {
-    if (prim >= n_pos) return;
+// Setup of position `prim` (the draw primitive, or gid in list mode); returns its
+// tile bbox (empty when culled or owning no tile).
+__device__ __forceinline__ BBox setup_finish(const DrawParams& P, uint32_t prim, uint32_t gid, const PrimIn& in,
+                                             uint32_t* s_hist, int& nvalid, int& ndropped) {
     BBox box{kEmptyBox, 0u};
     PrimGeom g;
     // List mode: the record is indexed by the draw primitive (records are sized
@@ -694,7 +714,7 @@ __device__ __forceinline__ void setup_finish(const DrawParams& P, uint32_t prim,
         ++nvalid;
         if (count_owned(P, g, s_hist)) box = write_record(P, P.list ? gid : prim, g);
     }
-    *bbox_out = box;
+    return box;
 }
 
 // ----------------------------------------------------------------- k_route
@@ -778,116 +798,29 @@ __global__ __launch_bounds__(kRouteThreads) void k_route(DrawParams P) {
     }
 }
 
-// ------------------------------------------------------------ grid barrier
-//
-// Grid barrier of the persistent binning kernel (one workgroup per CU, so every
-// workgroup is resident), XCD-hierarchical as MI355X_MICROARCH.md "barrier-xcd":
-// lane 0 of each workgroup arrives on its group's counter (blockIdx % 8: a group
-// label for workgroups that usually share an XCD; correctness never depends on
-// the placement), the last arrival of a group arrives on the top counter, the
-// last group opens the 8 group flags, and every workgroup polls its group's
-// flag.  Relaxed agent-scope atomics and sc1 polls: nothing handed across the
-// barrier is a plain store (tile counts are atomics, read back with sc1 loads;
-// every bbox phase 4 reads was stored by its own workgroup), so no release /
-// acquire fence -- a release would write back the XCD L2.
-// Bounded: a timeout sets a status word instead of hanging.
-__device__ __forceinline__ void grid_barrier(uint32_t* ctr, uint32_t nwg, uint32_t w, uint32_t* status, bool drain) {
-    // every storing wave drains its stores, unless nothing after the barrier reads
-    // what this workgroup stored before it (drain == false)
-    if (drain) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-    __syncthreads();
-    if (threadIdx.x == 0) {
-        const uint32_t g = w % kBarrierGroups;
-        const uint32_t groups = min(nwg, kBarrierGroups);
-        const uint32_t in_group = nwg / kBarrierGroups + (g < nwg % kBarrierGroups ? 1u : 0u);
-        const uint32_t prev = __hip_atomic_fetch_add(&ctr[kCtGroup + 32u * g], 1u, __ATOMIC_RELAXED,
-                                                     __HIP_MEMORY_SCOPE_AGENT);
-        if (prev + 1u == in_group &&
-            __hip_atomic_fetch_add(&ctr[kCtTop], 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) + 1u == groups) {
-            for (uint32_t k = 0; k < groups; ++k)
-                __hip_atomic_store(&ctr[kCtRelease + 32u * k], 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-        }
-        uint32_t spins = 0;
-        while (__hip_atomic_load(&ctr[kCtRelease + 32u * g], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == 0u) {
-            __builtin_amdgcn_s_sleep(1);
-            if (++spins > (1u << 24)) {  // never expected: report instead of hanging
-                ((volatile uint32_t*)status)[kStBarrierTimeout] = 1u;
-                break;
-            }
-        }
-        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");  // compiler-only: keep loads below the poll
-    }
-    __syncthreads();
-}
-
-// Hand-off words between workgroups of k_setup_bin are written and read with
-// sc1 (agent-scope relaxed atomics): write-through stores, L1-bypassing loads.
-// That is "Valid forms" row 1 of MI355X_MICROARCH.md §Workgroup dispatch, which
-// needs no release/acquire fence -- a release would also write back the XCD
-// L2's freshly written records (hundreds of KB per workgroup).
-__device__ __forceinline__ void st_sc1(uint32_t* p, uint32_t v) {
-    __hip_atomic_store(p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-}
-__device__ __forceinline__ uint32_t ld_sc1(const uint32_t* p) {
-    return __hip_atomic_load(const_cast<uint32_t*>(p), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-}
-
-// Exclusive scan of a[0..n) in LDS by a 1024-thread workgroup; returns the total.
-__device__ __forceinline__ uint32_t block_exclusive_scan(uint32_t* a, uint32_t n, uint32_t* s_wave) {
-    const uint32_t tid = threadIdx.x;
-    const uint32_t per = (n + 1023u) / 1024u;
-    const uint32_t beg = min(tid * per, n), end = min(beg + per, n);
-    uint32_t sum = 0;
-    for (uint32_t i = beg; i < end; ++i) sum += a[i];
-    const int lane = tid & 63, wave = tid >> 6;
-    uint32_t incl = sum;
-#pragma unroll
-    for (int d = 1; d < 64; d <<= 1) {
-        const uint32_t v = __shfl_up(incl, d, 64);
-        if (lane >= d) incl += v;
-    }
-    if (lane == 63) s_wave[wave] = incl;
-    __syncthreads();
-    if (tid < 16) {
-        const uint32_t w = s_wave[tid];
-        uint32_t wi = w;
-#pragma unroll
-        for (int d = 1; d < 16; d <<= 1) {
-            const uint32_t v = __shfl_up(wi, d, 16);
-            if ((int)tid >= d) wi += v;
-        }
-        s_wave[tid] = wi - w;
-        if (tid == 15) s_wave[16] = wi;
-    }
-    __syncthreads();
-    uint32_t run = s_wave[wave] + incl - sum;
-    for (uint32_t i = beg; i < end; ++i) {
-        const uint32_t c = a[i];
-        a[i] = run;
-        run += c;
-    }
-    const uint32_t total = s_wave[16];
-    __syncthreads();
-    return total;
-}
-
 // ----------------------------------------------------------- k_setup_bin
 //
-// One persistent launch, one 1024-thread workgroup per CU (fewer for small draws):
+// One launch, one 1024-thread workgroup per CU (fewer for small draws), no grid
+// barrier (workgroups never wait for each other, so nothing assumes they are
+// co-resident):
 //   phase 1  vertex stage + setup in units of 64 * KB * rounds primitives, one
-//            wave per unit (units assigned statically, P.setup_sched); records and
-//            tile bboxes to HBM, pairs counted in an LDS histogram of all tiles
+//            wave per unit (units assigned statically); records and tile bboxes
+//            to HBM (bboxes also to LDS when they fit), pairs counted in an LDS
+//            histogram of all tiles
 //   phase 2  the histogram is added into the global per-tile counters with
 //            returning atomics (a wave's adds to consecutive tiles leave L2 as
 //            64-B requests); the value returned is this workgroup's offset inside
-//            each tile's list.  Order inside a tile's list is therefore arbitrary,
-//            which is free: visibility keys carry the primitive sequence (k_tile).
-//   -- grid barrier --
-//   phase 3  tile bases (exclusive scan of the totals, redundantly per workgroup);
-//            LDS cursors = base[t] + own offset[t]
-//   phase 4  scatter the workgroup's (tile, primitive) pairs through the cursors.
-// The last workgroup to finish returns the tile counters and the grid counters to
-// zero, so a draw needs no memset.
+//            the tile's list
+//   phase 4  scatter the workgroup's (tile, primitive) pairs straight into the
+//            tile's slab: tile t's list lives at bins[t * slab, (t + 1) * slab),
+//            so a list start needs no scan of the totals (the round-1 design's
+//            grid barrier + phase 3 scan cost ~6 us of a C2 frame).  Pairs past a
+//            full slab are dropped and counted: k_tile rasterizes that tile
+//            exactly by scanning every record's bbox, and the runtime grows the
+//            bin buffer at the next sync point.
+// Order inside a tile's list is arbitrary (whatever order the atomics returned),
+// which is free: visibility keys carry the primitive sequence (k_tile).  The
+// counters return to zero in k_tile, so a draw needs no memset.
 #define ZR_STAMP(i)                                                                         \
     do {                                                                                    \
         if ((P.debug & kDebugStamps) && tid == 0) P.dbg_ts[w * 8 + (i)] = __builtin_amdgcn_s_memrealtime(); \
@@ -898,22 +831,15 @@ __device__ __forceinline__ uint32_t block_exclusive_scan(uint32_t* a, uint32_t n
 // blocks per workgroup measured slower: C4 setup 286 vs 339 us).
 __device__ __forceinline__ uint32_t own_unit(uint32_t w, uint32_t G, uint32_t i) { return w + i * G; }
 
-// PASS 0: the whole persistent kernel.  PASS 1 / 2: its halves on either side of
-// the grid barrier as two launches (no co-residency needed, so the first half of
-// draw i+1 can fill CUs the tile pass of draw i frees): pass 1
-// leaves each workgroup's per-tile offsets in P.wg_offsets and the bboxes in
-// P.bboxes, pass 2 reloads them.
-template <uint32_t KB, bool MESH, int PASS>
+template <uint32_t KB, bool MESH>
 __global__ __launch_bounds__(kSetupThreads) void k_setup_bin(DrawParams P) {
-    extern __shared__ __attribute__((aligned(16))) uint32_t s_lds[];  // [2 * ntiles + kSetupMiscWords] + bboxes
+    extern __shared__ __attribute__((aligned(16))) uint32_t s_lds[];  // [ntiles (16-B padded) + kSetupMiscWords] + bboxes
     const uint32_t nt = P.ntiles, G = gridDim.x, w = blockIdx.x, tid = threadIdx.x;
-    uint32_t* s_hist = s_lds;            // histogram -> own offsets -> cursors
-    uint32_t* s_base = s_lds + nt;       // tile totals -> tile bases
-    uint32_t* s_misc = s_base + nt;      // [32]
+    uint32_t* s_hist = s_lds;                       // histogram -> cursors
+    uint32_t* s_misc = s_hist + ((nt + 3u) & ~3u);  // [32]
     uint32_t* s_pre = s_misc + 32;       // list mode: exclusive prefix of the received blocks' counts
     // this workgroup's primitives' tile bboxes, indexed like phase 4's flattened
-    // (own unit, primitive in unit) space, when they fit (P.bbox_lds): then
-    // nothing read after the grid barrier depends on phase 1's global stores
+    // (own unit, primitive in unit) space, when they fit (P.bbox_lds)
     BBox* s_bbox = reinterpret_cast<BBox*>(s_misc + kSetupMiscWords);
     ZR_STAMP(0);
     for (uint32_t t = tid; t < nt; t += kSetupThreads) s_hist[t] = 0;
@@ -931,10 +857,12 @@ __global__ __launch_bounds__(kSetupThreads) void k_setup_bin(DrawParams P) {
     // the received blocks, in units of 2^unit_shift
     const uint32_t n_pos = P.list ? min(s_pre[P.shard_count], P.prims) : P.prims;
     const uint32_t units = P.list ? (n_pos + (1u << P.unit_shift) - 1u) >> P.unit_shift : P.units;
+    // records k_tile's overflow scan covers
+    if (w == 0 && tid == 0) P.draw_info[kInfoRecords] = MESH ? kMeshFans * n_pos : n_pos;
 
     // ---- phase 1
     int nvalid = 0, ndropped = 0;
-    if (PASS != 2) {
+    {
         const DrawParams& P = kernarg_params();  // phase 1's own loads of the parameters (SGPR pressure)
         const uint32_t lane = tid & 63u, wave = tid >> 6;
         const uint32_t rounds = (1u << P.unit_shift) / (64u * KB);
@@ -963,12 +891,16 @@ __global__ __launch_bounds__(kSetupThreads) void k_setup_bin(DrawParams P) {
 #endif
 #pragma unroll
                 for (uint32_t b = 0; b < KB; ++b) {
-                    const uint32_t prim = min(pb + b * 64u, n_pos);
-                    BBox* out = P.bbox_lds ? &s_bbox[lb + b * 64u] : &P.bboxes[min(prim, P.prims - 1u)];
-                    if (MESH)
-                        setup_finish_mesh(P, prim, n_pos, in[b], s_hist, out, nvalid, ndropped);
+                    const uint32_t prim = pb + b * 64u;
+                    if (prim >= n_pos) continue;
+                    BBox box;
+                    if constexpr (MESH)
+                        box = setup_finish_mesh(P, prim, in[b], s_hist, nvalid, ndropped);
                     else
-                        setup_finish(P, prim, n_pos, gid[b], in[b], s_hist, out, nvalid, ndropped);
+                        box = setup_finish(P, prim, gid[b], in[b], s_hist, nvalid, ndropped);
+                    // global: the overflow scan of any tile may need it; LDS: phase 4
+                    P.bboxes[prim] = box;
+                    if (P.bbox_lds) s_bbox[lb + b * 64u] = box;
                 }
             }
         }
@@ -979,78 +911,49 @@ __global__ __launch_bounds__(kSetupThreads) void k_setup_bin(DrawParams P) {
     ZR_STAMP(1);
     if (P.debug & kDebugPhase1Only) return;
 
-    if (PASS != 2) {
+    // ---- phase 2: reserve this workgroup's slots in every tile's list; the
+    // cursor of tile t becomes t * slab + the offset the atomic returned.  Each
+    // workgroup starts at a different 64-tile block so that the workgroups' adds
+    // spread over the counter lines instead of all queueing on the same ones.
+    {
         const DrawParams& P = kernarg_params();
-        // ---- phase 2: reserve this workgroup's slots in every tile's list.  Each
-        // workgroup starts at a different 64-tile block so that the workgroups' adds
-        // spread over the counter lines instead of all queueing on the same ones.
         const uint32_t rot = nt ? ((w * 64u) % nt) : 0u;
+        uint32_t top = 0, sum = 0;  // the largest tile count this workgroup saw, its pairs
         for (uint32_t i = tid; i < nt; i += kSetupThreads) {
             const uint32_t t = i + rot < nt ? i + rot : i + rot - nt;
             const uint32_t c = s_hist[t];
-            s_hist[t] = c ? __hip_atomic_fetch_add(&P.tile_counts[t], c, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) : 0u;
+            const uint32_t o = c ? __hip_atomic_fetch_add(&P.tile_counts[t], c, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) : 0u;
+            s_hist[t] = t * P.slab + o;
+            top = max(top, o + c);
+            sum += c;
         }
+#pragma unroll
+        for (int o = 32; o > 0; o >>= 1) {
+            top = max(top, (uint32_t)__shfl_xor((int)top, o, 64));
+            sum += (uint32_t)__shfl_xor((int)sum, o, 64);
+        }
+        if ((tid & 63u) == 0) {
+            if (top) atomicMax(&s_misc[2], top);
+            if (sum) atomicAdd(&s_misc[3], sum);
+        }
+        __syncthreads();
         if (tid == 0) {
             if (s_misc[0]) atomicAdd(&P.counters[kCtSetup], s_misc[0]);
             if (s_misc[1]) atomicAdd(&P.counters[kCtDropped], s_misc[1]);
+            if (s_misc[2]) atomicMax(&P.counters[kCtMaxTile], s_misc[2]);
+            if (s_misc[3]) atomicAdd(reinterpret_cast<unsigned long long*>(&P.counters[kCtPairs]), (unsigned long long)s_misc[3]);
         }
     }
     ZR_STAMP(2);
-    if (PASS == 1) {  // the second launch continues from here
-        __syncthreads();
-        for (uint32_t t = tid; t < nt; t += kSetupThreads) P.wg_offsets[(size_t)w * nt + t] = s_hist[t];
-        return;
-    }
-    if (PASS == 0) grid_barrier(P.counters, G, w, P.status, !P.bbox_lds);
-    if (PASS == 2) {
-        for (uint32_t t = tid; t < nt; t += kSetupThreads) s_hist[t] = P.wg_offsets[(size_t)w * nt + t];
-        __syncthreads();
-    }
-    ZR_STAMP(3);
-    if (P.debug & kDebugStopAfterScan) return;
-
-    // ---- phase 3: tile bases and this workgroup's cursors.  The pair total is
-    // also summed in 64 bits: a draw of 2^32 pairs or more would wrap the u32 tile
-    // offsets, so it reports a total past any bin capacity instead (spill path).
-    unsigned long long* s_total64 = reinterpret_cast<unsigned long long*>(s_misc + 26);
-    if (tid == 0) *s_total64 = 0ull;
+    if (!P.bbox_lds) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // phase 4 reads the global bboxes
     __syncthreads();
-    {
-        unsigned long long part = 0;
-        for (uint32_t t = tid; t < nt; t += kSetupThreads) {
-            const uint32_t c = ld_sc1(&P.tile_counts[t]);
-            s_base[t] = c;
-            part += c;
-        }
-#pragma unroll
-        for (int o = 32; o > 0; o >>= 1) part += __shfl_xor(part, o, 64);
-        if ((tid & 63u) == 0 && part) atomicAdd(s_total64, part);
-    }
-    __syncthreads();
-    const bool wrapped = *s_total64 > 0xFFFFFFFFull;
-    uint32_t total = block_exclusive_scan(s_base, nt, s_misc + 8);
-    if (wrapped) total = 0xFFFFFFFFu;
-    if (w == 0) {
-        for (uint32_t t = tid; t < nt; t += kSetupThreads) P.tile_offsets[t] = s_base[t];
-        if (tid == 0) {
-            P.tile_offsets[nt] = total;
-            P.tile_offsets[nt + 1] = MESH ? kMeshFans * n_pos : n_pos;  // records k_tile's overflow scan covers
-            volatile uint32_t* st = P.status;
-            st[kStTotalPairs] = total;
-            if (total > P.bin_capacity) st[kStOverflow] += 1u;  // draws run in stream order
-            if (total > st[kStMaxPairs]) st[kStMaxPairs] = total;
-        }
-    }
-    for (uint32_t t = tid; t < nt; t += kSetupThreads) s_hist[t] += s_base[t];
-    __syncthreads();
-    ZR_STAMP(4);
 
     // ---- phase 4: scatter the pairs of this workgroup's units, flattened over
     // (own unit, primitive in unit) so every thread has work
     {
         const DrawParams& P = kernarg_params();
         const uint32_t usz = 1u << P.unit_shift;
-        // appends (tile, record) pairs of one setup record to its owned tiles' lists
+        // appends (tile, record) pairs of one setup record to its owned tiles' slabs
         auto scatter = [&](uint32_t rec, const BBox bb) {
             if (bb.bb0 == kEmptyBox) return;
             const int tx0 = (int)(bb.bb0 & 0xFFFFu) >> kTileShift, tx1 = (int)(bb.bb1 & 0xFFFFu) >> kTileShift;
@@ -1065,8 +968,9 @@ __global__ __launch_bounds__(kSetupThreads) void k_setup_bin(DrawParams P) {
                     const int cx1 = min((int)(bb.bb1 & 0xFFFFu), (tx << kTileShift) + kTile - 1);
                     const uint32_t area = (uint32_t)((cx1 - cx0 + 1) * (cy1 - cy0 + 1));
                     const uint32_t bucket = min((area - 1u) >> 2, kSortBuckets - 1u);
-                    const uint32_t pos = atomicAdd(&s_hist[r + tx], 1u);
-                    if (pos < P.bin_capacity) P.bins[pos] = rec | (bucket << kBinPrimBits);
+                    const uint32_t t = r + (uint32_t)tx;
+                    const uint32_t pos = atomicAdd(&s_hist[t], 1u);
+                    if (pos - t * P.slab < P.slab) P.bins[pos] = rec | (bucket << kBinPrimBits);
                 }
             }
         };
@@ -1076,8 +980,6 @@ __global__ __launch_bounds__(kSetupThreads) void k_setup_bin(DrawParams P) {
             const uint32_t prim = (own_unit(w, G, j >> P.unit_shift) << P.unit_shift) + (j & (usz - 1u));
             if (prim >= n_pos) continue;
             const BBox bb = P.bbox_lds ? s_bbox[j] : P.bboxes[prim];
-            // overflowed draw: k_tile rasterizes by scanning every record's bbox
-            if (P.bbox_lds && total > P.bin_capacity) P.bboxes[prim] = bb;
             scatter(P.list && bb.bb0 != kEmptyBox ? P.gids[prim] : prim, bb);
             if (MESH) {  // fans 1 and 2 (bboxes stored by this workgroup in phase 1)
                 scatter(mesh_record(P, prim, 1), P.bboxes[mesh_record(P, prim, 1)]);
@@ -1086,9 +988,6 @@ __global__ __launch_bounds__(kSetupThreads) void k_setup_bin(DrawParams P) {
         }
     }
     ZR_STAMP(5);
-    // The counters go back to zero in k_tile (it runs after every workgroup here
-    // read them): an exit fan-in of all workgroups on one counter cost ~3 us.
-    ZR_STAMP(6);
 }
 
 // ------------------------------------------------------------------- k_tile
@@ -1205,13 +1104,14 @@ __device__ __forceinline__ void raster_prim(const DrawParams& P, const TriRecord
     const int rows = 64 >> sh;
     const int lx = lane & ((1 << sh) - 1), lyo = lane >> sh;
     const long long bias0 = (r.flags >> 1) & 1, bias1 = (r.flags >> 2) & 1, bias2 = (r.flags >> 3) & 1;
+    const DepthPlane dp = depth_plane(r.z0, r.dz1, r.dz2, r.invA2, (int)bias1, (int)bias2);
     for (int ry = 0; ry < bh; ry += rows) {
         const int ly = ry + lyo;
         if (lx < bw && ly < bh) {
             const int px = bx0 + lx, py = by0 + ly;
             const EdgeEval e = eval_edges(r, px, py);
             if (e.w0 >= bias0 && e.w1 >= bias1 && e.w2 >= bias2) {
-                const float z = interp_depth(r, e.w1, e.w2);
+                const float z = plane_z(dp, (float)(e.w1 - bias1), (float)(e.w2 - bias2));
                 if (z >= P.dlo && z <= P.dhi) {
                     const int li = (py - y0) * kTile + (px - x0);
                     if (!INITD || depth_pass(P.depth_op, z, s_initd[li]))
@@ -1250,10 +1150,10 @@ __device__ __forceinline__ void raster_lane(const DrawParams& P, const TriRecord
     // the end of a row the jump back to the next row's first pixel, chosen with
     // selects (no divergent branch: a nested row / column loop, or a wrap branch,
     // idles the lanes of narrower primitives and measured slower).  The top-left
-    // bias is folded into the edge values, so coverage is one sign test; depth adds
-    // it back.  Fragment depth is never -0 here: setup canonicalised the vertex
-    // depths to +0 (the oracle's per-fragment -0 -> +0 rule therefore gives the
-    // same bits).  The sweep ends when the key address reaches the row after the
+    // bias is folded into the edge values, so coverage is one sign test, and the
+    // depth plane is defined on the biased values (§3.6).  Fragment depth is never
+    // -0 here: setup canonicalised the vertex depths to +0 (the oracle's
+    // per-fragment -0 -> +0 rule therefore gives the same bits).  The sweep ends when the key address reaches the row after the
     // last one (no separate step counter).
     const int rows = (bh - sub + k - 1) >> ksh;
     const int j0 = k * sy0 - (bw - 1) * sx0, j1 = k * sy1 - (bw - 1) * sx1, j2 = k * sy2 - (bw - 1) * sx2;
@@ -1269,9 +1169,9 @@ __device__ __forceinline__ void raster_lane(const DrawParams& P, const TriRecord
     const float z1v = z0 + dz1, z2v = z0 + dz2, zlo = P.dlo + 1e-4f, zhi = P.dhi - 1e-4f;
     const bool zsafe = z0 >= zlo && z0 <= zhi && z1v >= zlo && z1v <= zhi && z2v >= zlo && z2v <= zhi;
     // one covered sample: depth from the (un-biased) edge values, test, key
+    const DepthPlane dp = depth_plane(z0, dz1, dz2, invA2, b1, b2);
     auto frag = [&](auto ztest, int e1, int e2, uint32_t a) {
-        const float fb1 = (float)(e1 + b1) * invA2, fb2 = (float)(e2 + b2) * invA2;
-        const float z = fmaf(fb2, dz2, fmaf(fb1, dz1, z0));
+        const float z = plane_z(dp, (float)e1, (float)e2);  // e1, e2: the biased values
         if ((!decltype(ztest)::value || (z >= P.dlo && z <= P.dhi)) &&
             (!INITD || depth_pass(P.depth_op, z, s_initd[a >> 3])))
             atomicMin(reinterpret_cast<unsigned long long*>(reinterpret_cast<char*>(s_key) + a), frag_key<MODE>(z, seq));
@@ -1496,7 +1396,7 @@ __device__ __forceinline__ void resolve_pixels(const DrawParams& P, int x0, int 
                     if constexpr (PROG == kProgMesh) shade_mesh(P, gp[b], vid[b], px[b], py[b], col[b]);
                     else shade_winner<PROG>(P, r, e, col[b]);
                 }
-                zw[b] = (MODE == kDepthLastWins) ? interp_depth_f(r, e.f1, e.f2) : key_depth<MODE>(key[b]);
+                zw[b] = (MODE == kDepthLastWins) ? winner_depth(r, px[b], py[b]) : key_depth<MODE>(key[b]);
             }
         } else {
 #pragma unroll
@@ -1647,7 +1547,7 @@ __device__ __forceinline__ void shade_from_lds(const DrawParams& P, const float*
             if (large) r = P.records_big[g.x];
         }
         e = eval_edges_f(r, px, py);
-        if (L::kZ) zw = interp_depth_f(r, e.f1, e.f2);
+        if (L::kZ) zw = winner_depth(r, px, py);
     }
     const float* a = w + L::kAttrOff;
     out[3] = 1.0f;
@@ -1862,20 +1762,16 @@ __global__ __launch_bounds__(NT, ZR_TILE_WGS * kTileThreads / 256) void k_tile(D
     unsigned long long* ts = P.dbg_ts + 8192 * 8 + (size_t)t * 8;
     if (stamp) ts[0] = __builtin_amdgcn_s_memrealtime();
 
-    // The tile's list bounds and its first segment of bin entries are requested
-    // before anything else: workgroups dispatched last would otherwise queue these
-    // loads behind the record gathers of every tile that started earlier.
-    const uint32_t begin = P.tile_offsets[t], end = P.tile_offsets[t + 1];
-    // A draw with more pairs than the bin buffer holds (the runtime grows it for
-    // later draws) is rasterized exactly but slowly: every tile scans all records'
-    // bboxes (k_setup_bin stored them) instead of reading its list.
-    const bool spill = P.tile_offsets[P.ntiles] > P.bin_capacity;
-    const uint32_t cnt = spill ? 0u : end - begin;
-    const uint32_t lbeg = begin;
+    // The tile's first segment of bin entries is requested before anything else
+    // (workgroups dispatched last would otherwise queue these loads behind the
+    // record gathers of every tile that started earlier), in parallel with its
+    // count: the list lives at a fixed slab, bins[t * slab, ...), so the loads need
+    // not wait for it; entries past the count are never used.
+    const uint32_t slab = P.slab;
+    const uint32_t lbeg = t * slab;
     constexpr uint32_t kPerThread = kSortCap / NT;
     uint32_t ent[kPerThread];
-    auto load_segment = [&](uint32_t seg) {
-        const uint32_t n = min(kSortCap, cnt - seg);
+    auto load_segment = [&](uint32_t seg, uint32_t n) {
         // the segment's base as a uniform (scalar) pointer: lane addresses then come
         // from threadIdx alone instead of per-lane bases held (spilled) across the pass
         const uint32_t* bp = P.bins + lbeg + seg;
@@ -1886,7 +1782,13 @@ __global__ __launch_bounds__(NT, ZR_TILE_WGS * kTileThreads / 256) void k_tile(D
             ent[k] = i < n ? bp[i] : 0u;  // prim | area bucket (k_setup_bin phase 4)
         }
     };
-    if (cnt && !(tile_debug(P) & kDebugSkipRaster)) load_segment(0);
+    if (!(tile_debug(P) & kDebugSkipRaster)) load_segment(0, min(kSortCap, slab));
+    const uint32_t count = P.tile_counts[t];
+    // A tile whose list outgrew its slab (the runtime grows the bin buffer for
+    // later draws) is rasterized exactly but slowly: it scans every record's bbox
+    // (k_setup_bin stored them all) instead of reading its list.
+    const bool spill = count > slab;
+    const uint32_t cnt = spill ? 0u : count;
 
     for (int i = threadIdx.x; i < kTilePixels; i += NT) {
         const int px = x0 + (i & (kTile - 1)), py = y0 + (i >> kTileShift);
@@ -1897,16 +1799,27 @@ __global__ __launch_bounds__(NT, ZR_TILE_WGS * kTileThreads / 256) void k_tile(D
     }
     if (threadIdx.x < 255) s_srgb[threadIdx.x] = c_srgbT[threadIdx.x];
     if (threadIdx.x < 2) s_dbg[threadIdx.x] = 0u;
-    // k_setup_bin's counters back to zero for the next draw on this scratch set
-    // (the tile lists live in tile_offsets / bins): each tile its own count,
-    // tile 0 the grid counters, after reporting the draw's primitive stats
-    if (threadIdx.x == 0) P.tile_counts[t] = 0u;
+    // tile 0 reports the draw's setup and binning stats (k_setup_bin's counters,
+    // complete before this launch) and flags a slab overflow to the runtime
     if (t == 0 && threadIdx.x == 0) {
         volatile uint32_t* st = P.status;
+        const uint32_t top = P.counters[kCtMaxTile];
+        const unsigned long long pairs = *reinterpret_cast<const unsigned long long*>(&P.counters[kCtPairs]);
         st[kStTrianglesSetup] = P.counters[kCtSetup];
         st[kStDroppedClip] = P.counters[kCtDropped];
+        st[kStTotalPairs] = pairs > 0xFFFFFFFFull ? 0xFFFFFFFFu : (uint32_t)pairs;
+        if (top > slab) {  // draws run in stream order
+            st[kStOverflow] += 1u;
+            const unsigned long long need = (unsigned long long)top * P.ntiles;  // bin entries for slabs of `top`
+            const uint32_t need32 = need > 0x80000000ull ? 0x80000000u : (uint32_t)need;
+            if (need32 > st[kStMaxPairs]) st[kStMaxPairs] = need32;
+        }
     }
     __syncthreads();
+    // k_setup_bin's counters back to zero for the next draw on this scratch set:
+    // each tile its own count (every wave has read it: the barrier above), tile 0
+    // the draw counters
+    if (threadIdx.x == 0) P.tile_counts[t] = 0u;
     if (t == 0)
         for (uint32_t i = threadIdx.x; i < kCtWords; i += NT) P.counters[i] = 0u;
 
@@ -1921,7 +1834,7 @@ __global__ __launch_bounds__(NT, ZR_TILE_WGS * kTileThreads / 256) void k_tile(D
         // lane per entry loads the 64-B record, and the wave walks the chunk.
         for (uint32_t seg = 0; seg < cnt; seg += kSortCap) {
             const uint32_t n = min(kSortCap, cnt - seg);
-            if (seg) load_segment(seg);
+            if (seg) load_segment(seg, n);
             const DrawParams& P = kernarg_params();  // re-loaded per segment, not held across the pass
             if (threadIdx.x < kSortBuckets) s_bucket[threadIdx.x] = 0u;
             if (threadIdx.x == 0) s_claim = s_nbig = s_bclaim = 0u;
@@ -2097,7 +2010,7 @@ __global__ __launch_bounds__(NT, ZR_TILE_WGS * kTileThreads / 256) void k_tile(D
             __syncthreads();
         }
         if (spill) {
-            const uint32_t r0 = 0u, n_rec = P.tile_offsets[P.ntiles + 1];  // setup records of the draw
+            const uint32_t r0 = 0u, n_rec = P.draw_info[kInfoRecords];  // setup records of the draw
             for (uint32_t cb = r0 + wave * 64u; cb < n_rec; cb += NT) {
                 const uint32_t j = cb + (uint32_t)lane;
                 bool hit = false;
@@ -2171,53 +2084,29 @@ __global__ __launch_bounds__(kTileThreads) void k_clear(DrawParams P) {
 static inline uint32_t blocks_for(uint32_t n, uint32_t per) { return (n + per - 1) / per; }
 
 size_t setup_bin_lds_bytes(uint32_t ntiles, uint32_t bbox_entries) {
-    return (2 * (size_t)ntiles + kSetupMiscWords) * sizeof(uint32_t) + (size_t)bbox_entries * sizeof(BBox);
+    return (((size_t)ntiles + 3u) / 4u * 4u + kSetupMiscWords) * sizeof(uint32_t) + (size_t)bbox_entries * sizeof(BBox);
 }
 
 const void* setup_bin_kernel(uint32_t batch, bool mesh) {
-    if (mesh) return reinterpret_cast<const void*>(&k_setup_bin<1, true, 0>);
+    if (mesh) return reinterpret_cast<const void*>(&k_setup_bin<1, true>);
     switch (batch) {
-    case 1: return reinterpret_cast<const void*>(&k_setup_bin<1, false, 0>);
-    case 2: return reinterpret_cast<const void*>(&k_setup_bin<2, false, 0>);
-    default: return reinterpret_cast<const void*>(&k_setup_bin<4, false, 0>);
+    case 1: return reinterpret_cast<const void*>(&k_setup_bin<1, false>);
+    case 2: return reinterpret_cast<const void*>(&k_setup_bin<2, false>);
+    default: return reinterpret_cast<const void*>(&k_setup_bin<4, false>);
     }
-}
-
-const void* setup_split_kernel(int pass, bool mesh) {
-    if (mesh)
-        return pass == 1 ? reinterpret_cast<const void*>(&k_setup_bin<1, true, 1>)
-                         : reinterpret_cast<const void*>(&k_setup_bin<1, true, 2>);
-    return pass == 1 ? reinterpret_cast<const void*>(&k_setup_bin<2, false, 1>)
-                     : reinterpret_cast<const void*>(&k_setup_bin<2, false, 2>);
-}
-
-void launch_setup_split(const DrawParams& p, int pass, void* stream) {
-    const size_t lds = setup_bin_lds_bytes(p.ntiles, 0);
-    const hipStream_t s = (hipStream_t)stream;
-    if (p.program == kProgMesh) {  // batch 1, as the persistent mesh instance
-        if (pass == 1)
-            hipLaunchKernelGGL((k_setup_bin<1, true, 1>), dim3(p.setup_wgs), dim3(kSetupThreads), lds, s, p);
-        else
-            hipLaunchKernelGGL((k_setup_bin<1, true, 2>), dim3(p.setup_wgs), dim3(kSetupThreads), lds, s, p);
-        return;
-    }
-    if (pass == 1)
-        hipLaunchKernelGGL((k_setup_bin<2, false, 1>), dim3(p.setup_wgs), dim3(kSetupThreads), lds, s, p);
-    else
-        hipLaunchKernelGGL((k_setup_bin<2, false, 2>), dim3(p.setup_wgs), dim3(kSetupThreads), lds, s, p);
 }
 
 void launch_setup_bin(const DrawParams& p, void* stream) {
     const size_t lds = setup_bin_lds_bytes(p.ntiles, p.bbox_lds);
     const hipStream_t s = (hipStream_t)stream;
     if (p.program == kProgMesh) {  // batch 1: the clip path is heavy
-        hipLaunchKernelGGL((k_setup_bin<1, true, 0>), dim3(p.setup_wgs), dim3(kSetupThreads), lds, s, p);
+        hipLaunchKernelGGL((k_setup_bin<1, true>), dim3(p.setup_wgs), dim3(kSetupThreads), lds, s, p);
         return;
     }
     switch (p.setup_batch) {
-    case 1: hipLaunchKernelGGL((k_setup_bin<1, false, 0>), dim3(p.setup_wgs), dim3(kSetupThreads), lds, s, p); break;
-    case 2: hipLaunchKernelGGL((k_setup_bin<2, false, 0>), dim3(p.setup_wgs), dim3(kSetupThreads), lds, s, p); break;
-    default: hipLaunchKernelGGL((k_setup_bin<4, false, 0>), dim3(p.setup_wgs), dim3(kSetupThreads), lds, s, p); break;
+    case 1: hipLaunchKernelGGL((k_setup_bin<1, false>), dim3(p.setup_wgs), dim3(kSetupThreads), lds, s, p); break;
+    case 2: hipLaunchKernelGGL((k_setup_bin<2, false>), dim3(p.setup_wgs), dim3(kSetupThreads), lds, s, p); break;
+    default: hipLaunchKernelGGL((k_setup_bin<4, false>), dim3(p.setup_wgs), dim3(kSetupThreads), lds, s, p); break;
     }
 }
 

@@ -191,8 +191,8 @@ struct ScratchSet {
     uint64_t bboxes_cap = 0;
     uint32_t* tile_counts = nullptr;
     uint64_t tiles_cap = 0;
-    uint32_t* tile_offsets = nullptr;
-    uint64_t tiles_cap2 = 0;
+    uint32_t* draw_info = nullptr;  // k_setup_bin -> k_tile (kInfoWords)
+    uint64_t draw_info_cap = 0;
     uint32_t* counters = nullptr;
     uint64_t counters_cap = 0;
     uint32_t* bins = nullptr;
@@ -205,8 +205,6 @@ struct ScratchSet {
     uint64_t gids_cap = 0;
     uint32_t* rcounts = nullptr;// route: ids per destination block + finished workgroups
     uint64_t rcounts_cap = 0;
-    uint32_t* wg_offsets = nullptr;  // split setup: per-workgroup tile offsets
-    uint64_t wg_offsets_cap = 0;
     hipEvent_t setup_done = nullptr;  // k_setup_bin of the last draw that used this set
     hipEvent_t tile_done = nullptr;   // k_tile of the last draw that used this set
     bool tile_done_valid = false;
@@ -226,13 +224,14 @@ struct zr_device_t {
     ScratchSet sets[2];
     uint32_t cur_set = 0;
     hipStream_t setup_stream = nullptr;
-    // k_setup_bin as two launches split at its grid barrier, on the setup stream,
-    // so draw i+1's setup fills CUs draw i's tile pass frees.  Measured (1 GPU):
-    // C1 (100k tris) 1180 -> 1274 Mtri/s, C2 7925 -> 8007, C3 equal, C4 (10M)
-    // 25.1 -> 23.8 G (the co-running passes contend), so by default only draws of
-    // <= 2^18 primitives split, and tile-row shards (whose tile pass leaves most
-    // CUs idle: C2 G=2/4/8 +2.8/+2.3/+0.7 %, C3 G=8 +7 %).  ZR_SETUP_SPLIT=0 / 1 forces it off / on.
-    int setup_split = -1;
+    // k_setup_bin on the setup stream (two scratch sets), so draw i+1's setup
+    // fills CUs draw i's tile pass frees.  Measured with round 1's two-launch
+    // split setup (1 GPU): C1 (100k tris) 1180 -> 1274 Mtri/s, C2 7925 -> 8007,
+    // C3 equal, C4 (10M) 25.1 -> 23.8 G (the co-running passes contend), so by
+    // default only draws of <= 2^18 primitives overlap, and tile-row shards (whose
+    // tile pass leaves most CUs idle: C2 G=2/4/8 +2.8/+2.3/+0.7 %, C3 G=8 +7 %).
+    // ZR_SETUP_OVERLAP=0 / 1 forces it off / on.
+    int setup_overlap = -1;
     int cu_count = 0;
     uint32_t occupancy_checked_tiles = 0;
     bool occupancy_checked_mesh = false;
@@ -428,17 +427,13 @@ zr_result device_sync(zr_device* d) {
     d->overflowed_draws += st[kStOverflow];
     d->last.overflowed_draws = d->overflowed_draws;
     d->pending.clear();
-    if (st[kStBarrierTimeout]) {
-        st[kStBarrierTimeout] = 0;
-        return fail(ZR_ERROR_DEVICE_LOST, "k_setup_bin grid barrier timed out (workgroups not co-resident)");
-    }
     if (d->dbg_ts && !d->dbg_ts_path.empty()) dump_stamps(d);
     if (st[kStOverflow]) {
-        // Draws with more (tile, primitive) pairs than the bin buffer holds were
-        // rasterized exactly by k_tile's scan of all records (slow); size the
-        // buffer for the largest draw seen so later draws read tile lists again.
-        // (capped at 2^30 entries, 4 GiB: a larger draw -- k_setup_bin reports a
-        // wrapped 2^32 total as 0xFFFFFFFF -- keeps using the exact spill path)
+        // Draws with a tile list longer than its slab (bin buffer / tiles) had that
+        // tile rasterized exactly by k_tile's scan of all records (slow); size the
+        // buffer so that every tile of the largest such draw gets a slab of its
+        // longest list, and later draws read tile lists again.  (Capped at 2^30
+        // entries, 4 GiB: a larger draw keeps using the exact spill path.)
         const uint64_t need = std::min<uint64_t>((uint64_t)st[kStMaxPairs] * 5 / 4 + 4096, 1ull << 30);
         st[kStOverflow] = 0;
         d->min_bins = std::max(d->min_bins, need);  // also for a scratch set not allocated yet
@@ -551,7 +546,7 @@ zr_result ensure_scratch(zr_device* d, ScratchSet& S, DrawParams& P) {
         if ((rc = grow(d, S.tile_counts, S.tiles_cap, P.ntiles + 1, 4))) return rc;
         if (S.tiles_cap != cap) ZR_HIP(hipMemset(S.tile_counts, 0, S.tiles_cap * 4));
     }
-    if ((rc = grow(d, S.tile_offsets, S.tiles_cap2, P.ntiles + 2, 4))) return rc;
+    if ((rc = grow(d, S.draw_info, S.draw_info_cap, kInfoWords, 4))) return rc;
     if (!S.counters) {  // zeroed once; k_setup_bin leaves them zero after every draw
         if ((rc = grow(d, S.counters, S.counters_cap, kCtWords, 4))) return rc;
         ZR_HIP(hipMemset(S.counters, 0, S.counters_cap * 4));
@@ -569,10 +564,11 @@ zr_result ensure_scratch(zr_device* d, ScratchSet& S, DrawParams& P) {
     P.mesh_edges = S.mesh_edges;
     P.bboxes = S.bboxes;
     P.tile_counts = S.tile_counts;
-    P.tile_offsets = S.tile_offsets;
+    P.draw_info = S.draw_info;
     P.counters = S.counters;
     P.bins = S.bins;
-    P.bin_capacity = (uint32_t)std::min<uint64_t>(S.bins_cap, 0xFFFFFFFFull);
+    // tile t's list lives at bins[t * slab, (t + 1) * slab)
+    P.slab = (uint32_t)std::min<uint64_t>(S.bins_cap / std::max<uint32_t>(P.ntiles, 1u), 0xFFFFFFFFull / std::max<uint32_t>(P.ntiles, 1u));
     P.status = d->status_dev;
     return ZR_SUCCESS;
 }
@@ -716,7 +712,7 @@ zr_result exec_draw(zr_device* d, ExecState& s, const Cmd& c, bool indexed) {
     }
     if (mesh && !P.view_proj) return fail(ZR_ERROR_VALIDATION_FAILED, "descriptor 'View' not bound");
     // binning geometry: k_setup_bin runs one kSetupThreads workgroup per CU at most
-    // (every workgroup resident: it synchronises through grid barriers)
+    // (its LDS histogram of all tiles; workgroups never wait for each other)
     if (P.ntiles > kMaxTilesPerPass)
         return fail(ZR_ERROR_FEATURE_NOT_PRESENT, "more than 16384 owned 32x32 tiles in one pass");
     P.setup_batch = mesh ? 1u : 2u;  // k_setup_bin<2> (the mesh instance: <1, true>)
@@ -747,11 +743,10 @@ zr_result exec_draw(zr_device* d, ExecState& s, const Cmd& c, bool indexed) {
         // (mesh: fans 1 and 2 keep their bboxes in global memory, so all of them do)
         P.bbox_lds = (!mesh && entries * sizeof(BBox) <= budget) ? (uint32_t)entries : 0u;
     }
-    // split setup: default batch or the mesh instance, not list mode; bboxes and per-workgroup
-    // offsets cross the launch boundary through global memory
-    const bool split = (d->setup_split > 0 || (d->setup_split < 0 && (prims <= (1u << 18) || P.shard_count > 1))) &&
-                       !partitioned && !d->use_graphs && !d->debug;
-    if (split) P.bbox_lds = 0;
+    // k_setup_bin on the setup stream with two scratch sets (zr_device_t::setup_overlap);
+    // not while debugging or with graph replay, whose captures bake in set 0
+    const bool overlap_setup = (d->setup_overlap > 0 || (d->setup_overlap < 0 && (prims <= (1u << 18) || P.shard_count > 1))) &&
+                       !d->use_graphs && !d->debug;
     P.tile_threads = d->tile_threads ? d->tile_threads : tile_threads_for(P.ntiles, (uint32_t)std::max(d->cu_count, 1), prims);
     P.debug = d->debug;
     if (d->debug & kDebugStamps) {
@@ -760,12 +755,10 @@ zr_result exec_draw(zr_device* d, ExecState& s, const Cmd& c, bool indexed) {
         d->dbg_wgs = P.setup_wgs;
         d->dbg_tiles = P.ntiles;
     }
-    // Split and partitioned draws alternate between the two scratch sets (not while
-    // debugging or with graph replay, whose captures bake in set 0: one stream).
-    // Partitioned draws always use both scratch sets and streams: the route and the
-    // exchange of draw i+1 run on setup_stream while draw i's setup + tile pass
-    // run on the main stream.
-    const bool overlap = partitioned || split;
+    // Overlapped and partitioned draws alternate between the two scratch sets.
+    // Partitioned draws always do: the route, exchange and setup of draw i+1 run
+    // on setup_stream while draw i's tile pass runs on the main stream.
+    const bool overlap = partitioned || overlap_setup;
     ScratchSet& S = d->sets[overlap ? d->cur_set : 0];
     if (overlap) d->cur_set ^= 1u;
     if ((rc = ensure_scratch(d, S, P))) return rc;
@@ -807,28 +800,11 @@ zr_result exec_draw(zr_device* d, ExecState& s, const Cmd& c, bool indexed) {
             s.depth_clear_pending = false;
             return ZR_SUCCESS;
         }
-        // List mode runs as the two split launches (no grid barrier): a partitioned
-        // draw shares the GPU with the collectives' kernels on other streams, so a
-        // persistent launch could not count on every workgroup being resident.
-        // They run on the setup stream behind the exchange, so draw i+1's route,
-        // exchange and setup overlap draw i's tile pass (the main stream only
-        // runs tile passes).
-        if ((rc = grow(d, S.wg_offsets, S.wg_offsets_cap, (uint64_t)P.setup_wgs * P.ntiles, 4))) return rc;
-        P.wg_offsets = S.wg_offsets;
-        P.bbox_lds = 0;
-        timed_launch(d, "setup_bin", ss, [&] {
-            launch_setup_split(P, 1, ss);
-            launch_setup_split(P, 2, ss);
-        });
-        ZR_HIP(hipEventRecord(S.setup_done, ss));
-        ZR_HIP(hipStreamWaitEvent(d->stream, S.setup_done, 0));
-    } else if (split) {
-        if ((rc = grow(d, S.wg_offsets, S.wg_offsets_cap, (uint64_t)P.setup_wgs * P.ntiles, 4))) return rc;
-        P.wg_offsets = S.wg_offsets;
-        timed_launch(d, "setup_bin", ss, [&] {
-            launch_setup_split(P, 1, ss);
-            launch_setup_split(P, 2, ss);
-        });
+        // List-mode setup runs on the setup stream behind the exchange, so draw
+        // i+1's route, exchange and setup overlap draw i's tile pass (the main
+        // stream only runs tile passes).  k_setup_bin has no grid
+        // barrier, so sharing the GPU with the collectives' kernels is safe.
+        timed_launch(d, "setup_bin", ss, [&] { launch_setup_bin(P, ss); });
         ZR_HIP(hipEventRecord(S.setup_done, ss));
         ZR_HIP(hipStreamWaitEvent(d->stream, S.setup_done, 0));
     } else {
@@ -841,7 +817,7 @@ zr_result exec_draw(zr_device* d, ExecState& s, const Cmd& c, bool indexed) {
     timed_launch(d, "tile", d->stream, [&] { launch_tile(P, d->stream); });
     // Every draw marks its set's last reader, overlapping or not: a later draw that
     // sets up on setup_stream into this set waits for it (a draw on d->stream alone
-    // would otherwise leave the set's event stale for the next split draw).
+    // would otherwise leave the set's event stale for the next overlapped draw).
     // (A graph capture uses set 0 only; submit_graph_or_eager marks it after the replay.)
     if (!d->capturing) {
         ZR_HIP(hipEventRecord(S.tile_done, d->stream));
@@ -956,7 +932,7 @@ ZR_API zr_result zr_device_create(int32_t hip_device, zr_device** out) {
     if (const char* p = getenv("ZR_DEBUG_TS")) d->dbg_ts_path = p;
     if (const char* cap = getenv("ZR_BIN_CAPACITY")) d->initial_bins = std::max<uint64_t>(64, strtoull(cap, nullptr, 0));
     if (const char* g = getenv("ZR_GRAPH")) d->use_graphs = strtoul(g, nullptr, 0) != 0;
-    if (const char* o = getenv("ZR_SETUP_SPLIT")) d->setup_split = strtoul(o, nullptr, 0) != 0 ? 1 : 0;
+    if (const char* o = getenv("ZR_SETUP_OVERLAP")) d->setup_overlap = strtoul(o, nullptr, 0) != 0 ? 1 : 0;
     if (const char* nt = getenv("ZR_TILE_NT")) {
         const unsigned long v = strtoul(nt, nullptr, 0);
         d->tile_threads = v >= 512 ? 512u : v ? 256u : 0u;
@@ -970,10 +946,6 @@ ZR_API zr_result zr_device_create(int32_t hip_device, zr_device** out) {
                                    (int)kSetupLdsBudget));
     ZR_HIP(hipFuncSetAttribute(setup_bin_kernel(1, true), hipFuncAttributeMaxDynamicSharedMemorySize,
                                (int)kSetupLdsBudget));
-    for (int pass : {1, 2})
-        for (bool mesh : {false, true})
-            ZR_HIP(hipFuncSetAttribute(setup_split_kernel(pass, mesh), hipFuncAttributeMaxDynamicSharedMemorySize,
-                                       (int)kSetupLdsBudget));
     ZR_HIP(hipDeviceGetAttribute(&d->cu_count, hipDeviceAttributeMultiprocessorCount, hip_device));
     void* st = nullptr;
     ZR_HIP(hipHostMalloc(&st, kStWords * 4, hipHostMallocMapped));
@@ -996,8 +968,8 @@ ZR_API void zr_device_destroy(zr_device* d) {
     if (d->dbg_ts) (void)hipFree(d->dbg_ts);
     for (ScratchSet& S : d->sets) {
         for (void* p : {(void*)S.records, (void*)S.records_big, (void*)S.mesh_edges, (void*)S.bboxes, (void*)S.tile_counts,
-                        (void*)S.tile_offsets, (void*)S.counters, (void*)S.bins, (void*)S.xsend, (void*)S.xrecv,
-                        (void*)S.gids, (void*)S.rcounts, (void*)S.wg_offsets})
+                        (void*)S.draw_info, (void*)S.counters, (void*)S.bins, (void*)S.xsend, (void*)S.xrecv,
+                        (void*)S.gids, (void*)S.rcounts})
             if (p) (void)hipFree(p);
         if (S.setup_done) (void)hipEventDestroy(S.setup_done);
         if (S.tile_done) (void)hipEventDestroy(S.tile_done);
