@@ -371,8 +371,8 @@ def test_partitioned_ranks_without_rows():
 
 def test_partitioned_beside_busy_stream():
     """A partitioned draw while another stream keeps every CU busy (matmuls):
-    list-mode setup runs as two launches with no grid barrier, so it needs no
-    co-residency and cannot time out; the frame is exact."""
+    setup kernel has no grid barrier, so it needs no co-residency and cannot
+    time out; the frame is exact."""
     import threading
     import torch
     side = torch.cuda.Stream()
@@ -396,8 +396,8 @@ def test_partitioned_beside_busy_stream():
 
 
 def test_mixed_draw_sizes_no_sync(device):
-    """A draw above 2^18 primitives (persistent setup, scratch set 0, main stream)
-    followed by small draws (split setup on the setup stream, alternating sets)
+    """A draw above 2^18 primitives (setup on the main stream, scratch set 0)
+    followed by small draws (setup on the setup stream, alternating sets)
     with no host sync in between: every target equals its own oracle frame."""
     big = scenes.soup_scene(79, 300_000, 640, 480, 3.0, scenes.PROGRAM_BLINN_PHONG)
     small = [scenes.soup_scene(80 + i, 2000 + 1000 * i, 320, 240, 9.0, scenes.PROGRAM_FLAT_COLOR) for i in range(3)]
