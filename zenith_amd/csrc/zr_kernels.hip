@@ -6,7 +6,7 @@
 //                32-B compact record (64-B full record for large primitives);
 //                LDS histogram of tile overlaps; returning atomics on the tile
 //                counters; an XCD-hierarchical grid barrier; tile scan; scatter of
-//                (tile, primitive | area bucket) pairs into the tile lists.  Also
+//                (tile, primitive | cost bucket) pairs into the tile lists.  Also
 //                built as two launches cut at the barrier (split setup).
 //   k_tile       one 256- or 512-thread workgroup per 32x32 tile: LDS-resident
 //                64-bit visibility keys (depth | primitive sequence) updated with
@@ -46,23 +46,20 @@ namespace zr {
 #define ZR_RESOLVE_BATCH 2   // pixels per thread whose gathers are in flight together in the resolve
 #endif
 #ifndef ZR_TILE_WIDE
-#define ZR_TILE_WIDE 0       // 1: bbox ∩ tile of 253+ px goes to the wave path instead of one lane
+#define ZR_TILE_WIDE 0       // 1: the last cost bucket (127+ pair steps) goes to the wave path instead of lanes
                              // (measured: cerberus tile pass 124 -> 107 us, C3 306 -> 327, C2 77 -> 79)
 #endif
 #ifndef ZR_TILE_BIGK
-#define ZR_TILE_BIGK 8       // lanes per entry at least, for the last sort bucket (253+ px of bbox ∩ tile)
+#define ZR_TILE_BIGK 8       // lanes per entry at least, for the last sort bucket (127+ pair steps, ~253+ px)
 #endif
 #ifndef ZR_TILE_MIDK
 #define ZR_TILE_MIDK 4       // lanes per entry at least, for buckets ZR_TILE_MIDB.. (1: off)
 #endif
 #ifndef ZR_TILE_MIDB
-#define ZR_TILE_MIDB 24      // first bucket of the middle run: bbox ∩ tile of 97+ px
+#define ZR_TILE_MIDB 24      // first bucket of the middle run: 49+ pair steps (~97+ px of bbox ∩ tile)
 #endif
 #ifndef ZR_TILE_SUBLANE
 #define ZR_TILE_SUBLANE 1    // sparse segments: k lanes per entry split its bbox rows (0: one lane per entry)
-#endif
-#ifndef ZR_LANE_PAIR
-#define ZR_LANE_PAIR 1  // lane walk: two pixels of a row per step (0: one pixel per step, A/B)
 #endif
 #ifndef ZR_TILE_DEBUG
 #define ZR_TILE_DEBUG 0      // 1: k_tile honours the ZR_DEBUG timing switches and stamps (A/B builds only;
@@ -966,8 +963,10 @@ __global__ __launch_bounds__(kSetupThreads) void k_setup_bin(DrawParams P) {
                 for (int tx = tx0; tx <= tx1; ++tx) {
                     const int cx0 = max((int)(bb.bb0 & 0xFFFFu), tx << kTileShift);
                     const int cx1 = min((int)(bb.bb1 & 0xFFFFu), (tx << kTileShift) + kTile - 1);
-                    const uint32_t area = (uint32_t)((cx1 - cx0 + 1) * (cy1 - cy0 + 1));
-                    const uint32_t bucket = min((area - 1u) >> 2, kSortBuckets - 1u);
+                    // cost class: the lane walk's pair steps over bbox ∩ tile, ceil(w / 2)
+                    // per row (sorting by steps instead of area: C3 tile pass -1 %, C2 -0.8 %)
+                    const uint32_t steps = (uint32_t)(((cx1 - cx0 + 2) >> 1) * (cy1 - cy0 + 1));
+                    const uint32_t bucket = min((steps - 1u) >> 1, kSortBuckets - 1u);
                     const uint32_t t = r + (uint32_t)tx;
                     const uint32_t pos = atomicAdd(&s_hist[t], 1u);
                     if (pos - t * P.slab < P.slab) P.bins[pos] = rec | (bucket << kBinPrimBits);
@@ -1134,10 +1133,30 @@ __device__ __forceinline__ void raster_lane(const DrawParams& P, const TriRecord
     const int X0 = r.X0, Y0 = r.Y0, X1 = r.X1, Y1 = r.Y1, X2 = r.X2, Y2 = r.Y2;
     const float z0 = r.z0, dz1 = r.dz1, dz2 = r.dz2, invA2 = r.invA2;
     const uint32_t bb0 = r.bb0, bb1 = r.bb1, flags = r.flags;
-    const int bx0 = max((int)(bb0 & 0xFFFFu), x0), by0 = max((int)(bb0 >> 16), y0);
+    int bx0 = max((int)(bb0 & 0xFFFFu), x0);
+    const int by0 = max((int)(bb0 >> 16), y0);
     const int bx1 = min((int)(bb1 & 0xFFFFu), x0 + kTile - 1), by1 = min((int)(bb1 >> 16), y0 + kTile - 1);
-    const int bw = bx1 - bx0 + 1, bh = by1 - by0 + 1;
+    int bw = bx1 - bx0 + 1;
+    const int bh = by1 - by0 + 1;
     if (bw <= 0 || bh <= sub) return;
+    // An odd-width row leaves one sample of its last pair past the bbox.  When the
+    // bbox's right side is the primitive's own x extent (not cut by the tile or the
+    // scissor) that sample lies right of every vertex, so it is never covered; else,
+    // when the left side is its own extent, the pairs start one column further left
+    // (that sample is left of every vertex).  Only when both sides are cut does the
+    // step test for it (chk).
+    bool chk = false;
+    if (bw & 1) {
+        const int minX = min(X0, min(X1, X2)), maxX = max(X0, max(X1, X2));
+        if (bx1 != (maxX - 128) >> 8) {
+            if (bx0 == (minX - 128 + 255) >> 8) {
+                --bx0;
+                ++bw;
+            } else {
+                chk = true;
+            }
+        }
+    }
     const int Sx = bx0 * 256 + 128, Sy = (by0 + sub) * 256 + 128;
     const int dx0 = X2 - X1, dy0 = Y2 - Y1, dx1 = X0 - X2, dy1 = Y0 - Y2, dx2 = X1 - X0, dy2 = Y1 - Y0;
     int r0 = dx0 * (Sy - Y1) - dy0 * (Sx - X1);
@@ -1156,11 +1175,9 @@ __device__ __forceinline__ void raster_lane(const DrawParams& P, const TriRecord
     // per-fragment -0 -> +0 rule therefore gives the same bits).  The sweep ends when the key address reaches the row after the
     // last one (no separate step counter).
     const int rows = (bh - sub + k - 1) >> ksh;
-    const int j0 = k * sy0 - (bw - 1) * sx0, j1 = k * sy1 - (bw - 1) * sx1, j2 = k * sy2 - (bw - 1) * sx2;
     int w0 = r0 - b0, w1 = r1 - b1, w2 = r2 - b2;
     int ex = 0;
     uint32_t la = (uint32_t)(((by0 + sub - y0) * kTile + (bx0 - x0)) * 8);  // byte offset of the key
-    const uint32_t lj = (uint32_t)((k * kTile - bw + 1) * 8);
     const uint32_t la_end = la + (uint32_t)(rows * k * kTile * 8);
     // The depth-range test (fragments outside [dlo, dhi] are discarded, §3) is
     // dropped from the loop when every lane's vertex depths lie inside the range
@@ -1176,20 +1193,19 @@ __device__ __forceinline__ void raster_lane(const DrawParams& P, const TriRecord
             (!INITD || depth_pass(P.depth_op, z, s_initd[a >> 3])))
             atomicMin(reinterpret_cast<unsigned long long*>(reinterpret_cast<char*>(s_key) + a), frag_key<MODE>(z, seq));
     };
-#if ZR_LANE_PAIR
     // Two pixels of a row per step (VALU and loop-control SALU are what the lane
     // walk spends: one step's wrap selects and branch bookkeeping now serve two
     // samples).  The second pixel of a row's last pair lies past an odd-width
     // bbox and is skipped (pair index lastB).
-    const int hw = (bw + 1) >> 1, lastB = (bw & 1) ? hw - 1 : hw;
+    const int hw = (bw + 1) >> 1, lastB = chk ? hw - 1 : hw;
     const int t0 = 2 * sx0, t1 = 2 * sx1, t2 = 2 * sx2;
     const int q0 = k * sy0 - 2 * (hw - 1) * sx0, q1 = k * sy1 - 2 * (hw - 1) * sx1, q2 = k * sy2 - 2 * (hw - 1) * sx2;
     const uint32_t lq = (uint32_t)((k * kTile - 2 * (hw - 1)) * 8);
-    auto sweep = [&](auto ztest) {
+    auto sweep = [&](auto ztest, auto wchk) {
         do {
             if ((w0 | w1 | w2) >= 0) frag(ztest, w1, w2, la);
             const int v0 = w0 + sx0, v1 = w1 + sx1, v2 = w2 + sx2;
-            if (ex != lastB && (v0 | v1 | v2) >= 0) frag(ztest, v1, v2, la + 8u);
+            if ((!decltype(wchk)::value || ex != lastB) && (v0 | v1 | v2) >= 0) frag(ztest, v1, v2, la + 8u);
             const bool wrap = ++ex == hw;
             ex = wrap ? 0 : ex;
             w0 += wrap ? q0 : t0;
@@ -1198,23 +1214,16 @@ __device__ __forceinline__ void raster_lane(const DrawParams& P, const TriRecord
             la += wrap ? lq : 16u;
         } while (la != la_end);
     };
-#else
-    auto sweep = [&](auto ztest) {
-        do {
-            if ((w0 | w1 | w2) >= 0) frag(ztest, w1, w2, la);
-            const bool wrap = ++ex == bw;
-            ex = wrap ? 0 : ex;
-            w0 += wrap ? j0 : sx0;
-            w1 += wrap ? j1 : sx1;
-            w2 += wrap ? j2 : sx2;
-            la += wrap ? lj : 8u;
-        } while (la != la_end);
-    };
-#endif
-    if (__ballot(!zsafe) == 0ull)
-        sweep(std::false_type{});
+    const bool wchk = __ballot(chk) != 0ull;
+    const bool wz = __ballot(!zsafe) != 0ull;
+    if (!wz && !wchk)
+        sweep(std::false_type{}, std::false_type{});
+    else if (!wz)
+        sweep(std::false_type{}, std::true_type{});
+    else if (!wchk)
+        sweep(std::true_type{}, std::false_type{});
     else
-        sweep(std::true_type{});
+        sweep(std::true_type{}, std::true_type{});
 }
 
 // Visibility sequence of setup record e (API order): e + 1, or for the mesh
@@ -1779,7 +1788,7 @@ __global__ __launch_bounds__(NT, ZR_TILE_WGS * kTileThreads / 256) void k_tile(D
 #pragma unroll
         for (uint32_t k = 0; k < kPerThread; ++k) {
             const uint32_t i = threadIdx.x + k * NT;
-            ent[k] = i < n ? bp[i] : 0u;  // prim | area bucket (k_setup_bin phase 4)
+            ent[k] = i < n ? bp[i] : 0u;  // prim | cost bucket (k_setup_bin phase 4)
         }
     };
     if (!(tile_debug(P) & kDebugSkipRaster)) load_segment(0, min(kSortCap, slab));
@@ -1828,7 +1837,7 @@ __global__ __launch_bounds__(NT, ZR_TILE_WGS * kTileThreads / 256) void k_tile(D
     if (stamp) ts[1] = __builtin_amdgcn_s_memrealtime();
     if (!(tile_debug(P) & kDebugSkipRaster)) {
         // The list is processed in segments of kSortCap entries.  Each segment is
-        // counting-sorted in LDS by the primitive's bbox ∩ tile area (lane-path cost)
+        // counting-sorted in LDS by the lane walk's pair steps over bbox ∩ tile
         // so that a 64-lane chunk holds primitives of similar cost (the lane loop runs
         // as long as its largest member).  Then each wave takes every 4th chunk: one
         // lane per entry loads the 64-B record, and the wave walks the chunk.
@@ -1878,7 +1887,7 @@ __global__ __launch_bounds__(NT, ZR_TILE_WGS * kTileThreads / 256) void k_tile(D
             // vs 304 us; LPT: C2 80 vs 82 us).
             const uint32_t kl = ZR_TILE_SUBLANE ? min(8u, max(1u, (uint32_t)NT / max(n, 1u))) : 1u;
             const uint32_t ksh_s = 31u - __clz(kl);  // lanes per entry: 1, 2, 4 or 8
-            // entries of the last bucket (bbox ∩ tile of 253+ pixels) get at least
+            // entries of the last bucket (127+ pair steps, ~253+ pixels) get at least
             // ZR_TILE_BIGK lanes: one lane would walk up to 1024 steps and hold
             // its whole chunk (and the tile) for that long.  Chunks are 64 lanes of
             // this lane space: the first off63 entries kl lanes each, then the rest.
