@@ -133,6 +133,31 @@ def test_bin_overflow_spill(monkeypatch):
         dev.close()
 
 
+def test_slab_overflow_one_tile():
+    """Tile lists live in fixed per-tile slabs (bin buffer / tiles): a draw whose
+    pairs fit the buffer but whose one crowded tile outgrows its slab rasterizes
+    that tile by the record scan and every other tile from its list, in the same
+    pass; the runtime then grows the slabs."""
+    w, h = 640, 480
+    dense = scenes.soup_arrays(41, 9000, 32, 32, 2.0, False)  # 9000 small triangles, most in one 32x32 tile
+    dense[:, 0] = dense[:, 0] * (32.0 / w) + (2 * 32 * 5 + 32) / w - 1.0  # tile (5, 7)
+    dense[:, 1] = dense[:, 1] * (32.0 / h) + (2 * 32 * 7 + 32) / h - 1.0
+    sparse = scenes.soup_arrays(42, 3000, w, h, 10.0, False)
+    v = np.concatenate([sparse[:4500], dense, sparse[4500:]]).astype(np.float32)
+    s = scenes.Scene("slab_overflow", w, h, scenes.PROGRAM_FLAT_COLOR, v, np.arange(len(v), dtype=np.uint32),
+                     depth=True)
+    dev = rhi.RenderDevice(0)
+    try:
+        assert_parity(dev, s)
+        st = dev.last_draw_stats()
+        # 2^20 entries over 300 tiles: slabs of 3495 < the crowded tile's ~8900
+        assert st["overflowed_draws"] == 1 and st["bin_pairs"] < (1 << 20)
+        assert_parity(dev, s)
+        assert dev.last_draw_stats()["overflowed_draws"] == 1  # grown: no new overflow
+    finally:
+        dev.close()
+
+
 @pytest.mark.parametrize("nt", [256, 512])
 def test_tile_workgroup_sizes(monkeypatch, nt):
     """k_tile at each workgroup size (4 or 8 waves per tile; the runtime picks by
