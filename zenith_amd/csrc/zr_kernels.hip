@@ -540,13 +540,26 @@ __device__ __forceinline__ bool mesh_geometry_unclipped(const DrawParams& P, con
 
 // Counts the owned (tile, primitive) pairs of a set-up triangle in the LDS
 // histogram; returns how many there are.
+// The first tile row at or after ty0 that this shard owns (ty % G == rank) and its
+// index among the owned rows; the next owned row is G further.  One division per
+// primitive, none when the target is not sharded (G == 1, wave-uniform).
+__device__ __forceinline__ int first_owned_row(uint32_t G, uint32_t rank, int ty0, uint32_t& orow) {
+    if (G == 1u) {
+        orow = (uint32_t)ty0;
+        return ty0;
+    }
+    const uint32_t q = (uint32_t)ty0 / G, m = (uint32_t)ty0 - q * G;
+    orow = m <= rank ? q : q + 1u;
+    return (int)(orow * G + rank);
+}
+
 __device__ __forceinline__ uint32_t count_owned(const DrawParams& P, const PrimGeom& g, uint32_t* s_hist) {
     const int tx0 = g.px0 >> kTileShift, tx1 = g.px1 >> kTileShift;
     const int ty0 = g.py0 >> kTileShift, ty1 = g.py1 >> kTileShift;
-    uint32_t owned = 0;
-    for (int ty = ty0; ty <= ty1; ++ty) {
-        if ((uint32_t)ty % P.shard_count != P.shard_rank) continue;
-        const uint32_t row = ((uint32_t)ty / P.shard_count) * P.tiles_x;
+    const uint32_t G = P.shard_count, tiles_x = P.tiles_x;
+    uint32_t owned = 0, orow;
+    for (int ty = first_owned_row(G, P.shard_rank, ty0, orow); ty <= ty1; ty += (int)G, ++orow) {
+        const uint32_t row = orow * tiles_x;
         for (int tx = tx0; tx <= tx1; ++tx) atomicAdd(&s_hist[row + tx], 1u);
         owned += (uint32_t)(tx1 - tx0 + 1);
     }
@@ -951,13 +964,17 @@ __global__ __launch_bounds__(kSetupThreads) void k_setup_bin(DrawParams P) {
         const DrawParams& P = kernarg_params();
         const uint32_t usz = 1u << P.unit_shift;
         // appends (tile, record) pairs of one setup record to its owned tiles' slabs
+        // (the parameters the loops use, read once: kernarg_params() would reload them
+        // per iteration)
+        uint32_t* const bins = P.bins;
+        const uint32_t slab = P.slab, sG = P.shard_count, srank = P.shard_rank, tiles_x = P.tiles_x;
         auto scatter = [&](uint32_t rec, const BBox bb) {
             if (bb.bb0 == kEmptyBox) return;
             const int tx0 = (int)(bb.bb0 & 0xFFFFu) >> kTileShift, tx1 = (int)(bb.bb1 & 0xFFFFu) >> kTileShift;
             const int ty0 = (int)(bb.bb0 >> 16) >> kTileShift, ty1 = (int)(bb.bb1 >> 16) >> kTileShift;
-            for (int ty = ty0; ty <= ty1; ++ty) {
-                if ((uint32_t)ty % P.shard_count != P.shard_rank) continue;
-                const uint32_t r = ((uint32_t)ty / P.shard_count) * P.tiles_x;
+            uint32_t orow;
+            for (int ty = first_owned_row(sG, srank, ty0, orow); ty <= ty1; ty += (int)sG, ++orow) {
+                const uint32_t r = orow * tiles_x;
                 const int cy0 = max((int)(bb.bb0 >> 16), ty << kTileShift);
                 const int cy1 = min((int)(bb.bb1 >> 16), (ty << kTileShift) + kTile - 1);
                 for (int tx = tx0; tx <= tx1; ++tx) {
@@ -969,7 +986,7 @@ __global__ __launch_bounds__(kSetupThreads) void k_setup_bin(DrawParams P) {
                     const uint32_t bucket = min((steps - 1u) >> 1, kSortBuckets - 1u);
                     const uint32_t t = r + (uint32_t)tx;
                     const uint32_t pos = atomicAdd(&s_hist[t], 1u);
-                    if (pos - t * P.slab < P.slab) P.bins[pos] = rec | (bucket << kBinPrimBits);
+                    if (pos - t * slab < slab) bins[pos] = rec | (bucket << kBinPrimBits);
                 }
             }
         };
