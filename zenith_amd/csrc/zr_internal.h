@@ -216,12 +216,14 @@ constexpr uint32_t kSetupMiscWords = 96;
 // A draw of fewer than 32 primitives per tile (cerberus at 1080p: 16) also gets 8
 // waves: its few heavy tiles (large triangles) end the pass alone on their CUs
 // (cerberus tile pass 124 -> 113 us; C1, 49 per tile, is 14% slower at 8 waves).
-// A draw of 256+ primitives per tile gets 8 waves too: its tiles are long enough
-// for the extra waves to pay (v46, ZR_TILE_NT A/B: C2, 490 per tile, tile pass
-// 78.9 -> 77.1 us; C4 equal; C3 at 122 per tile and C1 at 49 are 2-13 % slower).
+// A draw of 80+ primitives per tile gets 8 waves too: its tiles are long enough
+// for the extra waves to pay (round 1 v46, ZR_TILE_NT A/B: C2, 490 per tile,
+// tile pass 78.9 -> 77.1 us; C4 equal.  Round 2, after the lane-walk changes:
+// C3, 122 per tile, frame 250.7 -> 239.9 us at 8 waves; C1, 49 per tile, 54.5 ->
+// 57.0 us, so it keeps 4).
 inline uint32_t tile_threads_for(uint32_t ntiles, uint32_t cus, uint64_t prims) {
     const uint32_t per_cu = ntiles / (cus ? cus : 1u);
-    return (per_cu >= 6u && prims >= 32ull * ntiles && prims < 256ull * ntiles) ? (uint32_t)kTileThreads : 512u;
+    return (per_cu >= 6u && prims >= 32ull * ntiles && prims < 80ull * ntiles) ? (uint32_t)kTileThreads : 512u;
 }
 
 // Launchers (zr_kernels.hip).  All enqueue on `stream`; no host synchronisation.
