@@ -342,6 +342,15 @@ zr_result grow(zr_device* d, T*& ptr, uint64_t& cap, uint64_t need, uint64_t ele
 
 zr_result execute(zr_device* d, zr_cmd* cmd);
 
+// Events that only order this device's streams (hipStreamWaitEvent), never waited
+// on by the host: device-scope release, no system-scope cache writeback when they
+// are recorded.  (Host waits go through hipStreamSynchronize or a fence's own event.)
+#ifndef ZR_EVENT_SYSTEM_FENCE
+constexpr unsigned kStreamEventFlags = hipEventDisableTiming | hipEventDisableSystemFence;
+#else
+constexpr unsigned kStreamEventFlags = hipEventDisableTiming;
+#endif
+
 // kDebugStamps: per-phase durations of k_setup_bin across workgroups (us, 100 MHz clock).
 void dump_stamps(zr_device* d) {
     std::vector<unsigned long long> ts(d->dbg_wgs * 8);
@@ -556,8 +565,8 @@ zr_result ensure_scratch(zr_device* d, ScratchSet& S, DrawParams& P) {
         if ((rc = grow(d, S.bins, S.bins_cap, want, 4))) return rc;
     }
     if (!S.setup_done) {
-        ZR_HIP(hipEventCreateWithFlags(&S.setup_done, hipEventDisableTiming));
-        ZR_HIP(hipEventCreateWithFlags(&S.tile_done, hipEventDisableTiming));
+        ZR_HIP(hipEventCreateWithFlags(&S.setup_done, kStreamEventFlags));
+        ZR_HIP(hipEventCreateWithFlags(&S.tile_done, kStreamEventFlags));
     }
     P.records = S.records;
     P.records_big = S.records_big;
@@ -1640,7 +1649,7 @@ ZR_API zr_result zr_device_init_rccl(zr_device* d, const void* exchange_id, cons
     d->comm_rank = rank;
     d->comm_size = nranks;
     ZR_HIP(hipStreamCreateWithFlags(&d->gather_stream, hipStreamNonBlocking));
-    ZR_HIP(hipEventCreateWithFlags(&d->frame_done, hipEventDisableTiming));
+    ZR_HIP(hipEventCreateWithFlags(&d->frame_done, kStreamEventFlags));
     return ZR_SUCCESS;
 }
 
@@ -1652,7 +1661,7 @@ ZR_API zr_result zr_device_gather_tile_rows(zr_device* d, zr_texture* t, int32_t
     if (root < 0 || root >= d->comm_size) return fail(ZR_ERROR_VALIDATION_FAILED, "bad root rank");
     zr_result rc = set_device(d);
     if (rc) return rc;
-    if (!t->gather_done) ZR_HIP(hipEventCreateWithFlags(&t->gather_done, hipEventDisableTiming));
+    if (!t->gather_done) ZR_HIP(hipEventCreateWithFlags(&t->gather_done, kStreamEventFlags));
     // after everything enqueued so far on the device stream (the frame)
     ZR_HIP(hipEventRecord(d->frame_done, d->stream));
     ZR_HIP(hipStreamWaitEvent(d->gather_stream, d->frame_done, 0));
