@@ -208,6 +208,10 @@ struct ScratchSet {
     hipEvent_t setup_done = nullptr;  // k_setup_bin of the last draw that used this set
     hipEvent_t tile_done = nullptr;   // k_tile of the last draw that used this set
     bool tile_done_valid = false;
+    // a draw on the main stream alone used this set after tile_done was recorded:
+    // the event is recorded on the main stream only when a setup-stream draw next
+    // needs this set (an event record between two frames costs ~4.4 us of idle GPU)
+    bool main_reader_pending = false;
 };
 
 struct TimedLaunch {
@@ -777,6 +781,12 @@ zr_result exec_draw(zr_device* d, ExecState& s, const Cmd& c, bool indexed) {
     const hipStream_t ss = overlap ? d->setup_stream : d->stream;
     // the first pass on ss may start once the previous reader of this scratch set
     // (the k_tile two draws back) is done
+    if (overlap && S.main_reader_pending) {
+        // everything enqueued on the main stream so far includes that last reader
+        ZR_HIP(hipEventRecord(S.tile_done, d->stream));
+        S.tile_done_valid = true;
+        S.main_reader_pending = false;
+    }
     if (overlap && S.tile_done_valid) ZR_HIP(hipStreamWaitEvent(ss, S.tile_done, 0));
     // debug early exits skip the self-reset at the end of k_setup_bin
     if (d->debug) {
@@ -824,13 +834,21 @@ zr_result exec_draw(zr_device* d, ExecState& s, const Cmd& c, bool indexed) {
         }
     }
     timed_launch(d, "tile", d->stream, [&] { launch_tile(P, d->stream); });
-    // Every draw marks its set's last reader, overlapping or not: a later draw that
-    // sets up on setup_stream into this set waits for it (a draw on d->stream alone
-    // would otherwise leave the set's event stale for the next overlapped draw).
-    // (A graph capture uses set 0 only; submit_graph_or_eager marks it after the replay.)
+    // Every draw marks its set's last reader: a later draw that sets up on
+    // setup_stream into this set waits for it.  An overlapped draw records its own
+    // tile_done right here (the next setup into the other set must not wait for
+    // it); a draw on the main stream alone only flags the set, and the event is
+    // recorded when an overlapped draw next needs the set (above), so back-to-back
+    // single-stream frames carry no event at all.
+    // (A graph capture uses set 0 only; submit_graph_or_eager flags it after the replay.)
     if (!d->capturing) {
-        ZR_HIP(hipEventRecord(S.tile_done, d->stream));
-        S.tile_done_valid = true;
+        if (overlap) {
+            ZR_HIP(hipEventRecord(S.tile_done, d->stream));
+            S.tile_done_valid = true;
+            S.main_reader_pending = false;
+        } else {
+            S.main_reader_pending = true;
+        }
     }
     ZR_HIP(hipGetLastError());
     s.color_clear_pending = false;
@@ -1721,9 +1739,7 @@ static zr_result submit_graph_or_eager(zr_device* d, zr_cmd* c) {
     }
     // a replayed graph's draws read and write scratch set 0 on the main stream
     auto mark_set0 = [d]() -> zr_result {
-        if (!d->sets[0].tile_done) return ZR_SUCCESS;
-        ZR_HIP(hipEventRecord(d->sets[0].tile_done, d->stream));
-        d->sets[0].tile_done_valid = true;
+        d->sets[0].main_reader_pending = true;
         return ZR_SUCCESS;
     };
     if (c->graph && c->graph_gen == d->scratch_gen) {
