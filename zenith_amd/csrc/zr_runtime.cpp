@@ -346,9 +346,11 @@ zr_result grow(zr_device* d, T*& ptr, uint64_t& cap, uint64_t need, uint64_t ele
 
 zr_result execute(zr_device* d, zr_cmd* cmd);
 
-// Events that only order this device's streams (hipStreamWaitEvent), never waited
-// on by the host: device-scope release, no system-scope cache writeback when they
-// are recorded.  (Host waits go through hipStreamSynchronize or a fence's own event.)
+// Events that only order this device's streams around data this device's own
+// kernels write and read (setup_done, tile_done), never waited on by the host:
+// device-scope release, no system-scope cache writeback when they are recorded.
+// (Host waits go through hipStreamSynchronize or a fence's own event.)  The row
+// gather's events keep the system-scope fence: RCCL moves the rows between devices.
 #ifndef ZR_EVENT_SYSTEM_FENCE
 constexpr unsigned kStreamEventFlags = hipEventDisableTiming | hipEventDisableSystemFence;
 #else
@@ -1667,7 +1669,7 @@ ZR_API zr_result zr_device_init_rccl(zr_device* d, const void* exchange_id, cons
     d->comm_rank = rank;
     d->comm_size = nranks;
     ZR_HIP(hipStreamCreateWithFlags(&d->gather_stream, hipStreamNonBlocking));
-    ZR_HIP(hipEventCreateWithFlags(&d->frame_done, kStreamEventFlags));
+    ZR_HIP(hipEventCreateWithFlags(&d->frame_done, hipEventDisableTiming));
     return ZR_SUCCESS;
 }
 
@@ -1679,7 +1681,7 @@ ZR_API zr_result zr_device_gather_tile_rows(zr_device* d, zr_texture* t, int32_t
     if (root < 0 || root >= d->comm_size) return fail(ZR_ERROR_VALIDATION_FAILED, "bad root rank");
     zr_result rc = set_device(d);
     if (rc) return rc;
-    if (!t->gather_done) ZR_HIP(hipEventCreateWithFlags(&t->gather_done, kStreamEventFlags));
+    if (!t->gather_done) ZR_HIP(hipEventCreateWithFlags(&t->gather_done, hipEventDisableTiming));
     // after everything enqueued so far on the device stream (the frame)
     ZR_HIP(hipEventRecord(d->frame_done, d->stream));
     ZR_HIP(hipStreamWaitEvent(d->gather_stream, d->frame_done, 0));
