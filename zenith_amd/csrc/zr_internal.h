@@ -221,8 +221,17 @@ constexpr uint32_t kSetupMiscWords = 96;
 // tile pass 78.9 -> 77.1 us; C4 equal.  Round 2, after the lane-walk changes:
 // C3, 122 per tile, frame 250.7 -> 239.9 us at 8 waves; C1, 49 per tile, 54.5 ->
 // 57.0 us, so it keeps 4).
-inline uint32_t tile_threads_for(uint32_t ntiles, uint32_t cus, uint64_t prims) {
-    const uint32_t per_cu = ntiles / (cus ? cus : 1u);
+// A partitioned shard whose 512-thread tile pass would take nearly every wave
+// slot of the GPU (>= 3.5 tiles per CU) gets 4 waves per tile instead: the next
+// draw's route, exchange and list setup on the setup stream then run beside the
+// tile pass rather than after it (round 2, C3 rank 0 of 8 on one GPU: 67.5 ->
+// 61.9 us per frame; replicated shards, whose single setup kernel needs whole
+// CUs, are 13-20 % slower that way, and C2's shard of 8, at one tile per CU,
+// equal).
+inline uint32_t tile_threads_for(uint32_t ntiles, uint32_t cus, uint64_t prims, bool partitioned) {
+    const uint32_t c = cus ? cus : 1u;
+    const uint32_t per_cu = ntiles / c;
+    if (partitioned) return 2ull * ntiles >= 7ull * c ? (uint32_t)kTileThreads : 512u;
     return (per_cu >= 6u && prims >= 32ull * ntiles && prims < 80ull * ntiles) ? (uint32_t)kTileThreads : 512u;
 }
 

@@ -762,7 +762,8 @@ zr_result exec_draw(zr_device* d, ExecState& s, const Cmd& c, bool indexed) {
     // not while debugging or with graph replay, whose captures bake in set 0
     const bool overlap_setup = (d->setup_overlap > 0 || (d->setup_overlap < 0 && (prims <= (1u << 18) || P.shard_count > 1))) &&
                        !d->use_graphs && !d->debug;
-    P.tile_threads = d->tile_threads ? d->tile_threads : tile_threads_for(P.ntiles, (uint32_t)std::max(d->cu_count, 1), prims);
+    P.tile_threads = d->tile_threads ? d->tile_threads
+                                     : tile_threads_for(P.ntiles, (uint32_t)std::max(d->cu_count, 1), prims, partitioned);
     P.debug = d->debug;
     if (d->debug & kDebugStamps) {
         if (!d->dbg_ts) ZR_HIP(hipMalloc((void**)&d->dbg_ts, (8192 + kMaxTilesPerPass) * 8 * sizeof(unsigned long long)));
