@@ -46,8 +46,9 @@ def parse():
                         "frame (K=3 puts C2's 360 MB of input past the 256 MiB Infinity Cache: the HBM-honest "
                         "rate, SURVEY.md §8d); 0 skips it")
     p.add_argument("--emulate-shard", type=int, default=0, metavar="G",
-                   help="diagnostic (1 GPU): run only rank 0's share of a G-way tile-row shard, no gather "
-                        "(partitioned setup: rank 0's routed block stands in for every source's)")
+                   help="diagnostic (1 GPU): every rank of a G-way tile-row shard in turn, beside the unsharded "
+                        "frame; reports the max-over-ranks frame time and T1 / that (no gather; partitioned "
+                        "setup: each rank receives the records the other ranks really route to it)")
     p.add_argument("--setup", choices=["partitioned", "replicated"], default="replicated",
                    help="tile-row shards: set up every primitive on every rank (binning only its own rows), "
                         "or route 1/G of the primitives per rank through an RCCL all-to-all (DESIGN.md §7; "
@@ -67,15 +68,18 @@ def algorithmic_bytes(kernel, n_tris, b_in, pairs, pixels, n_route=0):
 
     setup_bin: read index+vertex data once (b_in per triangle), write one 32-B
                record per triangle and one 4-B bin entry per (tile, triangle) pair.
-               With a partitioned setup n_tris is the rank's received triangles
-               (+ their 4-B ids).
+               With a partitioned setup n_tris is the rank's received records:
+               read each 48-B route entry, write its 32-B record.
     route:     (partitioned setup) read indices + positions of the rank's range
-               (12 + 3 * 12 B per triangle).
+               (12 + 3 * 12 B per triangle; the 48-B entries it writes are the
+               receivers' reads).
     tile:      read each pair's bin entry + record once, write the colour + depth
                texel of every owned pixel (4 + 4 B).
     """
     if kernel == "setup_bin":
-        return n_tris * (b_in + RECORD_BYTES + (4 if n_route else 0)) + pairs * BIN_ENTRY_BYTES
+        if n_route:
+            return n_tris * (shard.ENTRY_BYTES + RECORD_BYTES) + pairs * BIN_ENTRY_BYTES
+        return n_tris * (b_in + RECORD_BYTES) + pairs * BIN_ENTRY_BYTES
     if kernel == "route":
         return n_route * 48
     if kernel == "tile":
@@ -125,20 +129,142 @@ def cpu_baseline(scene, seconds, max_frames=500):
                       f"after 1 warm-up; {dt:.2f} s wall on {threads} threads (nproc; {total} CPUs online, {model})"}
 
 
-class MirrorExchange(shard.Exchange):
-    """--emulate-shard diagnostic (1 GPU, partitioned setup): rank 0's own routed
-    block stands in for every source's, so the per-rank list-mode setup and tile
-    pass see a workload of the real size (duplicate primitives, not the real frame)."""
+class CaptureExchange(shard.Exchange):
+    """--emulate-shard, partitioned setup: keeps this rank's send blocks (its
+    routed records for every destination) and delivers nothing."""
 
     def __init__(self, device, world):
         super().__init__()
-        self.device, self.world = device, world
+        self.device, self.world, self.sent = device, world, None
 
     def exchange(self, stream, send, recv, nbytes):
         with torch.cuda.stream(torch.cuda.ExternalStream(stream, device=self.device)):
-            src = shard.device_bytes(send, nbytes, self.device)
-            dst = shard.device_bytes(recv, nbytes * self.world, self.device).view(self.world, nbytes)
-            dst.copy_(src.unsqueeze(0).expand(self.world, nbytes))
+            self.sent = shard.device_bytes(send, nbytes * self.world, self.device).clone().view(self.world, nbytes)
+            shard.device_bytes(recv, nbytes * self.world, self.device).zero_()
+
+
+class ReplayExchange(shard.Exchange):
+    """--emulate-shard, partitioned setup: delivers the blocks every source rank
+    really routed to this rank (assembled from their captured sends), so the
+    rank's binning and tile pass see its real received set.  The delivery is a
+    device copy of those bytes on the runtime's setup stream (the real all-to-all
+    over xGMI is the driver's 8-GPU run to measure)."""
+
+    def __init__(self, device, recv_blocks: torch.Tensor):
+        super().__init__()
+        self.device, self.src = device, recv_blocks.reshape(-1)
+
+    def exchange(self, stream, send, recv, nbytes):
+        with torch.cuda.stream(torch.cuda.ExternalStream(stream, device=self.device)):
+            shard.device_bytes(recv, self.src.numel(), self.device).copy_(self.src)
+
+
+def route_totals(sent: torch.Tensor):
+    """Per-destination entry totals from a captured send buffer's block headers."""
+    hdr = sent[:, :8].contiguous().cpu().view(torch.int32)
+    return [int(t) for t in hdr[:, 1]]
+
+
+def emulate(a, scene, cuda):
+    """--emulate-shard G (1 GPU): every rank r of a G-way tile-row shard in turn,
+    each timed like the bench's step (W warm-up, K frames between syncs), beside
+    the unsharded frame T1 on the same GPU.  Partitioned setup: every source
+    rank's route runs first (captured), each rank then receives exactly the
+    records the others routed to it.  Reports T1, every rank's frame time, the
+    speed-up T1 / max-rank time and the 6x target; the row gather is excluded
+    (modelled only) and so is the all-to-all's time on the wire (a device copy
+    of the received bytes stands in for it)."""
+    G = a.emulate_shard
+    W, H, N = scene.width, scene.height, scene.triangles
+    dev = rhi.RenderDevice(0)
+    color_t = torch.zeros((H, W * 4), dtype=torch.uint8, device=cuda)
+    depth_t = torch.zeros((H, W), dtype=torch.float32, device=cuda)
+    torch.cuda.synchronize()
+    color = rhi.Texture(dev, rhi.TextureDesc.new_color("frame.color", W, H, scene.color_format), color_t.data_ptr())
+    depth = rhi.Texture(dev, rhi.TextureDesc.new_depth("frame.depth", W, H), depth_t.data_ptr())
+    rend = renderer.SceneRenderer(dev, scene)
+
+    def timed(enc):
+        for _ in range(a.warmup):
+            dev.submit(enc)
+        dev.wait_idle()
+        torch.cuda.synchronize()
+        t0 = time.perf_counter()
+        for _ in range(a.steps):
+            dev.submit(enc)
+        dev.wait_idle()
+        torch.cuda.synchronize()
+        return (time.perf_counter() - t0) / a.steps
+
+    def kernels(enc):
+        dev.kernel_times(reset=True)
+        dev.set_profiling(True)
+        for _ in range(a.steps):
+            dev.submit(enc)
+        dev.wait_idle()
+        dev.set_profiling(False)
+        return {k: round(ms * 1e3 / max(n, 1), 2) for k, (ms, n) in dev.kernel_times().items()}
+
+    enc1 = rend.record(color, depth, encoder=rhi.CommandEncoder(dev))
+    t1 = timed(enc1)
+    enc1.destroy()
+    part = a.setup == "partitioned"
+    cap = 0
+    recv = None
+    if part:
+        _, span, _, _ = shard.route_geometry(N, G)
+
+        def capture(c):
+            sends = []
+            for s in range(G):
+                ex = CaptureExchange(cuda, G)
+                enc = rend.record(color, depth, shard=(s, G, ex, c), encoder=rhi.CommandEncoder(dev))
+                dev.submit(enc)
+                dev.wait_idle()
+                sends.append(ex.sent)
+                enc.destroy()
+            return sends
+        # exact block capacity for this static scene: the largest routed total
+        sends = capture(span)
+        cap = max(max(route_totals(x)) for x in sends) + 64
+        sends = capture(cap)
+        recv = [torch.stack([sends[s][r] for s in range(G)]) for r in range(G)]
+    ranks = []
+    for r in range(G):
+        sh = (r, G, ReplayExchange(cuda, recv[r]), cap) if part else (r, G)
+        enc = rend.record(color, depth, shard=sh, encoder=rhi.CommandEncoder(dev))
+        tr = timed(enc)
+        kt = kernels(enc)
+        st = dev.last_draw_stats()
+        pixels = int(shard.owned_rows(H, r, G).numel()) * W
+        ranks.append({"rank": r, "ms": round(tr * 1e3, 4), "kernels_us": kt, "bin_pairs": st["bin_pairs"],
+                      "triangles_setup": st["triangles_setup"], "pixels": pixels,
+                      "route_fallback_draws": st["route_fallback_draws"]})
+        enc.destroy()
+    worst = max(ranks, key=lambda x: x["ms"])
+    # the row gather (DESIGN.md §7), modelled: the largest peer's rows into rank 0
+    # over one xGMI link at ~153 GB/s, overlapped with the next frame
+    peer_rows = max((int(shard.owned_rows(H, r, G).numel()) for r in range(1, G)), default=0)
+    gather_us = peer_rows * W * 4 / 153e9 * 1e6
+    b_in = scenes.config_bytes_per_triangle(a.config)
+    n_route = shard.route_range(N, worst["rank"], G)
+    rank_bytes = (((n_route[1] - n_route[0]) * b_in + worst["triangles_setup"] * shard.ENTRY_BYTES) if part
+                  else N * b_in) + worst["pixels"] * 8
+    out = {"metric": METRIC + " [1-GPU emulation of a tile-row shard; diagnostic, not the bench line]",
+           "config": {"workload": f"{a.config}: {N} tris, {W}x{H}", "shards": G, "setup": a.setup},
+           "t1_ms": round(t1 * 1e3, 4), "rank_ms": [x["ms"] for x in ranks],
+           "max_rank": worst["rank"], "max_rank_ms": worst["ms"],
+           "speedup": round(t1 / (worst["ms"] * 1e-3), 3), "target_speedup": 6.0 if G == 8 else None,
+           "value_emulated": round(N / (worst["ms"] * 1e-3) / 1e6, 2), "unit": "Mtri/s",
+           "excluded": "row gather (modelled below, overlapped with the next frame) and the all-to-all's wire "
+                       "time (a device copy of the received bytes stands in)",
+           "gather_model_us": round(gather_us, 1), "route_capacity": cap or None,
+           "rank_alg_bytes": rank_bytes, "rank_gbps": round(rank_bytes / (worst["ms"] * 1e-3) / 1e9, 1),
+           "ranks": ranks, "steps": a.steps, "warmup": a.warmup}
+    for t in (color, depth):
+        t.destroy()
+    dev.close()
+    return out
 
 
 def main():
@@ -164,6 +290,11 @@ def main():
 
     scene = scenes.config_scene(a.config)
     W, H, N = scene.width, scene.height, scene.triangles
+    if a.emulate_shard > 1:
+        if distributed:
+            raise SystemExit("--emulate-shard is a 1-GPU diagnostic")
+        print(json.dumps(emulate(a, scene, cuda)), file=json_out, flush=True)
+        return
     dev = rhi.RenderDevice(local)
     # Multi-GPU frames ping-pong between two colour targets: frame f+1 renders
     # while frame f's rows are gathered on a stream of their own.
@@ -178,9 +309,7 @@ def main():
     depth = rhi.Texture(dev, rhi.TextureDesc.new_depth("frame.depth", W, H), depth_t.data_ptr())
     # copy 0 is the warm (value) pass's geometry; copies 0..K-1 cycle in the cold pass
     rs = [renderer.SceneRenderer(dev, scene) for _ in range(max(1, a.cold_copies))]
-    if a.emulate_shard and distributed:
-        raise SystemExit("--emulate-shard is a 1-GPU diagnostic")
-    shard_g = a.emulate_shard if a.emulate_shard > 1 else world
+    shard_g = world
     exchange = None
     runtime_comm = distributed and a.comm == "runtime"
     if runtime_comm:
@@ -199,9 +328,21 @@ def main():
         # its own communicator (and so its own RCCL stream): the exchange of frame
         # f+1 must not queue behind the row gather of frame f
         exchange = shard.RcclExchange(cuda, group=dist.new_group(list(range(world))))
-    elif a.setup == "partitioned" and shard_g > 1:
-        exchange = MirrorExchange(cuda, shard_g)
-    sh = (rank, shard_g, exchange) if exchange is not None else ((rank, shard_g) if shard_g > 1 else None)
+    cap = 0
+    if exchange is not None:
+        # exchange block capacity: this static scene's largest routed total over all
+        # ranks, from one captured route per rank (nothing delivered), max-reduced so
+        # every rank records the same capacity (zr_cmd_set_route_capacity)
+        _, span, _, _ = shard.route_geometry(N, shard_g)
+        cx = CaptureExchange(cuda, shard_g)
+        enc = rs[0].record(color, depth, shard=(rank, shard_g, cx, span), encoder=rhi.CommandEncoder(dev))
+        dev.submit(enc)
+        dev.wait_idle()
+        enc.destroy()
+        top = torch.tensor([max(route_totals(cx.sent)) + 64], device=cuda)
+        dist.all_reduce(top, op=dist.ReduceOp.MAX)
+        cap = int(top.item())
+    sh = (rank, shard_g, exchange, cap) if exchange is not None else ((rank, shard_g) if shard_g > 1 else None)
     # encs[copy][target]: frame f draws geometry copy f % K into target f % nbuf
     encs = [[r.record(c, depth, shard=sh, encoder=rhi.CommandEncoder(dev)) for c in colors] for r in rs]
     gather = shard.TileRowGather(H, W * 4, rank, world, cuda) if distributed and not runtime_comm else None
@@ -363,7 +504,6 @@ def main():
                      "achieved_survey": achieved_survey,
                      "frac_survey": round(achieved_survey / HBM_PEAK_GBPS, 4) if achieved_survey else None},
         "kernels": kernels,
-        **({"emulated_shard": f"rank 0 of {shard_g} (diagnostic, no gather)"} if a.emulate_shard > 1 else {}),
         "bin_pairs": pairs,
         "triangles_setup": stats["triangles_setup"],
     }

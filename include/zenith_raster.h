@@ -125,6 +125,11 @@ ZR_API int32_t zr_device_kernel_times(zr_device *dev, zr_kernel_time *out, int32
 typedef struct zr_draw_stats {
     uint64_t triangles_in, triangles_setup, triangles_dropped_clip;
     uint64_t bin_pairs, bin_capacity, overflowed_draws;
+    /* partitioned tile shards (zr_cmd_set_tile_shard_exchange): the largest number
+     * of entries this rank routed to one destination in the draws since the
+     * previous sync point, and the draws (so far) whose received blocks overflowed
+     * zr_cmd_set_route_capacity and were set up in full instead */
+    uint64_t route_max_entries, route_fallback_draws;
 } zr_draw_stats;
 ZR_API zr_result zr_device_last_draw_stats(zr_device *dev, zr_draw_stats *out);
 /* Last error message recorded on this thread (for logging; never NULL). */
@@ -330,10 +335,11 @@ ZR_API void zr_cmd_draw_indexed(zr_cmd *cmd, uint32_t index_count, uint32_t inst
  * render passes touch only screen-tile rows r with r % count == rank. */
 ZR_API void zr_cmd_set_tile_shard(zr_cmd *cmd, uint32_t rank, uint32_t count);
 /* Partitioned tile-row shards: as zr_cmd_set_tile_shard, but each
- * draw's primitive setup is split across the ranks too.  Rank r routes only its
- * 1/count of the primitives to the ranks owning the tile rows they touch; the
- * routing lists are exchanged by `exchange`, an all-to-all the caller provides
- * (RCCL, MPI, ...), called from zr_submit once per draw on every rank:
+ * draw's primitive setup is split across the ranks too.  Rank r sets up only its
+ * 1/count of the primitives and ships each one's setup record to the ranks
+ * owning the tile rows it touches; the blocks of records are exchanged by
+ * `exchange`, an all-to-all the caller provides (RCCL, MPI, ...), called from
+ * zr_submit once per draw on every rank:
  *   send: `count` blocks of bytes_per_rank, block d for rank d;
  *   recv: the block each rank s addressed to this rank, at s * bytes_per_rank.
  * It must be ordered after earlier work on hip_stream and before later work on
@@ -343,6 +349,12 @@ typedef zr_result (*zr_exchange_fn)(void *user, void *hip_stream, const void *se
                                     uint64_t bytes_per_rank);
 ZR_API void zr_cmd_set_tile_shard_exchange(zr_cmd *cmd, uint32_t rank, uint32_t count, zr_exchange_fn exchange,
                                            void *user);
+/* Records per exchange block of later partitioned draws (bytes_per_rank = 16 +
+ * 48 * entries); 0 = the runtime's default (twice a uniform share + 4096 from 3
+ * ranks on).  Every rank must record the same value.  A block that would need
+ * more keeps `entries` and flags the overflow: its receiver then sets up every
+ * primitive of that draw itself (exact, slower; zr_draw_stats reports it). */
+ZR_API void zr_cmd_set_route_capacity(zr_cmd *cmd, uint32_t entries);
 
 /* Multi-GPU over RCCL inside the runtime (no reference counterpart).
  * One process per GPU.  Rank 0 makes two ids (zr_rccl_get_unique_id), the caller
@@ -363,6 +375,22 @@ ZR_API zr_result zr_device_init_rccl(zr_device *dev, const void *exchange_id, co
                                      int32_t rank);
 ZR_API zr_exchange_fn zr_rccl_exchange_fn(void);
 ZR_API zr_result zr_device_gather_tile_rows(zr_device *dev, zr_texture *tex, int32_t root);
+/* The point-to-point transfers the two collectives enqueue on this rank (host
+ * only, no device): zr_device_gather_tile_rows of a `height`-row image with
+ * `row_bytes` per row, and the built-in exchange's grouped send/recv pairing.
+ * Each op moves `bytes` at byte `offset` of the image (gather: the same offset on
+ * both sides) or of the send / receive buffer (exchange) to or from `peer`.
+ * Returns the number of ops (at most `capacity` written; out may be NULL), or -1
+ * for bad ranks. */
+typedef struct zr_transfer_op {
+    int32_t peer;
+    int32_t send; /* 1 = send to peer, 0 = receive from peer */
+    uint64_t offset, bytes;
+} zr_transfer_op;
+ZR_API int32_t zr_gather_plan(uint32_t height, uint64_t row_bytes, int32_t nranks, int32_t rank, int32_t root,
+                              zr_transfer_op *out, int32_t capacity);
+ZR_API int32_t zr_exchange_plan(int32_t nranks, int32_t rank, uint64_t bytes_per_rank, zr_transfer_op *out,
+                                int32_t capacity);
 
 /* -------------------------------------------------------------- submission */
 

@@ -157,3 +157,62 @@ def test_buffer_range_write_overflow_is_host_checked():
         rng.write(b"12345")
     assert e.value.code == zr.ERROR_OUT_OF_DEVICE_MEMORY
     rng.write(b"")  # empty write is a no-op (buffer.rs:301-303)
+
+
+# ----------------------------------------------- collective plans (host only)
+def _plan(fn, *args):
+    n = fn(*args, None, 0)
+    assert n >= 0
+    ops = (zr.zr_transfer_op * max(n, 1))()
+    assert fn(*args, ops, n) == n
+    return [(o.peer, o.send, o.offset, o.bytes) for o in ops[:n]]
+
+
+@pytest.mark.parametrize("height", [1080, 2160, 120, 40, 33, 1])
+@pytest.mark.parametrize("world", [2, 3, 4, 5, 8])
+@pytest.mark.parametrize("root", [0, 1])
+def test_gather_plan_covers_every_row_once(height, world, root):
+    """zr_device_gather_tile_rows' plan (zr_gather_plan) against shard.owned_rows:
+    the root receives every row it does not own exactly once, from that row's
+    owner, into the row's own place; each peer sends exactly its own rows to the
+    root; the root's rows never move; a partial last tile row moves only its rows."""
+    from zenith_amd import shard
+    root = root % world
+    row_bytes = 7680
+    lib = zr.lib()
+    want = {r: set(shard.owned_rows(height, r, world).tolist()) for r in range(world)}
+    recv = _plan(lib.zr_gather_plan, height, row_bytes, world, root, root)
+    got_rows = {}
+    for peer, send, off, nbytes in recv:
+        assert send == 0 and peer != root
+        assert off % row_bytes == 0 and nbytes % row_bytes == 0 and nbytes > 0
+        for y in range(off // row_bytes, (off + nbytes) // row_bytes):
+            assert y not in got_rows, f"row {y} received twice"
+            got_rows[y] = peer
+    assert set(got_rows) == set(range(height)) - want[root]
+    assert all(y in want[p] for y, p in got_rows.items())
+    sent = []
+    for r in range(world):
+        ops = _plan(lib.zr_gather_plan, height, row_bytes, world, r, root)
+        if r == root:
+            continue
+        assert all(send == 1 and peer == root for peer, send, _, _ in ops)
+        rows = {y for _, _, off, nb in ops for y in range(off // row_bytes, (off + nb) // row_bytes)}
+        assert rows == want[r]
+        sent += [(r, off, nb) for _, _, off, nb in ops]
+    assert sorted(sent) == sorted((p, off, nb) for p, _, off, nb in recv)  # every send has its receive
+
+
+@pytest.mark.parametrize("world", [1, 2, 3, 8, 32])
+def test_exchange_plan_pairs_every_peer(world):
+    """The built-in exchange's grouped send/recv (zr_exchange_plan): block p of the
+    send buffer goes to rank p, and rank p's block lands at p * bytes_per_rank; per
+    rank one send and one receive with every peer (itself included)."""
+    lib = zr.lib()
+    bpr = 16 + 48 * 1000
+    for r in range(world):
+        ops = _plan(lib.zr_exchange_plan, world, r, bpr)
+        assert sorted((p, s) for p, s, _, _ in ops) == sorted((p, s) for p in range(world) for s in (0, 1))
+        assert all(off == p * bpr and nb == bpr for p, _, off, nb in ops)
+    assert lib.zr_exchange_plan(33, 0, bpr, None, 0) == -1
+    assert lib.zr_gather_plan(1080, 7680, 2, 2, 0, None, 0) == -1

@@ -25,8 +25,8 @@ def test_algorithmic_bytes():
     n, pairs, px = 1_000_000, 1_315_362, 1920 * 1080
     # setup: inputs once + one 32-B compact record per triangle + a 4-B bin entry per pair
     assert bench.algorithmic_bytes("setup_bin", n, 120, pairs, px) == n * (120 + 32) + pairs * 4
-    # partitioned setup adds the 4-B id of every received triangle
-    assert bench.algorithmic_bytes("setup_bin", n, 120, pairs, px, n_route=10) == n * (120 + 32 + 4) + pairs * 4
+    # partitioned setup: a received 48-B route entry in, its 32-B record out
+    assert bench.algorithmic_bytes("setup_bin", n, 120, pairs, px, n_route=10) == n * (48 + 32) + pairs * 4
     # tile: bin entry + record per pair, colour + depth texel per owned pixel
     assert bench.algorithmic_bytes("tile", n, 120, pairs, px) == pairs * 36 + px * 8
     assert bench.algorithmic_bytes("route", n, 120, pairs, px, n_route=1000) == 48_000
@@ -61,3 +61,22 @@ def test_bench_json_line():
     assert cb["kind"] == "port" and cb["cores"] >= 1 and cb["value"] > 0
     assert cb["nproc"] == cb["cores"] and cb["nproc_all"] >= cb["nproc"] and cb["cpu_model"]
     assert set(d["kernels"]) >= {"setup_bin", "tile"}
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("setup", ["replicated", "partitioned"])
+def test_bench_emulate_shard(setup):
+    """--emulate-shard G: every rank of the shard timed in turn beside T1; the
+    speed-up is T1 / the slowest rank's frame, and partitioned ranks receive the
+    records the others really routed (no block overflow at the measured capacity)."""
+    cmd = [sys.executable, os.path.join(ROOT, "bench.py"), "--config", "c1", "--steps", "4", "--warmup", "2",
+           "--emulate-shard", "4", "--setup", setup, "--no-cpu-baseline"]
+    out = subprocess.run(cmd, cwd=ROOT, capture_output=True, text=True, timeout=110)
+    assert out.returncode == 0, out.stderr[-2000:]
+    d = json.loads([ln for ln in out.stdout.splitlines() if ln.strip()][-1])
+    assert len(d["rank_ms"]) == 4 and d["max_rank_ms"] == max(d["rank_ms"])
+    assert abs(d["speedup"] - d["t1_ms"] / d["max_rank_ms"]) < 1e-2
+    assert d["ranks"][d["max_rank"]]["ms"] == d["max_rank_ms"]
+    if setup == "partitioned":
+        assert d["route_capacity"] > 0 and all(r["route_fallback_draws"] == 0 for r in d["ranks"])
+        assert sum(r["triangles_setup"] for r in d["ranks"]) >= 100_000 * 0.9

@@ -104,8 +104,8 @@ def _a2a_worker(rank, world, port, n, out_path):
     send = shard.route_blocks(lo, hi, rank, world).reshape(-1)
     recv = torch.empty_like(send)
     dist.all_to_all_single(recv, send)  # RcclExchange's call, on host tensors
-    got = shard.received_primitives(recv, n, world)
-    ok = got == _expected(lo, hi, rank, world)
+    got, over = shard.received_primitives(recv, n, world)
+    ok = sorted(got) == _expected(lo, hi, rank, world) and not over
     np.save(f"{out_path}.{rank}.npy", np.array([ok]))
     dist.barrier()
     dist.destroy_process_group()
@@ -114,8 +114,8 @@ def _a2a_worker(rank, world, port, n, out_path):
 @pytest.mark.parametrize("world,n", [(2, 9000), (3, 5000)])
 def test_gloo_partitioned_exchange(world, n, tmp_path):
     """k_route's block layout (host model) through an all_to_all_single over gloo:
-    every rank receives exactly the primitives touching its tile rows, in API
-    order (several route chunks per rank at n=9000, G=2)."""
+    every rank receives exactly the primitives touching its tile rows (several
+    route chunks per rank at n=9000, G=2)."""
     out = str(tmp_path / "a2a")
     mp.spawn(_a2a_worker, args=(world, _free_port(), n, out), nprocs=world, join=True)
     for r in range(world):
@@ -130,16 +130,37 @@ def test_route_blocks_model():
     sends = [shard.route_blocks(lo, hi, r, world) for r in range(world)]
     for d in range(world):
         recv = torch.stack([sends[s][d] for s in range(world)])
-        assert shard.received_primitives(recv, n, world) == _expected(lo, hi, d, world)
+        got, over = shard.received_primitives(recv, n, world)
+        assert sorted(got) == _expected(lo, hi, d, world) and not over
+
+
+def test_route_blocks_overflow():
+    """A block capacity below a destination's share: the block keeps `cap`
+    entries, its header says total > count, and the receiver sees the overflow
+    (the device then sets up the whole draw on that rank)."""
+    from zenith_amd import shard
+    n, world, cap = 6000, 4, 100
+    lo, hi = _spans(n, seed=3)
+    sends = [shard.route_blocks(lo, hi, r, world, cap=cap) for r in range(world)]
+    for d in range(world):
+        recv = torch.stack([sends[s][d] for s in range(world)])
+        got, over = shard.received_primitives(recv, n, world, cap=cap)
+        assert over and len(got) == world * cap
+        assert set(got) <= set(_expected(lo, hi, d, world))
 
 
 def test_route_model_matches_device_constants():
-    """The host route model uses the kernels' chunk size (zr_internal.h)."""
+    """The host route model uses the kernels' chunk size, entry and header sizes
+    (zr_internal.h) and the runtime's default capacity (zr_runtime.cpp)."""
     import re
     from zenith_amd import shard
     src = open(os.path.join(ROOT, "zenith_amd", "csrc", "zr_internal.h")).read()
     assert int(re.search(r"kRouteChunk\s*=\s*(\d+)", src).group(1)) == shard.ROUTE_CHUNK
+    assert 'sizeof(RouteEntry) == 48' in src and 'sizeof(RouteHeader) == 16' in src
+    rt = open(os.path.join(ROOT, "zenith_amd", "csrc", "zr_runtime.cpp")).read()
+    assert "std::min<uint64_t>(span, (2 * span + G - 1) / G + 4096)" in rt and "if (G <= 2) return span;" in rt
     # 1M primitives over 8 ranks: span rounds ceil(N / G) up to whole chunks
-    chunks, span, bw = shard.route_geometry(1_000_000, 8)
-    assert span == 125_440 and bw == span + 1 and chunks == span // shard.ROUTE_CHUNK
+    chunks, span, cap, bb = shard.route_geometry(1_000_000, 8)
+    assert span == 125_440 and chunks == span // shard.ROUTE_CHUNK
+    assert cap == 2 * span // 8 + 4096 and bb == 16 + 48 * cap
     assert shard.route_range(1_000_000, 7, 8) == (7 * 125_440, 1_000_000)

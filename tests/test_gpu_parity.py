@@ -327,9 +327,11 @@ def test_resubmit_soup_graph_replay(resubmit_device):
 
 
 # ------------------------------------------- partitioned setup
-def render_partitioned(scene, world, **kw):
+def render_partitioned(scene, world, capacity=0, frames=1, **kw):
     """All `world` ranks of a partitioned tile-row shard, emulated by threads on
-    one GPU (each with its own RenderDevice); returns each rank's (colour, depth)."""
+    one GPU (each with its own RenderDevice); returns each rank's (colour, depth,
+    stats).  `capacity`: records per exchange block (0: the runtime's default);
+    `frames`: frames submitted back to back before the read-back."""
     import threading
     group = shard.ThreadGroupExchange.Group(world, "cuda:0")
     out = [None] * world
@@ -337,7 +339,8 @@ def render_partitioned(scene, world, **kw):
     def run(r):
         dev = rhi.RenderDevice(0)
         try:
-            out[r] = renderer.render_scene(dev, scene, shard=(r, world, shard.ThreadGroupExchange(group, r)), **kw)
+            sh = (r, world, shard.ThreadGroupExchange(group, r), capacity)
+            out[r] = renderer.render_scene(dev, scene, shard=sh, frames=frames, **kw)
             out[r] = out[r] + (dev.last_draw_stats(),)
         except BaseException as e:  # noqa: BLE001 - reported below
             out[r] = e
@@ -356,14 +359,17 @@ def render_partitioned(scene, world, **kw):
     return out
 
 
-def assert_partitioned_parity(scene, world, **kw):
-    oc, od = oracle.render(scene, **kw)
-    for r, (gc, gd, st) in enumerate(render_partitioned(scene, world, **kw)):
+def assert_partitioned_parity(scene, world, capacity=0, frames=1, nthreads=16, **kw):
+    oc, od = oracle.render(scene, nthreads=nthreads, **kw)
+    stats = []
+    for r, (gc, gd, st) in enumerate(render_partitioned(scene, world, capacity, frames, **kw)):
         rows = owned_rows(scene.height, 32, (r, world))
         bad = np.argwhere(np.any(gc[rows] != oc[rows], axis=-1))
         assert bad.size == 0, f"rank {r}/{world}: {len(bad)} pixels differ, first {bad[:5].tolist()}"
         if scene.depth:
             assert np.array_equal(gd[rows].view(np.uint32), od[rows].view(np.uint32)), f"rank {r}/{world} depth"
+        stats.append(st)
+    return stats
 
 
 @pytest.mark.parametrize("world", [1, 2, 3, 8])
@@ -449,6 +455,28 @@ def test_mixed_draw_sizes_no_sync(device):
 def test_partitioned_c2_full():
     """C2 (1M triangles, 1920x1080) as 8 partitioned ranks: union = oracle frame."""
     assert_partitioned_parity(scenes.config_scene("c2"), 8)
+
+
+def test_partitioned_c3_full():
+    """C3 (1M triangles, 3840x2160) as 8 partitioned ranks, two frames back to
+    back: each rank's ~1020 tiles take 4-wave tiles (tile_threads_for's
+    partitioned branch, >= 3.5 tiles per CU) and the second frame's route,
+    exchange and record binning run on the setup stream beside the first frame's
+    tile pass.  Union of the ranks' rows = the oracle frame; no block overflowed."""
+    stats = assert_partitioned_parity(scenes.config_scene("c3"), 8, frames=2)
+    assert all(st["route_fallback_draws"] == 0 for st in stats)
+    assert max(st["route_max_entries"] for st in stats) > 0
+
+
+@pytest.mark.parametrize("capacity", [1, 300])
+def test_partitioned_route_overflow(capacity):
+    """Exchange blocks far too small for the routed records: the receivers see the
+    overflow in the block headers and set up every primitive of the draw
+    themselves -- still exact -- and the stats report it."""
+    s = scenes.soup_scene(81, 8000, 320, 240, 10.0, scenes.PROGRAM_BLINN_PHONG)
+    stats = assert_partitioned_parity(s, 4, capacity=capacity)
+    assert all(st["route_fallback_draws"] >= 1 for st in stats)
+    assert all(st["route_max_entries"] > capacity for st in stats)
 
 
 def test_partitioned_overflow_spill(monkeypatch):

@@ -1,7 +1,7 @@
 #!/bin/bash
 # Builds an A/B variant of libzenith_raster with extra -D knobs into
 # zenith_amd/variants/<name>/ (load it with ZR_LIB_PATH=... for tests / bench.py).
-#   tools/build_variant.sh pf6 -DZR_TILE_PREFETCH=1 -DZR_TILE_WGS=6
+#   tools/build_variant.sh dbg -DZR_TILE_DEBUG=1
 set -e
 name=$1; shift
 root=$(cd "$(dirname "$0")/.." && pwd)

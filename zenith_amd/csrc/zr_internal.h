@@ -8,14 +8,10 @@ namespace zr {
 constexpr int kTile = 32;          // screen-tile edge in pixels (one workgroup per tile)
 constexpr int kTileShift = 5;
 constexpr int kTilePixels = kTile * kTile;
-#ifndef ZR_TILE_THREADS
-#define ZR_TILE_THREADS 256
-#endif
-constexpr int kTileThreads = ZR_TILE_THREADS;  // k_tile workgroup: 4 waves of 64 (build knob)
+constexpr int kTileThreads = 256;  // k_tile workgroup: 4 waves of 64 (512 for some passes: tile_threads_for)
 constexpr uint32_t kSortCap = 1024;     // tile-list segment sorted by area in LDS
 constexpr uint32_t kBigQueue = 512;     // k_tile: queued wave-path primitives per segment
-constexpr uint32_t kBigWide = 0x80000000u;  // queue entry: wide compact primitive (ZR_TILE_WIDE)
-constexpr uint32_t kSortBuckets = 64;   // bbox-shape classes: 8 width classes x 8 height classes
+constexpr uint32_t kSortBuckets = 64;   // cost classes: the lane walk's pair steps over bbox ∩ tile, min((steps - 1) >> 1, 63)
 constexpr int kSetupThreads = 1024;  // setup / bin workgroups (one LDS histogram each)
 constexpr uint32_t kSetupLdsBudget = 160u * 1024u;     // one k_setup_bin workgroup per CU owns the LDS
 constexpr uint32_t kSetupBboxLdsBytes = 96u * 1024u;  // cap on the per-workgroup bbox array in LDS
@@ -77,14 +73,10 @@ enum : uint32_t { kFlagSwapped = 1u, kFlagBias0 = 2u, kFlagBias1 = 4u, kFlagBias
 // raster path steps edges incrementally in 32-bit integers.
 constexpr int32_t kSmallExtent = 64 * 256;
 constexpr uint32_t kEmptyBox = 0xFFFFFFFFu;
-// Bin entry = primitive id | (shape class of its bbox ∩ tile, shape_bucket()) << kBinPrimBits
-// Size class of a bbox extent in pixels: 1, 2, 3, 4, 5-6, 7-8, 9-12, 13+.
-__host__ __device__ inline uint32_t extent_class(int d) {
-    return d <= 4 ? (uint32_t)(d - 1) : d <= 6 ? 4u : d <= 8 ? 5u : d <= 12 ? 6u : 7u;
-}
-// k_tile sorts a tile's entries by this so a 64-lane chunk shares one bbox shape
-// (the lane raster's nested row/column loops then hardly diverge).
-__host__ __device__ inline uint32_t shape_bucket(int w, int h) { return extent_class(w) * 8u + extent_class(h); }
+// Bin entry = setup record | cost class << kBinPrimBits, where the cost class is
+// the lane walk's pair steps over bbox ∩ tile, ceil(w / 2) * h, as
+// min((steps - 1) >> 1, kSortBuckets - 1) (k_setup_bin phase 4; k_tile sorts a
+// tile's entries by it so that a 64-lane chunk holds walks of similar length).
 constexpr uint32_t kBinPrimBits = 26;
 constexpr uint32_t kBinPrimMask = (1u << kBinPrimBits) - 1u;
 struct alignas(8) BBox {
@@ -92,12 +84,30 @@ struct alignas(8) BBox {
 };
 constexpr uint32_t kMaxTilesPerPass = 16384;  // LDS histogram of the setup pass (64 KB)
 
-// Partitioned setup for tile-row shards.  Rank r routes the
-// primitives of its range [r * span, (r + 1) * span) to the ranks owning the tile
-// rows they touch, kRouteChunk per workgroup of k_route.  Exchange block for one
-// destination = [1] u32 count, then up to `span` u32 primitive ids in no
-// particular order: the receiver's setup records are indexed by primitive id, so
-// visibility sequences are the API order whatever order the ids arrive in.
+// Partitioned setup for tile-row shards.  Rank r sets up the
+// primitives of its range [r * span, (r + 1) * span), kRouteChunk per workgroup
+// of k_route, and ships each set-up primitive -- its compact record, pixel bbox
+// and draw id -- to the ranks owning the tile rows it touches.  The exchange block
+// for one destination is a RouteHeader, then up to route_cap RouteEntry in no
+// particular order (workgroups append at atomically reserved offsets): the
+// receiver keys its records by the draw id, so visibility sequences are the API
+// order whatever order the entries arrive in.  A block that would hold more than
+// route_cap entries keeps the first route_cap and says so (total > count): its
+// receiver then sets up every primitive of the draw itself (exact, slower).
+struct alignas(16) RouteEntry {
+    TriCompact rec;   // dx1 == kCompactLarge: a large primitive, whose setup the receiver re-runs
+    uint32_t bb0, bb1;// clipped pixel bbox (BBox)
+    uint32_t gid;     // draw primitive
+    uint32_t pad;
+};
+static_assert(sizeof(RouteEntry) == 48, "RouteEntry must be 48 B");
+struct alignas(16) RouteHeader {
+    uint32_t count;   // entries in the block (<= route_cap)
+    uint32_t total;   // entries the sender had for this destination (> count: the block overflowed)
+    uint32_t pad[2];
+};
+static_assert(sizeof(RouteHeader) == 16, "RouteHeader must be 16 B");
+__host__ __device__ inline uint64_t route_block_bytes(uint32_t cap) { return sizeof(RouteHeader) + (uint64_t)cap * sizeof(RouteEntry); }
 constexpr uint32_t kRouteChunk = 512;
 constexpr int kRouteThreads = 512;   // 1 primitive per thread (a latency chain: index -> positions)
 constexpr uint32_t kMaxShards = 32;  // destination masks are u32
@@ -114,6 +124,8 @@ enum StatusWord : uint32_t {
     kStMaxPairs = 2,        // bin entries (ntiles * longest list) the largest such draw needs
     kStTrianglesSetup = 3,
     kStDroppedClip = 4,
+    kStRouteMax = 5,        // partitioned draws: the largest per-destination entry total routed (since the last sync)
+    kStRouteFallback = 6,   // partitioned draws whose received blocks overflowed (set up in full; since the last sync)
     kStWords = 16,
 };
 // Device counters of k_setup_bin, read by the draw's k_tile (tile 0 reports them
@@ -125,7 +137,11 @@ enum CounterWord : uint32_t {
     kCtWords = 32,
 };
 // draw_info words (written by k_setup_bin for k_tile)
-enum DrawInfoWord : uint32_t { kInfoRecords = 0, kInfoWords = 4 };
+enum DrawInfoWord : uint32_t {
+    kInfoRecords = 0,     // setup records the overflow scan covers (bboxes[0, n))
+    kInfoByPosition = 1,  // 1: bboxes are indexed by received position, records by gids[position] (records mode)
+    kInfoWords = 4,
+};
 
 struct DrawParams {
     // vertex input (binding 0) and index buffer
@@ -175,16 +191,17 @@ struct DrawParams {
     // tiling / sharding
     uint32_t tiles_x, tiles_y, shard_rank, shard_count, owned_rows, ntiles;
     uint32_t tile_threads;    // k_tile workgroup size: 256 or 512 (tile_threads_for)
-    // partitioned setup (list mode).  In list mode `prims` is the
-    // capacity of the received blocks (shard_count * span); the setup pass runs
-    // over the dense positions [0, sum of the blocks' counts) and writes the
-    // record of position j at its primitive id gids[j] (< draw_prims <= prims).
+    // partitioned setup (records mode).  In records mode `prims` is
+    // max(draw primitives, shard_count * route_cap); the setup pass runs over the
+    // dense positions [0, sum of the blocks' counts) of the received entries and
+    // stores each record at its draw id gids[j] (< draw_prims <= prims) -- or,
+    // when a received block overflowed, sets up every draw primitive (gids[j] = j).
     uint32_t draw_prims;      // primitives of the draw (instances * triangles per instance)
-    const uint32_t* list;     // received exchange blocks ([shard_count][list_block_words]), or nullptr
-    uint32_t list_block_words;// 1 + span
-    uint32_t* gids;           // list mode: the draw primitive at each dense position
-    uint32_t* route_out;      // k_route: this rank's send blocks ([shard_count][list_block_words])
-    uint32_t* route_counts;   // [shard_count + 1] ids per destination, finished workgroups (zero between routes)
+    const uint8_t* rlist;     // received exchange blocks ([shard_count] x route_block_bytes(route_cap)), or nullptr
+    uint32_t route_cap;       // entries per exchange block
+    uint32_t* gids;           // records mode: the draw primitive at each dense position
+    uint8_t* route_out;       // k_route: this rank's send blocks ([shard_count] x route_block_bytes(route_cap))
+    uint32_t* route_counts;   // [shard_count + 1] entries per destination, finished workgroups (zero between routes)
     uint32_t route_lo, route_hi, route_chunks;
     // scratch (binning without contended global atomics)
     TriCompact* records;      // [prims] compact records (every binned primitive)

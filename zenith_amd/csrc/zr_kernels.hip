@@ -1,16 +1,18 @@
 // zr_kernels.hip — the MI355X (gfx950) draw path.
 //
-//   k_setup_bin  one persistent launch, one 1024-thread workgroup per CU: vertex
-//                stage, clip (mesh program), viewport, 8-bit sub-pixel snap,
-//                facing/cull, orientation, top-left biases, clipped pixel bbox ->
-//                32-B compact record (64-B full record for large primitives);
-//                LDS histogram of tile overlaps; returning atomics on the tile
-//                counters; an XCD-hierarchical grid barrier; tile scan; scatter of
-//                (tile, primitive | cost bucket) pairs into the tile lists.  Also
-//                built as two launches cut at the barrier (split setup).
+//   k_setup_bin  one launch, one 1024-thread workgroup per CU (fewer for small
+//                draws), no grid barrier: vertex stage, clip (mesh program),
+//                viewport, 8-bit sub-pixel snap, facing/cull, orientation,
+//                top-left biases, clipped pixel bbox -> 32-B compact record (64-B
+//                full record for large primitives); an LDS histogram of the
+//                workgroup's (tile, primitive) pairs; returning atomics on the
+//                per-tile counters give the workgroup's offsets in each tile's
+//                fixed slab of the bin buffer; scatter of (primitive | cost
+//                class) entries into the slabs.  Workgroups never wait for each
+//                other, so nothing assumes co-residency.
 //   k_tile       one 256- or 512-thread workgroup per 32x32 tile: LDS-resident
 //                64-bit visibility keys (depth | primitive sequence) updated with
-//                ds_min_u64 -- lane per primitive for small ones (area-sorted
+//                ds_min_u64 -- lane per primitive for small ones (cost-sorted
 //                64-lane chunks), wave per primitive for large ones -- then a
 //                resolve that shades each pixel's winner once, encodes to the
 //                attachment format and writes colour + depth with coalesced
@@ -30,44 +32,23 @@
 
 namespace zr {
 
-// Build-time tuning knobs of k_tile (A/B builds: tools/build_variant.sh).
+// Diagnostic builds only (tools/build_variant.sh); production builds keep both 0.
 #ifndef ZR_TILE_WORK_STATS
-// Per-tile lane-walk steps and wave-path sweeps in the debug stamps (build knob:
-// the counting code costs k_tile 5 VGPRs, one wave per SIMD at 512 threads).
+// Per-tile lane-walk steps and wave-path sweeps in the debug stamps (the counting
+// code costs k_tile 5 VGPRs, one wave per SIMD at 512 threads).
 #define ZR_TILE_WORK_STATS 0
 #endif
-#ifndef ZR_TILE_WGS
-#define ZR_TILE_WGS 8        // k_tile workgroups per CU the register budget is sized for
-#endif
-#ifndef ZR_TILE_LPT
-#define ZR_TILE_LPT 1        // waves claim raster chunks largest-first from an LDS counter (0: static)
-#endif
-#ifndef ZR_RESOLVE_BATCH
-#define ZR_RESOLVE_BATCH 2   // pixels per thread whose gathers are in flight together in the resolve
-#endif
-#ifndef ZR_TILE_WIDE
-#define ZR_TILE_WIDE 0       // 1: the last cost bucket (127+ pair steps) goes to the wave path instead of lanes
-                             // (measured: cerberus tile pass 124 -> 107 us, C3 306 -> 327, C2 77 -> 79)
-#endif
-#ifndef ZR_TILE_BIGK
-#define ZR_TILE_BIGK 8       // lanes per entry at least, for the last sort bucket (127+ pair steps, ~253+ px)
-#endif
-#ifndef ZR_TILE_MIDK
-#define ZR_TILE_MIDK 4       // lanes per entry at least, for buckets ZR_TILE_MIDB.. (1: off)
-#endif
-#ifndef ZR_TILE_MIDB
-#define ZR_TILE_MIDB 24      // first bucket of the middle run: 49+ pair steps (~97+ px of bbox ∩ tile)
-#endif
-#ifndef ZR_TILE_SUBLANE
-#define ZR_TILE_SUBLANE 1    // sparse segments: k lanes per entry split its bbox rows (0: one lane per entry)
-#endif
 #ifndef ZR_TILE_DEBUG
-#define ZR_TILE_DEBUG 0      // 1: k_tile honours the ZR_DEBUG timing switches and stamps (A/B builds only;
-                             // the checks cost the production kernel SGPRs)
+#define ZR_TILE_DEBUG 0      // 1: k_tile honours the ZR_DEBUG timing switches and stamps
+                             // (the checks cost the production kernel SGPRs)
 #endif
-#ifndef ZR_SETUP_LOAD_PROBE
-#define ZR_SETUP_LOAD_PROBE 0  // 1: ZR_DEBUG=16 makes phase 1 issue its loads only (timing probe)
-#endif
+
+// k_tile tuning constants (DESIGN.md §4 has the measurements behind each).
+constexpr uint32_t kTileWgs = 8;     // 256-thread k_tile workgroups per CU the register budget is sized for
+constexpr uint32_t kResolveBatch = 2;  // pixels per thread whose gathers are in flight together in the resolve
+constexpr uint32_t kBigLanes = 8;    // lanes per entry at least, for the last cost bucket (127+ pair steps, ~253+ px)
+constexpr uint32_t kMidLanes = 4;    // lanes per entry at least, for buckets kMidBucket..62
+constexpr uint32_t kMidBucket = 24;  // first bucket of the middle run: 49+ pair steps (~97+ px of bbox ∩ tile)
 
 __constant__ float c_srgbT[255] = ZR_SRGB_THRESHOLDS_INIT;
 
@@ -298,23 +279,10 @@ __device__ __forceinline__ void fetch_indices_gid(const DrawParams& P, uint32_t 
     in.ok = ok;
 }
 
-// List mode: the draw primitive at dense position `pos` of the received blocks
-// (s_pre: exclusive prefix of the blocks' counts, G + 1 entries, in LDS).
-__device__ __forceinline__ uint32_t list_gid(const DrawParams& P, const uint32_t* s_pre, uint32_t pos) {
-    uint32_t src = 0;
-    while (src + 1u < P.shard_count && pos >= s_pre[src + 1u]) ++src;
-    return P.list[(size_t)src * P.list_block_words + 1u + (pos - s_pre[src])];
-}
-
-// Setup record `pos` (< n_pos): the draw primitive itself, or in list mode the
-// one at that dense position of the received blocks.
-__device__ __forceinline__ void fetch_indices(const DrawParams& P, uint32_t pos, uint32_t n_pos, const uint32_t* s_pre,
-                                              PrimIn& in, uint32_t& gid) {
+// Setup record `pos` (< n_pos): the draw primitive itself.
+__device__ __forceinline__ void fetch_indices(const DrawParams& P, uint32_t pos, uint32_t n_pos, PrimIn& in) {
     in.ok = pos < n_pos;
-    gid = pos;
-    if (!in.ok) return;
-    if (P.list) gid = list_gid(P, s_pre, pos);
-    fetch_indices_gid(P, gid, in);
+    if (in.ok) fetch_indices_gid(P, pos, in);
 }
 
 __device__ __forceinline__ void fetch_positions(const DrawParams& P, PrimIn& in) {
@@ -553,9 +521,10 @@ __device__ __forceinline__ int first_owned_row(uint32_t G, uint32_t rank, int ty
     return (int)(orow * G + rank);
 }
 
-__device__ __forceinline__ uint32_t count_owned(const DrawParams& P, const PrimGeom& g, uint32_t* s_hist) {
-    const int tx0 = g.px0 >> kTileShift, tx1 = g.px1 >> kTileShift;
-    const int ty0 = g.py0 >> kTileShift, ty1 = g.py1 >> kTileShift;
+__device__ __forceinline__ uint32_t count_owned_box(const DrawParams& P, int px0, int py0, int px1, int py1,
+                                                    uint32_t* s_hist) {
+    const int tx0 = px0 >> kTileShift, tx1 = px1 >> kTileShift;
+    const int ty0 = py0 >> kTileShift, ty1 = py1 >> kTileShift;
     const uint32_t G = P.shard_count, tiles_x = P.tiles_x;
     uint32_t owned = 0, orow;
     for (int ty = first_owned_row(G, P.shard_rank, ty0, orow); ty <= ty1; ty += (int)G, ++orow) {
@@ -566,9 +535,15 @@ __device__ __forceinline__ uint32_t count_owned(const DrawParams& P, const PrimG
     return owned;
 }
 
-// Stores setup record `rec` (compact, plus the full record for a large
-// triangle) and returns its tile bbox.
-__device__ __forceinline__ BBox write_record(const DrawParams& P, uint32_t rec, const PrimGeom& g) {
+__device__ __forceinline__ uint32_t count_owned(const DrawParams& P, const PrimGeom& g, uint32_t* s_hist) {
+    return count_owned_box(P, g.px0, g.py0, g.px1, g.py1, s_hist);
+}
+
+// A compact record (as two 16-B words) whose primitive is too large for int16 deltas.
+__device__ __forceinline__ bool compact_is_large(const int4 q0) { return (int16_t)(q0.z & 0xFFFF) == kCompactLarge; }
+
+// The compact record and the clipped pixel bbox of a set-up triangle.
+__device__ __forceinline__ TriCompact make_compact(const PrimGeom& g, BBox& box) {
     const int32_t* X = g.X;
     const int32_t* Y = g.Y;
     const float invA2 = 1.0f / (float)g.A2;
@@ -583,15 +558,22 @@ __device__ __forceinline__ BBox write_record(const DrawParams& P, uint32_t rec, 
     c.dz1 = g.z[1] - g.z[0];
     c.dz2 = g.z[2] - g.z[0];
     c.invA2s = (g.flags & kFlagSwapped) ? -invA2 : invA2;
-    P.records[rec] = c;
-    BBox box;
     box.bb0 = (uint32_t)g.px0 | ((uint32_t)g.py0 << 16);
     box.bb1 = (uint32_t)g.px1 | ((uint32_t)g.py1 << 16);
-    if (!small) {
+    return c;
+}
+
+// Stores setup record `rec` (compact, plus the full record for a large
+// triangle) and returns its tile bbox.
+__device__ __forceinline__ BBox write_record(const DrawParams& P, uint32_t rec, const PrimGeom& g) {
+    BBox box;
+    const TriCompact c = make_compact(g, box);
+    P.records[rec] = c;
+    if (!(g.flags & kFlagSmall)) {
         TriRecord r;
-        r.X0 = X[0]; r.Y0 = Y[0]; r.X1 = X[1]; r.Y1 = Y[1]; r.X2 = X[2]; r.Y2 = Y[2];
+        r.X0 = g.X[0]; r.Y0 = g.Y[0]; r.X1 = g.X[1]; r.Y1 = g.Y[1]; r.X2 = g.X[2]; r.Y2 = g.Y[2];
         r.z0 = c.z0; r.dz1 = c.dz1; r.dz2 = c.dz2;
-        r.invA2 = invA2;
+        r.invA2 = fabsf(c.invA2s);
         r.v0 = g.rv[0]; r.v1 = g.rv[1]; r.v2 = g.rv[2];
         r.bb0 = box.bb0;
         r.bb1 = box.bb1;
@@ -708,37 +690,63 @@ __device__ __forceinline__ BBox setup_finish_mesh(const DrawParams& P, uint32_t 
     return box[0];
 }
 
-// Setup of position `prim` (the draw primitive, or gid in list mode); returns its
-// tile bbox (empty when culled or owning no tile).
-__device__ __forceinline__ BBox setup_finish(const DrawParams& P, uint32_t prim, uint32_t gid, const PrimIn& in,
-                                             uint32_t* s_hist, int& nvalid, int& ndropped) {
+// Setup of draw primitive `prim`; returns its tile bbox (empty when culled or
+// owning no tile).
+__device__ __forceinline__ BBox setup_finish(const DrawParams& P, uint32_t prim, const PrimIn& in, uint32_t* s_hist,
+                                             int& nvalid, int& ndropped) {
     BBox box{kEmptyBox, 0u};
     PrimGeom g;
-    // List mode: the record is indexed by the draw primitive (records are sized
-    // for every primitive of the draw), so bins, keys and the resolve all use
-    // global primitive ids -- the visibility sequence is the API order whatever
-    // order the exchange delivered the primitives in.  gids maps the dense
-    // position back for phase 4 and the spill scan.
-    if (P.list) P.gids[prim] = gid;
     if (prim_geometry(P, in, g, ndropped)) {
         ++nvalid;
-        if (count_owned(P, g, s_hist)) box = write_record(P, P.list ? gid : prim, g);
+        if (count_owned(P, g, s_hist)) box = write_record(P, prim, g);
     }
     return box;
+}
+
+// Records mode (partitioned setup): received entry `pos` of the
+// blocks (s_pre: exclusive prefix of the blocks' counts, G + 1 entries, in LDS).
+// The sender set the primitive up: its compact record is stored at its draw id
+// and its bbox counted; a large primitive (no compact form) is set up again here
+// from the vertices every rank holds.  Returns the bbox; *gid = the draw id.
+__device__ __forceinline__ BBox receive_entry(const DrawParams& P, const uint32_t* s_pre, uint32_t pos, uint32_t* s_hist,
+                                              int& nvalid, int& ndropped, uint32_t& gid) {
+    uint32_t src = 0;
+    while (src + 1u < P.shard_count && pos >= s_pre[src + 1u]) ++src;
+    const int4* e = reinterpret_cast<const int4*>(P.rlist + (size_t)src * route_block_bytes(P.route_cap) +
+                                                  sizeof(RouteHeader) + (size_t)(pos - s_pre[src]) * sizeof(RouteEntry));
+    const int4 q0 = e[0], q1 = e[1], q2 = e[2];
+    gid = (uint32_t)q2.z;
+    BBox box{(uint32_t)q2.x, (uint32_t)q2.y};
+    ++nvalid;
+    if (!compact_is_large(q0)) {
+        int4* r = reinterpret_cast<int4*>(P.records + gid);
+        r[0] = q0;
+        r[1] = q1;
+        count_owned_box(P, (int)(box.bb0 & 0xFFFFu), (int)(box.bb0 >> 16), (int)(box.bb1 & 0xFFFFu), (int)(box.bb1 >> 16),
+                        s_hist);
+        return box;
+    }
+    PrimIn in;
+    fetch_indices_gid(P, gid, in);
+    fetch_positions(P, in);
+    PrimGeom g;
+    if (prim_geometry(P, in, g, ndropped) && count_owned(P, g, s_hist)) return write_record(P, gid, g);
+    return BBox{kEmptyBox, 0u};
 }
 
 // ----------------------------------------------------------------- k_route
 //
 // Partitioned setup, step 1 (tile-row shards): one pass over this
-// rank's primitive range [route_lo, route_hi).  Workgroup c owns primitives
-// route_lo + c * kRouteChunk + t (kRouteThreads per pass, coalesced): setup geometry ->
-// the set of ranks owning a tile row the bbox touches (ty % G == rank), then the
-// ids appended to each destination's block.  A workgroup reserves its run in a
-// block with one returning atomic per destination (route_counts[d]), so runs
-// land in any order: the receiver keys everything by the primitive id (setup
-// records are indexed by it in list mode), so block order carries no meaning.
-// The last workgroup to finish stores the block totals and re-zeroes the
-// counters for the next draw (they start zeroed when allocated).
+// rank's primitive range [route_lo, route_hi).  Thread t of workgroup c sets up
+// primitive route_lo + c * kRouteChunk + t (the same setup geometry k_setup_bin
+// computes) and appends its RouteEntry -- compact record, bbox, draw id -- to the
+// block of every rank owning a tile row the bbox touches (ty % G == rank).  A
+// workgroup reserves its run in a block with one returning atomic per
+// destination (route_counts[d]), so runs land in any order: the receiver keys
+// records by the draw id, so block order carries no meaning.  Entries past a
+// block's capacity are dropped and the header says so (total > count).  The
+// last workgroup to finish writes the block headers, reports the largest total,
+// and re-zeroes the counters for the next draw (they start zeroed).
 __device__ __forceinline__ uint32_t dest_mask(const DrawParams& P, const PrimGeom& g) {
     const uint32_t G = P.shard_count;
     const int ty0 = g.py0 >> kTileShift, ty1 = g.py1 >> kTileShift;
@@ -749,39 +757,32 @@ __device__ __forceinline__ uint32_t dest_mask(const DrawParams& P, const PrimGeo
 }
 
 __global__ __launch_bounds__(kRouteThreads) void k_route(DrawParams P) {
-    constexpr uint32_t kPer = kRouteChunk / kRouteThreads, kWaves = kRouteThreads / 64, kSlots = kPer * kWaves;
-    __shared__ uint32_t s_off[kSlots][kMaxShards];  // ids per (part, wave) and destination -> run offsets
+    constexpr uint32_t kWaves = kRouteThreads / 64;
+    static_assert(kRouteChunk == kRouteThreads, "k_route: one primitive per thread");
+    __shared__ uint32_t s_off[kWaves][kMaxShards];  // entries per (wave, destination) -> run offsets
     __shared__ uint32_t s_base[kMaxShards];
     __shared__ uint32_t s_last;
     const uint32_t G = P.shard_count, c = blockIdx.x, tid = threadIdx.x;
     const uint32_t lane = tid & 63u, wave = tid >> 6;
-    const uint32_t p0 = P.route_lo + c * kRouteChunk + tid;
-    PrimIn in[kPer];
-#pragma unroll
-    for (uint32_t k = 0; k < kPer; ++k) {
-        in[k].ok = p0 + k * kRouteThreads < P.route_hi;
-        if (in[k].ok) fetch_indices_gid(P, p0 + k * kRouteThreads, in[k]);
-    }
-#pragma unroll
-    for (uint32_t k = 0; k < kPer; ++k) fetch_positions(P, in[k]);
-    uint32_t m[kPer];
+    const uint32_t gid = P.route_lo + c * kRouteChunk + tid;
+    PrimIn in;
+    in.ok = gid < P.route_hi;
+    if (in.ok) fetch_indices_gid(P, gid, in);
+    fetch_positions(P, in);
     int ndropped = 0;
-#pragma unroll
-    for (uint32_t k = 0; k < kPer; ++k) {
-        PrimGeom g;
-        m[k] = prim_geometry(P, in[k], g, ndropped) ? dest_mask(P, g) : 0u;
-    }
+    PrimGeom g;
+    const uint32_t m = prim_geometry(P, in, g, ndropped) ? dest_mask(P, g) : 0u;
+    BBox box{kEmptyBox, 0u};
+    TriCompact rec;
+    if (m) rec = make_compact(g, box);
     for (uint32_t d = 0; d < G; ++d) {
-#pragma unroll
-        for (uint32_t k = 0; k < kPer; ++k) {
-            const uint32_t n = (uint32_t)__popcll(__ballot((m[k] >> d) & 1u));
-            if (lane == 0) s_off[k * kWaves + wave][d] = n;
-        }
+        const uint32_t n = (uint32_t)__popcll(__ballot((m >> d) & 1u));
+        if (lane == 0) s_off[wave][d] = n;
     }
     __syncthreads();
     if (tid < G) {
         uint32_t run = 0;
-        for (uint32_t i = 0; i < kSlots; ++i) {
+        for (uint32_t i = 0; i < kWaves; ++i) {
             const uint32_t n = s_off[i][tid];
             s_off[i][tid] = run;
             run += n;
@@ -790,21 +791,39 @@ __global__ __launch_bounds__(kRouteThreads) void k_route(DrawParams P) {
     }
     __syncthreads();
     const unsigned long long below = (1ull << lane) - 1ull;
+    const uint64_t block = route_block_bytes(P.route_cap);
     for (uint32_t d = 0; d < G; ++d) {
-        uint32_t* ids = P.route_out + (size_t)d * P.list_block_words + 1u + s_base[d];
-#pragma unroll
-        for (uint32_t k = 0; k < kPer; ++k) {
-            const bool on = (m[k] >> d) & 1u;
-            const unsigned long long b = __ballot(on);
-            if (on) ids[s_off[k * kWaves + wave][d] + (uint32_t)__popcll(b & below)] = p0 + k * kRouteThreads;
+        const bool on = (m >> d) & 1u;
+        const unsigned long long b = __ballot(on);
+        const uint32_t k = s_base[d] + s_off[wave][d] + (uint32_t)__popcll(b & below);
+        if (on && k < P.route_cap) {
+            int4* e = reinterpret_cast<int4*>(P.route_out + (size_t)d * block + sizeof(RouteHeader) + (size_t)k * sizeof(RouteEntry));
+            const int4* q = reinterpret_cast<const int4*>(&rec);
+            e[0] = q[0];
+            e[1] = q[1];
+            e[2] = make_int4((int)box.bb0, (int)box.bb1, (int)gid, 0);
         }
     }
     // every reservation of this workgroup has returned (s_base) before its arrival
     if (tid == 0) s_last = atomicAdd(&P.route_counts[G], 1u) + 1u == gridDim.x;
     __syncthreads();
-    if (s_last && tid < G) {
-        P.route_out[(size_t)tid * P.list_block_words] = atomicExch(&P.route_counts[tid], 0u);
-        if (tid == 0) atomicExch(&P.route_counts[G], 0u);
+    if (s_last) {
+        uint32_t total = 0;
+        if (tid < G) {
+            total = atomicExch(&P.route_counts[tid], 0u);
+            RouteHeader* h = reinterpret_cast<RouteHeader*>(P.route_out + (size_t)tid * block);
+            h->count = min(total, P.route_cap);
+            h->total = total;
+        }
+        if (tid < 64) {  // wave 0 holds every destination (G <= 32)
+#pragma unroll
+            for (int o = 32; o > 0; o >>= 1) total = max(total, (uint32_t)__shfl_xor((int)total, o, 64));
+            if (tid == 0) {
+                atomicExch(&P.route_counts[G], 0u);
+                volatile uint32_t* st = P.status;  // route kernels of successive draws run in stream order
+                if (total > st[kStRouteMax]) st[kStRouteMax] = total;
+            }
+        }
     }
 }
 
@@ -847,32 +866,64 @@ __global__ __launch_bounds__(kSetupThreads) void k_setup_bin(DrawParams P) {
     const uint32_t nt = P.ntiles, G = gridDim.x, w = blockIdx.x, tid = threadIdx.x;
     uint32_t* s_hist = s_lds;                       // histogram -> cursors
     uint32_t* s_misc = s_hist + ((nt + 3u) & ~3u);  // [32]
-    uint32_t* s_pre = s_misc + 32;       // list mode: exclusive prefix of the received blocks' counts
+    uint32_t* s_pre = s_misc + 32;       // records mode: exclusive prefix of the received blocks' counts
     // this workgroup's primitives' tile bboxes, indexed like phase 4's flattened
     // (own unit, primitive in unit) space, when they fit (P.bbox_lds)
     BBox* s_bbox = reinterpret_cast<BBox*>(s_misc + kSetupMiscWords);
     ZR_STAMP(0);
     for (uint32_t t = tid; t < nt; t += kSetupThreads) s_hist[t] = 0;
     if (tid < 32) s_misc[tid] = 0;
-    if (P.list && tid == 0) {
-        uint32_t run = 0;
+    // Partitioned draws (records mode): the received blocks' counts, and whether
+    // any block overflowed -- then this workgroup, like every other (they all read
+    // the same headers), sets up every primitive of the draw instead.
+    if (P.rlist && tid == 0) {
+        uint32_t run = 0, over = 0;
         for (uint32_t src = 0; src < P.shard_count; ++src) {
+            const RouteHeader* h = reinterpret_cast<const RouteHeader*>(P.rlist + (size_t)src * route_block_bytes(P.route_cap));
             s_pre[src] = run;
-            run += P.list[(size_t)src * P.list_block_words];
+            run += h->count;
+            over |= h->total > h->count ? 1u : 0u;
         }
         s_pre[P.shard_count] = run;
+        s_misc[4] = over ? 0u : 1u;
+        if (over && w == 0) {
+            volatile uint32_t* st = P.status;
+            st[kStRouteFallback] += 1u;
+        }
     }
     __syncthreads();
-    // setup records: the draw's primitives, or (list mode) the dense positions of
-    // the received blocks, in units of 2^unit_shift
-    const uint32_t n_pos = P.list ? min(s_pre[P.shard_count], P.prims) : P.prims;
-    const uint32_t units = P.list ? (n_pos + (1u << P.unit_shift) - 1u) >> P.unit_shift : P.units;
-    // records k_tile's overflow scan covers
-    if (w == 0 && tid == 0) P.draw_info[kInfoRecords] = MESH ? kMeshFans * n_pos : n_pos;
+    const bool rec_mode = s_misc[4] != 0u;
+    // setup records: the draw's primitives, or (records mode) the dense positions
+    // of the received entries, in units of 2^unit_shift
+    const uint32_t n_pos = rec_mode ? min(s_pre[P.shard_count], P.prims) : P.rlist ? P.draw_prims : P.prims;
+    const uint32_t units = rec_mode || P.rlist ? (n_pos + (1u << P.unit_shift) - 1u) >> P.unit_shift : P.units;
+    // records k_tile's overflow scan covers, and how their bboxes are indexed
+    if (w == 0 && tid == 0) {
+        P.draw_info[kInfoRecords] = MESH ? kMeshFans * n_pos : n_pos;
+        P.draw_info[kInfoByPosition] = rec_mode ? 1u : 0u;
+    }
 
     // ---- phase 1
     int nvalid = 0, ndropped = 0;
-    {
+    if (rec_mode) {  // the received entries: records stored at their draw ids, bboxes counted
+        const DrawParams& P = kernarg_params();
+        const uint32_t lane = tid & 63u, wave = tid >> 6;
+        const uint32_t usz = 1u << P.unit_shift;
+        for (uint32_t i = 0;; ++i) {
+            const uint32_t u = own_unit(w, G, wave + i * (kSetupThreads / 64u));
+            if (u >= units) break;
+            const uint32_t jw = wave + i * (kSetupThreads / 64u);  // own-unit ordinal
+            for (uint32_t r = lane; r < usz; r += 64u) {
+                const uint32_t pos = (u << P.unit_shift) + r;
+                if (pos >= n_pos) break;
+                uint32_t gid;
+                const BBox box = receive_entry(P, s_pre, pos, s_hist, nvalid, ndropped, gid);
+                P.gids[pos] = gid;
+                P.bboxes[pos] = box;
+                if (P.bbox_lds) s_bbox[(jw << P.unit_shift) + r] = box;
+            }
+        }
+    } else {
         const DrawParams& P = kernarg_params();  // phase 1's own loads of the parameters (SGPR pressure)
         const uint32_t lane = tid & 63u, wave = tid >> 6;
         const uint32_t rounds = (1u << P.unit_shift) / (64u * KB);
@@ -884,21 +935,10 @@ __global__ __launch_bounds__(kSetupThreads) void k_setup_bin(DrawParams P) {
                 const uint32_t pb = (u << P.unit_shift) + r * 64u * KB + lane;
                 const uint32_t lb = (jw << P.unit_shift) + r * 64u * KB + lane;
                 PrimIn in[KB];
-                uint32_t gid[KB];
 #pragma unroll
-                for (uint32_t b = 0; b < KB; ++b) fetch_indices(P, pb + b * 64u, n_pos, s_pre, in[b], gid[b]);
+                for (uint32_t b = 0; b < KB; ++b) fetch_indices(P, pb + b * 64u, n_pos, in[b]);
 #pragma unroll
                 for (uint32_t b = 0; b < KB; ++b) fetch_positions(P, in[b]);
-#if ZR_SETUP_LOAD_PROBE
-                if (P.debug & kDebugLoadOnly) {  // timing probe: the loads alone
-#pragma unroll
-                    for (uint32_t b = 0; b < KB; ++b)
-                        asm volatile("" ::"v"(in[b].p[0].x), "v"(in[b].p[0].y), "v"(in[b].p[0].z), "v"(in[b].p[1].x),
-                                     "v"(in[b].p[1].y), "v"(in[b].p[1].z), "v"(in[b].p[2].x), "v"(in[b].p[2].y),
-                                     "v"(in[b].p[2].z));
-                    continue;
-                }
-#endif
 #pragma unroll
                 for (uint32_t b = 0; b < KB; ++b) {
                     const uint32_t prim = pb + b * 64u;
@@ -907,7 +947,7 @@ __global__ __launch_bounds__(kSetupThreads) void k_setup_bin(DrawParams P) {
                     if constexpr (MESH)
                         box = setup_finish_mesh(P, prim, in[b], s_hist, nvalid, ndropped);
                     else
-                        box = setup_finish(P, prim, gid[b], in[b], s_hist, nvalid, ndropped);
+                        box = setup_finish(P, prim, in[b], s_hist, nvalid, ndropped);
                     // global: the overflow scan of any tile may need it; LDS: phase 4
                     P.bboxes[prim] = box;
                     if (P.bbox_lds) s_bbox[lb + b * 64u] = box;
@@ -955,7 +995,7 @@ __global__ __launch_bounds__(kSetupThreads) void k_setup_bin(DrawParams P) {
         }
     }
     ZR_STAMP(2);
-    if (!P.bbox_lds) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // phase 4 reads the global bboxes
+    if (!P.bbox_lds || rec_mode) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // phase 4 reads global bboxes / gids
     __syncthreads();
 
     // ---- phase 4: scatter the pairs of this workgroup's units, flattened over
@@ -996,7 +1036,7 @@ __global__ __launch_bounds__(kSetupThreads) void k_setup_bin(DrawParams P) {
             const uint32_t prim = (own_unit(w, G, j >> P.unit_shift) << P.unit_shift) + (j & (usz - 1u));
             if (prim >= n_pos) continue;
             const BBox bb = P.bbox_lds ? s_bbox[j] : P.bboxes[prim];
-            scatter(P.list && bb.bb0 != kEmptyBox ? P.gids[prim] : prim, bb);
+            scatter(rec_mode && bb.bb0 != kEmptyBox ? P.gids[prim] : prim, bb);
             if (MESH) {  // fans 1 and 2 (bboxes stored by this workgroup in phase 1)
                 scatter(mesh_record(P, prim, 1), P.bboxes[mesh_record(P, prim, 1)]);
                 scatter(mesh_record(P, prim, 2), P.bboxes[mesh_record(P, prim, 2)]);
@@ -1097,7 +1137,6 @@ __device__ __forceinline__ TriRecord load_uniform_record(const TriRecord* p) {
     return uniform_record(q[0], q[1], q[2], q[3]);
 }
 
-__device__ __forceinline__ bool compact_is_large(const int4 q0) { return (int16_t)(q0.z & 0xFFFF) == kCompactLarge; }
 
 // Row sweeps raster_prim makes over a record's bbox ∩ tile (kDebugStamps).
 __device__ __forceinline__ uint32_t prim_sweeps(const TriRecord& r, int x0, int y0) {
@@ -1355,7 +1394,7 @@ template <int PROG, int MODE, bool IDX32, int NT>
 __device__ __forceinline__ void resolve_pixels(const DrawParams& P, int x0, int y0, const unsigned long long* s_key,
                                                const float* s_srgb) {
     constexpr int kPer = kTilePixels / NT;
-    constexpr int kB = kPer < ZR_RESOLVE_BATCH ? kPer : ZR_RESOLVE_BATCH;
+    constexpr int kB = kPer < (int)kResolveBatch ? kPer : (int)kResolveBatch;
     // recomputed here, not reused from the tile's init: a pixel coordinate kept
     // live across the raster loop spills at 64 VGPRs
     int tid = (int)threadIdx.x;
@@ -1747,19 +1786,14 @@ __device__ __forceinline__ void resolve_tile(const DrawParams& P, int x0, int y0
 template <int PROG, int MODE, bool INITD, int NT>
 // (launch bounds: the second argument is the minimum waves per SIMD -- 8, i.e.
 // 64 VGPRs, for both sizes; 8 x 256 or 4 x 512 threads per CU)
-__global__ __launch_bounds__(NT, ZR_TILE_WGS * kTileThreads / 256) void k_tile(DrawParams P) {
+__global__ __launch_bounds__(NT, kTileWgs * kTileThreads / 256) void k_tile(DrawParams P) {
     // LDS: a workgroup's share of the CU's 160 KiB at the occupancy the launch
     // bounds ask for (8 x 256 or 4 x 512 threads: 20 or 40 KiB).  The keys (8 KiB)
     // become the resolve's hash table; one union holds the raster scratch (sorted
     // segment, wave-path queue, bucket counts, initial depths) and then the
     // resolve's per-winner array.
-    constexpr uint32_t kWgsPerCu = (uint32_t)ZR_TILE_WGS * (uint32_t)kTileThreads / (uint32_t)NT;
-#ifdef ZR_TILE_LDS_BYTES
-    constexpr uint32_t kBudget = ZR_TILE_LDS_BYTES * 512u / NT < 160u * 1024u / kWgsPerCu
-                                     ? ZR_TILE_LDS_BYTES * 512u / NT : 160u * 1024u / kWgsPerCu;  // A/B knob
-#else
+    constexpr uint32_t kWgsPerCu = kTileWgs * (uint32_t)kTileThreads / (uint32_t)NT;
     constexpr uint32_t kBudget = 160u * 1024u / kWgsPerCu;
-#endif
     constexpr uint32_t kMiscWords = 16;
     constexpr uint32_t kUnionWords = (kBudget - kTilePixels * 8u - 256u * 4u - kMiscWords * 4u) / 4u;
     static_assert(kSortCap + kBigQueue + kSortBuckets + (INITD ? kTilePixels : 0u) <= kUnionWords,
@@ -1769,7 +1803,7 @@ __global__ __launch_bounds__(NT, ZR_TILE_WGS * kTileThreads / 256) void k_tile(D
     __shared__ __attribute__((aligned(16))) uint32_t s_u[kUnionWords];
     __shared__ uint32_t s_misc[kMiscWords];
     uint32_t* s_sorted = s_u;                       // [kSortCap]
-    // wave-path primitives of the segment (large / wide), rasterized after its
+    // wave-path (large) primitives of the segment, rasterized after its
     // chunks by whichever wave claims them next: the area sort groups them, so the
     // wave owning their chunk would otherwise sweep them all alone
     uint32_t* s_big = s_u + kSortCap;               // [kBigQueue]
@@ -1902,29 +1936,29 @@ __global__ __launch_bounds__(NT, ZR_TILE_WGS * kTileThreads / 256) void k_tile(D
             // which split its bbox rows.  With no more chunks than waves each wave
             // takes one statically (measured faster there: C1 78 vs 85 us, C3 299
             // vs 304 us; LPT: C2 80 vs 82 us).
-            const uint32_t kl = ZR_TILE_SUBLANE ? min(8u, max(1u, (uint32_t)NT / max(n, 1u))) : 1u;
+            const uint32_t kl = min(8u, max(1u, (uint32_t)NT / max(n, 1u)));
             const uint32_t ksh_s = 31u - __clz(kl);  // lanes per entry: 1, 2, 4 or 8
             // entries of the last bucket (127+ pair steps, ~253+ pixels) get at least
-            // ZR_TILE_BIGK lanes: one lane would walk up to 1024 steps and hold
+            // kBigLanes lanes: one lane would walk up to 1024 steps and hold
             // its whole chunk (and the tile) for that long.  Chunks are 64 lanes of
             // this lane space: the first off63 entries kl lanes each, then the rest.
-            // Likewise buckets from ZR_TILE_MIDB up (bbox ∩ tile > 4 * MIDB px) get at
-            // least ZR_TILE_MIDK lanes.  Three runs of the sorted segment, each a
+            // Likewise buckets from kMidBucket up (bbox ∩ tile > 4 * kMidBucket px) get at
+            // least kMidLanes lanes.  Three runs of the sorted segment, each a
             // fixed number of lanes per entry.
-            const uint32_t ksh_b = max(ksh_s, (uint32_t)(31 - __clz(ZR_TILE_BIGK)));
+            const uint32_t ksh_b = max(ksh_s, (uint32_t)(31 - __clz(kBigLanes)));
             // (2 lanes from 129 px, 4 from 253: C3 tile pass 262 -> 219 us, cerberus 68
             // -> 60 us, C1 / C2 within noise; 4 lanes from 97 px, 8 from 253: C1 58 ->
             // 51 us, cerberus 60 -> 57, C3 219 -> 226, C2 equal -- the default.
             // Gating it on the middle run's length lost the gains: a few mid-size
             // entries already make the chunk that ends the tile.)
             const uint32_t off63 = s_bucket[kSortBuckets - 1];
-            const uint32_t offm = s_bucket[ZR_TILE_MIDB];
-            const uint32_t ksh_m = max(ksh_s, (uint32_t)(31 - __clz(ZR_TILE_MIDK)));
+            const uint32_t offm = s_bucket[kMidBucket];
+            const uint32_t ksh_m = max(ksh_s, (uint32_t)(31 - __clz(kMidLanes)));
             const uint32_t lsp_s = offm << ksh_s;                      // lane space of buckets < MIDB
             const uint32_t lsp_m = lsp_s + ((off63 - offm) << ksh_m);  // ... and up to the last bucket
             const uint32_t lanes_all = lsp_m + ((n - off63) << ksh_b);
             const uint32_t nch = (lanes_all + 63u) / 64u;
-            const bool lpt = ZR_TILE_LPT && nch > NT / 64u;
+            const bool lpt = nch > NT / 64u;
             for (uint32_t it = 0;; ++it) {
                 uint32_t claim = wave + it * (NT / 64u);  // static: wave w takes chunks w, w + waves, ...
                 if (lpt) {
@@ -1949,16 +1983,13 @@ __global__ __launch_bounds__(NT, ZR_TILE_WGS * kTileThreads / 256) void k_tile(D
                 const bool valid = j < n && !(tile_debug(P) & kDebugLoadOnly);
                 if (tile_debug(P) & kDebugLoadOnly) asm volatile("" ::"v"(q0.x), "v"(q1.x), "v"(my_prim));
                 const bool large = compact_is_large(q0);
-                // wide: bbox ∩ tile of 253+ pixels (the last sort bucket, which lumps
-                // 253..1024); one lane would walk them for up to 1024 steps
-                const bool wide = ZR_TILE_WIDE && j >= off63;
-                if (valid && !large && !wide && !(tile_debug(P) & kDebugSkipLanePath)) {
+                if (valid && !large && !(tile_debug(P) & kDebugSkipLanePath)) {
                     const TriRecord r = decode_compact(P, q0, q1, true);
                     raster_lane<MODE, INITD>(P, r, entry_seq<PROG>(P, my_prim), x0, y0, s_key, s_initd, sub, (int)ksh);
                 }
                 if (ZR_TILE_WORK_STATS && (tile_debug(P) & kDebugStamps)) {  // work of the chunk: its longest lane walk
                     int steps = 0;
-                    if (valid && !large && !wide) {
+                    if (valid && !large) {
                         const TriRecord r = decode_compact(P, q0, q1, true);
                         const int bw = min((int)(r.bb1 & 0xFFFFu), x0 + kTile - 1) - max((int)(r.bb0 & 0xFFFFu), x0) + 1;
                         const int bh = min((int)(r.bb1 >> 16), y0 + kTile - 1) - max((int)(r.bb0 >> 16), y0) + 1;
@@ -1968,9 +1999,9 @@ __global__ __launch_bounds__(NT, ZR_TILE_WGS * kTileThreads / 256) void k_tile(D
                     for (int o = 1; o < 64; o <<= 1) steps = max(steps, __shfl_xor(steps, o, 64));
                     if (lane == 0) atomicAdd(&s_dbg[0], (uint32_t)steps);
                 }
-                // large and wide primitives: queued for the segment's wave pass; the
-                // whole wave sweeps them itself only when the queue is full
-                const bool is_big = valid && (large || wide) && sub == 0;
+                // large primitives: queued for the segment's wave pass; the whole
+                // wave sweeps them itself only when the queue is full
+                const bool is_big = valid && large && sub == 0;
                 unsigned long long big = __ballot(is_big);
                 if (big) {
                     uint32_t base = 0;
@@ -1978,8 +2009,7 @@ __global__ __launch_bounds__(NT, ZR_TILE_WGS * kTileThreads / 256) void k_tile(D
                     base = (uint32_t)__builtin_amdgcn_readfirstlane((int)base);
                     if (base + (uint32_t)__popcll(big) <= kBigQueue) {
                         if (is_big)
-                            s_big[base + (uint32_t)__popcll(big & ((1ull << lane) - 1ull))] =
-                                my_prim | (large ? 0u : kBigWide);
+                            s_big[base + (uint32_t)__popcll(big & ((1ull << lane) - 1ull))] = my_prim;
                         big = 0;
                     }
                 }
@@ -1987,14 +2017,7 @@ __global__ __launch_bounds__(NT, ZR_TILE_WGS * kTileThreads / 256) void k_tile(D
                     const uint32_t i = (uint32_t)__builtin_ctzll(big);
                     big &= big - 1ull;
                     const uint32_t prim = (uint32_t)rl((int)my_prim, i);
-                    TriRecord r;
-                    if (rl((int)large, i)) {
-                        r = load_uniform_record(P.records_big + prim);
-                    } else {
-                        const int4 a = make_int4(rl(q0.x, i), rl(q0.y, i), rl(q0.z, i), rl(q0.w, i));
-                        const int4 b = make_int4(rl(q1.x, i), rl(q1.y, i), rl(q1.z, i), rl(q1.w, i));
-                        r = decode_compact(P, a, b, true);
-                    }
+                    const TriRecord r = load_uniform_record(P.records_big + prim);
                     raster_prim<MODE, INITD>(P, r, entry_seq<PROG>(P, prim), x0, y0, lane, s_key, s_initd);
                     if (ZR_TILE_WORK_STATS && (tile_debug(P) & kDebugStamps) && lane == 0) atomicAdd(&s_dbg[1], prim_sweeps(r, x0, y0));
                 }
@@ -2008,35 +2031,22 @@ __global__ __launch_bounds__(NT, ZR_TILE_WGS * kTileThreads / 256) void k_tile(D
                 if (i >= nbig || (tile_debug(P) & kDebugSkipWavePath)) break;
                 const bool two = i + 1u < nbig;
                 const uint32_t e0 = s_big[i], e1 = two ? s_big[i + 1u] : e0;
-                if (!((e0 | e1) & kBigWide)) {
-                    // both full records' loads in flight at once (one exposed latency
-                    // per claim), the second held in scalar registers
-                    const int4* a = reinterpret_cast<const int4*>(P.records_big + e0);
-                    const int4* b = reinterpret_cast<const int4*>(P.records_big + e1);
-                    const int4 a0 = a[0], a1 = a[1], a2 = a[2], a3 = a[3];
-                    const int4 b0 = b[0], b1 = b[1], b2 = b[2], b3 = b[3];
-                    const TriRecord ra = uniform_record(a0, a1, a2, a3);
-                    const TriRecord rb = uniform_record(b0, b1, b2, b3);
-                    raster_prim<MODE, INITD>(P, ra, entry_seq<PROG>(P, e0), x0, y0, lane, s_key, s_initd);
-                    if (two) raster_prim<MODE, INITD>(P, rb, entry_seq<PROG>(P, e1), x0, y0, lane, s_key, s_initd);
-                    continue;
-                }
-                for (uint32_t q = 0; q < (two ? 2u : 1u); ++q) {  // a wide entry (ZR_TILE_WIDE builds)
-                    const uint32_t e = q ? e1 : e0, prim = e & ~kBigWide;
-                    TriRecord r;
-                    if (!(e & kBigWide)) {
-                        r = load_uniform_record(P.records_big + prim);
-                    } else {
-                        const int4* rp = reinterpret_cast<const int4*>(P.records + prim);
-                        r = decode_compact(P, rp[0], rp[1], true);
-                    }
-                    raster_prim<MODE, INITD>(P, r, entry_seq<PROG>(P, prim), x0, y0, lane, s_key, s_initd);
-                }
+                // both full records' loads in flight at once (one exposed latency per
+                // claim), the second held in scalar registers
+                const int4* a = reinterpret_cast<const int4*>(P.records_big + e0);
+                const int4* b = reinterpret_cast<const int4*>(P.records_big + e1);
+                const int4 a0 = a[0], a1 = a[1], a2 = a[2], a3 = a[3];
+                const int4 b0 = b[0], b1 = b[1], b2 = b[2], b3 = b[3];
+                const TriRecord ra = uniform_record(a0, a1, a2, a3);
+                const TriRecord rb = uniform_record(b0, b1, b2, b3);
+                raster_prim<MODE, INITD>(P, ra, entry_seq<PROG>(P, e0), x0, y0, lane, s_key, s_initd);
+                if (two) raster_prim<MODE, INITD>(P, rb, entry_seq<PROG>(P, e1), x0, y0, lane, s_key, s_initd);
             }
             __syncthreads();
         }
         if (spill) {
             const uint32_t r0 = 0u, n_rec = P.draw_info[kInfoRecords];  // setup records of the draw
+            const bool by_pos = P.draw_info[kInfoByPosition] != 0u;
             for (uint32_t cb = r0 + wave * 64u; cb < n_rec; cb += NT) {
                 const uint32_t j = cb + (uint32_t)lane;
                 bool hit = false;
@@ -2046,9 +2056,9 @@ __global__ __launch_bounds__(NT, ZR_TILE_WGS * kTileThreads / 256) void k_tile(D
                     hit = bb.bb0 != kEmptyBox && (int)(bb.bb0 & 0xFFFFu) < x0 + kTile && (int)(bb.bb1 & 0xFFFFu) >= x0 &&
                           (int)(bb.bb0 >> 16) < y0 + kTile && (int)(bb.bb1 >> 16) >= y0;
                 }
-                uint32_t rec = j;  // bboxes by position; records by primitive in list mode
+                uint32_t rec = j;  // bboxes by position; records by draw primitive (records mode: gids)
                 if (hit) {
-                    if (P.list) rec = P.gids[j];
+                    if (by_pos) rec = P.gids[j];
                     const int4* rp = reinterpret_cast<const int4*>(P.records + rec);
                     q0 = rp[0];
                     q1 = rp[1];

@@ -134,7 +134,7 @@ struct zr_pipeline_t {
 };
 
 enum CmdType { C_BEGIN_RENDERING, C_END_RENDERING, C_BIND_PIPELINE, C_BIND_UNIFORM, C_SET_VIEWPORT, C_SET_SCISSOR,
-               C_BIND_VB, C_BIND_IB, C_DRAW, C_SET_SHARD, C_CLEAR_IMAGE };
+               C_BIND_VB, C_BIND_IB, C_DRAW, C_SET_SHARD, C_CLEAR_IMAGE, C_SET_ROUTE_CAP };
 
 struct RenderingState {
     zr_rect2d area;
@@ -197,13 +197,13 @@ struct ScratchSet {
     uint64_t counters_cap = 0;
     uint32_t* bins = nullptr;
     uint64_t bins_cap = 0;
-    uint32_t* xsend = nullptr;  // partitioned setup: exchange blocks (words)
+    uint8_t* xsend = nullptr;   // partitioned setup: exchange blocks (bytes)
     uint64_t xsend_cap = 0;
-    uint32_t* xrecv = nullptr;
+    uint8_t* xrecv = nullptr;
     uint64_t xrecv_cap = 0;
-    uint32_t* gids = nullptr;   // draw primitive per setup record (list mode)
+    uint32_t* gids = nullptr;   // draw primitive per received position (records mode)
     uint64_t gids_cap = 0;
-    uint32_t* rcounts = nullptr;// route: ids per destination block + finished workgroups
+    uint32_t* rcounts = nullptr;// route: entries per destination block + finished workgroups
     uint64_t rcounts_cap = 0;
     hipEvent_t setup_done = nullptr;  // k_setup_bin of the last draw that used this set
     hipEvent_t tile_done = nullptr;   // k_tile of the last draw that used this set
@@ -251,6 +251,7 @@ struct zr_device_t {
     // command lists submitted since the last sync point (in flight) + stats
     std::vector<zr_cmd*> pending;
     uint64_t overflowed_draws = 0;
+    uint64_t route_fallbacks = 0;  // partitioned draws set up in full after a block overflow
     hipStream_t own_stream = nullptr;  // `stream` unless zr_device_set_stream installed the caller's
     // multi-GPU (zr_device_init_rccl): one communicator for the partitioned-setup
     // exchange (setup stream), one for the tile-row gather (gather stream), so an
@@ -441,6 +442,12 @@ zr_result device_sync(zr_device* d) {
     d->last.triangles_dropped_clip = st[kStDroppedClip];
     d->overflowed_draws += st[kStOverflow];
     d->last.overflowed_draws = d->overflowed_draws;
+    // partitioned draws since the previous sync point
+    d->last.route_max_entries = st[kStRouteMax];
+    d->route_fallbacks += st[kStRouteFallback];
+    d->last.route_fallback_draws = d->route_fallbacks;
+    st[kStRouteMax] = 0;
+    st[kStRouteFallback] = 0;
     d->pending.clear();
     if (d->dbg_ts && !d->dbg_ts_path.empty()) dump_stamps(d);
     if (st[kStOverflow]) {
@@ -490,7 +497,16 @@ struct ExecState {
     uint32_t shard_rank = 0, shard_count = 1;
     zr_exchange_fn exchange = nullptr;
     void* exchange_user = nullptr;
+    uint32_t route_cap = 0;  // entries per exchange block (zr_cmd_set_route_capacity; 0: route_capacity_default)
 };
+
+// Entries per exchange block when the caller sets none: every primitive of the
+// range for two ranks or fewer, else twice a uniform share plus a margin.  A block
+// that still overflows is exact (its receiver sets up the whole draw), only slower.
+uint64_t route_capacity_default(uint64_t span, uint64_t G) {
+    if (G <= 2) return span;
+    return std::min<uint64_t>(span, (2 * span + G - 1) / G + 4096);
+}
 
 int32_t choose_depth_mode(bool test, bool write, int32_t op) {
     if (!test) return kDepthLastWins;
@@ -673,10 +689,12 @@ zr_result exec_draw(zr_device* d, ExecState& s, const Cmd& c, bool indexed) {
         const uint64_t G = s.shard_count;
         const uint64_t per_rank = (prims + G - 1) / G;
         span = std::max<uint64_t>(1, (per_rank + kRouteChunk - 1) / kRouteChunk) * kRouteChunk;
-        positions = G * span;
+        const uint64_t cap = std::max<uint64_t>(1, std::min<uint64_t>(span, s.route_cap ? s.route_cap : route_capacity_default(span, G)));
+        // received entries, or every draw primitive when a block overflowed
+        positions = std::max<uint64_t>(prims, G * cap);
         if (positions > kBinPrimMask)
             return fail(ZR_ERROR_FEATURE_NOT_PRESENT, "partitioned draw: more than 2^26-1 block positions");
-        P.list_block_words = (uint32_t)(span + 1);
+        P.route_cap = (uint32_t)cap;
         P.route_chunks = (uint32_t)(span / kRouteChunk);
         P.route_lo = (uint32_t)std::min<uint64_t>(prims, (uint64_t)s.shard_rank * span);
         P.route_hi = (uint32_t)std::min<uint64_t>(prims, (uint64_t)P.route_lo + span);
@@ -791,15 +809,16 @@ zr_result exec_draw(zr_device* d, ExecState& s, const Cmd& c, bool indexed) {
         S.main_reader_pending = false;
     }
     if (overlap && S.tile_done_valid) ZR_HIP(hipStreamWaitEvent(ss, S.tile_done, 0));
-    // debug early exits skip the self-reset at the end of k_setup_bin
+    // debug early exits skip the self-reset at the end of k_setup_bin; the memsets
+    // go on the stream that runs this draw's k_setup_bin, so they precede it
     if (d->debug) {
-        ZR_HIP(hipMemsetAsync(P.counters, 0, kCtWords * 4, d->stream));
-        ZR_HIP(hipMemsetAsync(P.tile_counts, 0, (size_t)P.ntiles * 4, d->stream));
+        ZR_HIP(hipMemsetAsync(P.counters, 0, kCtWords * 4, ss));
+        ZR_HIP(hipMemsetAsync(P.tile_counts, 0, (size_t)P.ntiles * 4, ss));
     }
     if (partitioned) {
-        const uint64_t words = (uint64_t)s.shard_count * P.list_block_words;
-        if ((rc = grow(d, S.xsend, S.xsend_cap, words, 4))) return rc;
-        if ((rc = grow(d, S.xrecv, S.xrecv_cap, words, 4))) return rc;
+        const uint64_t bytes = (uint64_t)s.shard_count * route_block_bytes(P.route_cap);
+        if ((rc = grow(d, S.xsend, S.xsend_cap, bytes, 1))) return rc;
+        if ((rc = grow(d, S.xrecv, S.xrecv_cap, bytes, 1))) return rc;
         if ((rc = grow(d, S.gids, S.gids_cap, positions, 4))) return rc;
         if (!S.rcounts) {  // k_route's block counters: zeroed once, re-zeroed by every route
             if ((rc = grow(d, S.rcounts, S.rcounts_cap, kMaxShards + 1, 4))) return rc;
@@ -812,20 +831,25 @@ zr_result exec_draw(zr_device* d, ExecState& s, const Cmd& c, bool indexed) {
         ZR_HIP(hipGetLastError());
         zr_result xr = ZR_SUCCESS;
         timed_launch(d, "exchange", ss, [&] {
-            xr = s.exchange(s.exchange_user, (void*)ss, S.xsend, S.xrecv, (uint64_t)P.list_block_words * 4u);
+            xr = s.exchange(s.exchange_user, (void*)ss, S.xsend, S.xrecv, route_block_bytes(P.route_cap));
         });
         if (xr != ZR_SUCCESS) return fail(xr, "tile-shard exchange callback failed: " + g_last_error);
-        P.list = S.xrecv;
+        P.rlist = S.xrecv;
         if (no_tiles) {  // routed and exchanged; nothing of this target to draw here
+            // joined back into the device stream like every other setup-stream pass, so
+            // a fence (or a caller stream waiting on the device stream) covers the
+            // route's reads of the caller's vertex and index buffers
             ZR_HIP(hipEventRecord(S.setup_done, ss));
+            ZR_HIP(hipStreamWaitEvent(d->stream, S.setup_done, 0));
             s.color_clear_pending = false;
             s.depth_clear_pending = false;
             return ZR_SUCCESS;
         }
-        // List-mode setup runs on the setup stream behind the exchange, so draw
-        // i+1's route, exchange and setup overlap draw i's tile pass (the main
-        // stream only runs tile passes).  k_setup_bin has no grid
-        // barrier, so sharing the GPU with the collectives' kernels is safe.
+        // Records-mode setup (binning the received records) runs on the setup
+        // stream behind the exchange, so draw i+1's route, exchange and binning
+        // overlap draw i's tile pass (the main stream only runs tile passes;
+        // DESIGN.md §7).  k_setup_bin has no grid barrier, so sharing the GPU with
+        // the collectives' kernels is safe.
         timed_launch(d, "setup_bin", ss, [&] { launch_setup_bin(P, ss); });
         ZR_HIP(hipEventRecord(S.setup_done, ss));
         ZR_HIP(hipStreamWaitEvent(d->stream, S.setup_done, 0));
@@ -922,6 +946,7 @@ zr_result execute(zr_device* d, zr_cmd* cmd) {
             s.exchange = c.exchange;
             s.exchange_user = c.exchange_user;
             break;
+        case C_SET_ROUTE_CAP: s.route_cap = c.a; break;
         }
         if (rc) return rc;
     }
@@ -1614,6 +1639,14 @@ ZR_API void zr_cmd_set_tile_shard_exchange(zr_cmd* c, uint32_t rank, uint32_t co
     c->has_exchange = true;
 }
 
+ZR_API void zr_cmd_set_route_capacity(zr_cmd* c, uint32_t entries) {
+    if (!c) return;
+    Cmd k;
+    k.type = C_SET_ROUTE_CAP;
+    k.a = entries;
+    c->cmds.push_back(k);
+}
+
 // ------------------------------------------------------------ multi-GPU (RCCL)
 
 namespace {
@@ -1629,16 +1662,61 @@ zr_result rccl_exchange(void* user, void* stream, const void* send, void* recv, 
         if (!rccl_all_to_all(send, recv, bytes_per_rank, d->comm_x, s, err)) return fail(ZR_ERROR_DEVICE_LOST, err);
         return ZR_SUCCESS;
     }
-    bool ok = rccl_group_start(err);
-    for (int p = 0; ok && p < d->comm_size; ++p) {
-        ok = rccl_send((const uint8_t*)send + (uint64_t)p * bytes_per_rank, bytes_per_rank, p, d->comm_x, s, err) &&
-             rccl_recv((uint8_t*)recv + (uint64_t)p * bytes_per_rank, bytes_per_rank, p, d->comm_x, s, err);
-    }
-    if (!rccl_group_end(err) || !ok) return fail(ZR_ERROR_DEVICE_LOST, err);
+    zr_transfer_op plan[2 * kMaxShards];
+    const int32_t n = zr_exchange_plan(d->comm_size, d->comm_rank, bytes_per_rank, plan, 2 * (int32_t)kMaxShards);
+    bool ok = n >= 0 && rccl_group_start(err);
+    for (int32_t i = 0; ok && i < n; ++i)
+        ok = plan[i].send ? rccl_send((const uint8_t*)send + plan[i].offset, plan[i].bytes, plan[i].peer, d->comm_x, s, err)
+                          : rccl_recv((uint8_t*)recv + plan[i].offset, plan[i].bytes, plan[i].peer, d->comm_x, s, err);
+    if (!rccl_group_end(err) || !ok) return fail(ZR_ERROR_DEVICE_LOST, err.empty() ? "bad exchange plan" : err);
     return ZR_SUCCESS;
 }
 
 }  // namespace
+
+// Host-side plans of the two collectives (no device needed; tests/test_abi.py).
+// Gather: every tile row is a contiguous span of the linear image, sent from its
+// owner (ty % nranks) straight into place on the root -- one send/recv per tile
+// row, no packing; the root's own rows do not move.  `offset` is the span's byte
+// offset in the image (the same on both sides), the last row may be partial.
+ZR_API int32_t zr_gather_plan(uint32_t height, uint64_t row_bytes, int32_t nranks, int32_t rank, int32_t root,
+                              zr_transfer_op* out, int32_t capacity) {
+    if (nranks < 1 || rank < 0 || rank >= nranks || root < 0 || root >= nranks) return -1;
+    const uint32_t tiles_y = (height + kTile - 1) / kTile;
+    int32_t n = 0;
+    for (uint32_t ty = 0; ty < tiles_y; ++ty) {
+        const int32_t owner = (int32_t)(ty % (uint32_t)nranks);
+        if (owner == root || (rank != root && rank != owner)) continue;
+        if (out && n < capacity) {
+            out[n].peer = rank == root ? owner : root;
+            out[n].send = rank == root ? 0 : 1;
+            out[n].offset = (uint64_t)ty * kTile * row_bytes;
+            out[n].bytes = (uint64_t)std::min<uint32_t>(kTile, height - ty * kTile) * row_bytes;
+        }
+        ++n;
+    }
+    return n;
+}
+
+// Exchange (all-to-all without ncclAllToAll): to every rank p (itself included)
+// send block p of the send buffer, and receive p's block for this rank at p *
+// bytes_per_rank of the receive buffer, paired per peer in one group.
+ZR_API int32_t zr_exchange_plan(int32_t nranks, int32_t rank, uint64_t bytes_per_rank, zr_transfer_op* out,
+                                int32_t capacity) {
+    if (nranks < 1 || nranks > (int32_t)kMaxShards || rank < 0 || rank >= nranks) return -1;
+    int32_t n = 0;
+    for (int32_t p = 0; p < nranks; ++p)
+        for (int32_t send = 1; send >= 0; --send) {
+            if (out && n < capacity) {
+                out[n].peer = p;
+                out[n].send = send;
+                out[n].offset = (uint64_t)p * bytes_per_rank;
+                out[n].bytes = bytes_per_rank;
+            }
+            ++n;
+        }
+    return n;
+}
 
 ZR_API int32_t zr_rccl_available(void) {
     std::string err;
@@ -1687,19 +1765,15 @@ ZR_API zr_result zr_device_gather_tile_rows(zr_device* d, zr_texture* t, int32_t
     ZR_HIP(hipEventRecord(d->frame_done, d->stream));
     ZR_HIP(hipStreamWaitEvent(d->gather_stream, d->frame_done, 0));
     const uint64_t row_bytes = (uint64_t)t->width * t->bpp;
-    const uint32_t tiles_y = (t->height + kTile - 1) / kTile;
-    const int G = d->comm_size, me = d->comm_rank;
+    const int32_t n = zr_gather_plan(t->height, row_bytes, d->comm_size, d->comm_rank, root, nullptr, 0);
+    std::vector<zr_transfer_op> plan((size_t)std::max(n, 0));
+    zr_gather_plan(t->height, row_bytes, d->comm_size, d->comm_rank, root, plan.data(), n);
     std::string err;
     bool ok = rccl_group_start(err);
-    // every tile row is a contiguous span of the linear image: sent from its owner
-    // straight into place on the root, no packing
-    for (uint32_t ty = 0; ok && ty < tiles_y; ++ty) {
-        const int owner = (int)(ty % (uint32_t)G);
-        if (owner == root) continue;
-        uint8_t* p = (uint8_t*)t->ptr + (uint64_t)ty * kTile * row_bytes;
-        const uint64_t bytes = (uint64_t)std::min<uint32_t>(kTile, t->height - ty * kTile) * row_bytes;
-        if (me == root) ok = rccl_recv(p, bytes, owner, d->comm_g, d->gather_stream, err);
-        else if (me == owner) ok = rccl_send(p, bytes, root, d->comm_g, d->gather_stream, err);
+    for (const zr_transfer_op& op : plan) {
+        uint8_t* p = (uint8_t*)t->ptr + op.offset;
+        ok = ok && (op.send ? rccl_send(p, op.bytes, op.peer, d->comm_g, d->gather_stream, err)
+                            : rccl_recv(p, op.bytes, op.peer, d->comm_g, d->gather_stream, err));
     }
     if (!rccl_group_end(err) || !ok) return fail(ZR_ERROR_DEVICE_LOST, err);
     ZR_HIP(hipEventRecord(t->gather_done, d->gather_stream));

@@ -175,12 +175,15 @@ class SceneRenderer:
 
 
 def render_scene(device: rhi.RenderDevice, scene: Scene, shard: Optional[tuple] = None, viewport=None,
-                 scissor=None):
-    """One frame of ``scene`` on the GPU; returns (colour, depth) host arrays."""
+                 scissor=None, frames: int = 1):
+    """``frames`` frames of ``scene`` on the GPU, submitted back to back with no
+    host wait in between; returns the last one's (colour, depth) host arrays."""
     color = rhi.Texture(device, rhi.TextureDesc.new_color("rt", scene.width, scene.height, scene.color_format))
     depth = rhi.Texture(device, rhi.TextureDesc.new_depth("ds", scene.width, scene.height)) if scene.depth else None
     r = SceneRenderer(device, scene)
     enc = r.record(color, depth, shard=shard, viewport=viewport, scissor=scissor)
+    for _ in range(frames - 1):
+        device.submit(enc)
     device.submit_and_wait(enc)
     out = (color.read(), depth.read() if depth is not None else None)
     enc.destroy()

@@ -557,10 +557,14 @@ class CommandEncoder:
         CommandEncoder::custom (zenith-sandbox/src/main.rs:35-45)."""
         lib().zr_cmd_clear_color_image(self.handle, texture.handle, C.byref((C.c_float * 4)(*value)))
 
-    def set_tile_shard(self, rank: int, count: int, exchange=None):
+    def set_tile_shard(self, rank: int, count: int, exchange=None, route_capacity: int = 0):
         """Tile-row shard of the following render passes.  With ``exchange`` (a
         :class:`zenith_amd.shard.Exchange`) primitive setup is partitioned across
-        the ranks too and routed through that all-to-all."""
+        the ranks too and its records routed through that all-to-all (DESIGN.md
+        §7), ``route_capacity`` records per block (0: the runtime's default; the
+        same on every rank)."""
+        if exchange is not None:
+            lib().zr_cmd_set_route_capacity(self.handle, route_capacity)
         if exchange is None:
             lib().zr_cmd_set_tile_shard(self.handle, rank, count)
         elif exchange == "rccl":  # the runtime's own all-to-all (RenderDevice.init_rccl)

@@ -9,6 +9,7 @@ so the same code is exercised with gloo on CPU in tests/test_dist.py.
 """
 from __future__ import annotations
 
+import numpy as np
 import torch
 import torch.distributed as dist
 
@@ -52,66 +53,89 @@ class TileRowGather:
 # ------------------------------------------------ partitioned setup exchange
 #
 # zr_cmd_set_tile_shard_exchange (include/zenith_raster.h): each
-# rank routes 1/G of a draw's primitives to the ranks owning the tile rows they
-# touch; the routing lists travel in one all-to-all per draw.  Host model of the
-# device layout (zr_internal.h kRouteChunk, zr_runtime.cpp exec_draw): rank r
-# routes primitives [r * span, (r + 1) * span) with span = ceil(ceil(N / G) /
-# ROUTE_CHUNK) * ROUTE_CHUNK; its block for one destination is [1] u32 count, then
-# up to `span` u32 primitive ids (block_words = span + 1).  The device appends a
-# workgroup's run of ids at an atomically reserved offset, so the order of the ids
-# in a block is unspecified: the receiver keys its setup records by primitive id.
+# rank sets up 1/G of a draw's primitives and ships each set-up primitive to the
+# ranks owning the tile rows it touches; the blocks travel in one all-to-all per
+# draw.  Host model of the device layout (zr_internal.h RouteEntry / RouteHeader,
+# zr_runtime.cpp exec_draw): rank r routes primitives [r * span, (r + 1) * span)
+# with span = ceil(ceil(N / G) / ROUTE_CHUNK) * ROUTE_CHUNK; its block for one
+# destination is a 16-B header (u32 count, u32 total, 2 pad) then `cap` 48-B
+# entries (32-B compact record, u32 bb0, u32 bb1, u32 draw id, pad).  The device
+# appends a workgroup's run of entries at an atomically reserved offset, so their
+# order in a block is unspecified: the receiver keys records by the draw id.  A
+# destination with more than `cap` entries gets the first `cap` and total > count.
 
-ROUTE_CHUNK = 512  # zr::kRouteChunk (primitives per k_route workgroup)
+ROUTE_CHUNK = 512   # zr::kRouteChunk (primitives per k_route workgroup)
+HEADER_BYTES = 16   # sizeof(zr::RouteHeader)
+ENTRY_BYTES = 48    # sizeof(zr::RouteEntry)
+_ENTRY = np.dtype([("rec", "<i4", 8), ("bb0", "<u4"), ("bb1", "<u4"), ("gid", "<u4"), ("pad", "<u4")])
+_HEADER = np.dtype([("count", "<u4"), ("total", "<u4"), ("pad", "<u4", 2)])
+assert _ENTRY.itemsize == ENTRY_BYTES and _HEADER.itemsize == HEADER_BYTES
 
 
-def route_geometry(n_prims: int, world: int):
-    """(chunks, span, block_words) of a G-way partitioned draw of n primitives."""
+def capacity_default(span: int, world: int) -> int:
+    """zr_runtime.cpp route_capacity_default: entries per block when the caller sets none."""
+    return span if world <= 2 else min(span, -(-2 * span // world) + 4096)
+
+
+def route_geometry(n_prims: int, world: int, cap: int = 0):
+    """(chunks, span, cap, block_bytes) of a G-way partitioned draw of n primitives
+    with `cap` entries per block (0: the runtime's default)."""
     per_rank = -(-n_prims // world)
     chunks = max(1, -(-per_rank // ROUTE_CHUNK))
     span = chunks * ROUTE_CHUNK
-    return chunks, span, span + 1
+    cap = max(1, min(span, cap if cap else capacity_default(span, world)))
+    return chunks, span, cap, HEADER_BYTES + cap * ENTRY_BYTES
 
 
 def route_range(n_prims: int, rank: int, world: int):
     """[lo, hi) of the primitives rank `rank` routes."""
-    _, span, _ = route_geometry(n_prims, world)
+    _, span, _, _ = route_geometry(n_prims, world)
     lo = min(n_prims, rank * span)
     return lo, min(n_prims, lo + span)
 
 
-def route_blocks(row_lo, row_hi, rank: int, world: int) -> torch.Tensor:
+def route_blocks(row_lo, row_hi, rank: int, world: int, cap: int = 0) -> torch.Tensor:
     """Host model of k_route for rank `rank`: row_lo/row_hi are each primitive's
-    first/last tile row (row_lo < 0: no sample).  Returns the send buffer,
-    [world][block_words] uint32 (as int64 for portability), ids in primitive order
-    (one of the orders the device may produce)."""
+    first/last tile row (row_lo < 0: no sample); the entries' bbox words carry
+    them (bb0 = row_lo, bb1 = row_hi) in place of a pixel bbox.  Returns the send
+    buffer, [world][block_bytes] uint8, entries in primitive order (one of the
+    orders the device may produce)."""
     n = len(row_lo)
-    _, span, bw = route_geometry(n, world)
-    send = torch.zeros((world, bw), dtype=torch.int64)
+    _, span, cap, bb = route_geometry(n, world, cap)
+    hdr = np.zeros(world, dtype=_HEADER)
+    ent = np.zeros((world, cap), dtype=_ENTRY)
     lo, hi = route_range(n, rank, world)
-    fill = [0] * world
     for p in range(lo, hi):
         a, b = int(row_lo[p]), int(row_hi[p])
         if a < 0:
             continue
         dests = range(world) if b - a + 1 >= world else sorted({t % world for t in range(a, b + 1)})
         for d in dests:
-            send[d, 1 + fill[d]] = p
-            fill[d] += 1
+            k = int(hdr[d]["total"])
+            if k < cap:
+                ent[d][k]["bb0"], ent[d][k]["bb1"], ent[d][k]["gid"] = a, b, p
+            hdr[d]["total"] = k + 1
+    hdr["count"] = np.minimum(hdr["total"], cap)
+    out = np.zeros((world, bb), dtype=np.uint8)
     for d in range(world):
-        send[d, 0] = fill[d]
-    return send
+        out[d, :HEADER_BYTES] = np.frombuffer(hdr[d:d + 1].tobytes(), dtype=np.uint8)
+        out[d, HEADER_BYTES:] = np.frombuffer(ent[d].tobytes(), dtype=np.uint8)
+    return torch.from_numpy(out)
 
 
-def received_primitives(recv: torch.Tensor, n_prims: int, world: int) -> list:
-    """Primitive ids a rank's received blocks hold, in block-position order (the
-    device's dense setup positions; the visibility keys use the ids themselves)."""
-    _, _, bw = route_geometry(n_prims, world)
-    recv = recv.reshape(world, bw)
-    out = []
+def received_primitives(recv: torch.Tensor, n_prims: int, world: int, cap: int = 0):
+    """(draw ids of a rank's received entries in block-position order -- the
+    device's dense setup positions --, True if a block overflowed: the device then
+    sets up every primitive instead)."""
+    _, _, cap, bb = route_geometry(n_prims, world, cap)
+    raw = recv.reshape(world, bb).numpy()
+    out, over = [], False
     for s in range(world):
-        k = int(recv[s, 0])
-        out += recv[s, 1:1 + k].tolist()
-    return out
+        h = np.frombuffer(raw[s, :HEADER_BYTES].tobytes(), dtype=_HEADER)[0]
+        e = np.frombuffer(raw[s, HEADER_BYTES:].tobytes(), dtype=_ENTRY)
+        out += e["gid"][:int(h["count"])].tolist()
+        over |= int(h["total"]) > int(h["count"])
+    return out, over
 
 
 class _DeviceBytes:

@@ -69,10 +69,15 @@ class zr_kernel_time(C.Structure):
     _fields_ = [("name", C.c_char * 32), ("total_ms", C.c_double), ("launches", C.c_uint64)]
 
 
+class zr_transfer_op(C.Structure):
+    _fields_ = [("peer", C.c_int32), ("send", C.c_int32), ("offset", C.c_uint64), ("bytes", C.c_uint64)]
+
+
 class zr_draw_stats(C.Structure):
     _fields_ = [("triangles_in", C.c_uint64), ("triangles_setup", C.c_uint64),
                 ("triangles_dropped_clip", C.c_uint64), ("bin_pairs", C.c_uint64),
-                ("bin_capacity", C.c_uint64), ("overflowed_draws", C.c_uint64)]
+                ("bin_capacity", C.c_uint64), ("overflowed_draws", C.c_uint64),
+                ("route_max_entries", C.c_uint64), ("route_fallback_draws", C.c_uint64)]
 
 
 class zr_buffer_desc(C.Structure):
@@ -213,6 +218,10 @@ _SIGS = {
     "zr_cmd_set_tile_shard": (None, [_P, C.c_uint32, C.c_uint32]),
     "zr_cmd_clear_color_image": (None, [_P, _P, C.POINTER(C.c_float * 4)]),
     "zr_cmd_set_tile_shard_exchange": (None, [_P, C.c_uint32, C.c_uint32, _P, _P]),
+    "zr_cmd_set_route_capacity": (None, [_P, C.c_uint32]),
+    "zr_gather_plan": (C.c_int32, [C.c_uint32, C.c_uint64, C.c_int32, C.c_int32, C.c_int32,
+                                   C.POINTER(zr_transfer_op), C.c_int32]),
+    "zr_exchange_plan": (C.c_int32, [C.c_int32, C.c_int32, C.c_uint64, C.POINTER(zr_transfer_op), C.c_int32]),
     "zr_device_set_stream": (_R, [_P, _P]),
     "zr_device_stream": (_P, [_P]),
     "zr_rccl_available": (C.c_int32, []),
