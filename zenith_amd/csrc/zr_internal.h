@@ -92,7 +92,7 @@ constexpr uint32_t kMaxTilesPerPass = 16384;  // LDS histogram of the setup pass
 // particular order (workgroups append at atomically reserved offsets): the
 // receiver keys its records by the draw id, so visibility sequences are the API
 // order whatever order the entries arrive in.  A block that would hold more than
-// route_cap entries keeps the first route_cap and says so (total > count): its
+// route_cap entries keeps route_cap of them and says so (total > route_cap): its
 // receiver then sets up every primitive of the draw itself (exact, slower).
 struct alignas(16) RouteEntry {
     TriCompact rec;   // dx1 == kCompactLarge: a large primitive, whose setup the receiver re-runs
@@ -102,8 +102,8 @@ struct alignas(16) RouteEntry {
 };
 static_assert(sizeof(RouteEntry) == 48, "RouteEntry must be 48 B");
 struct alignas(16) RouteHeader {
-    uint32_t count;   // entries in the block (<= route_cap)
-    uint32_t total;   // entries the sender had for this destination (> count: the block overflowed)
+    uint32_t pad0;
+    uint32_t total;   // entries the sender had for this destination; the block holds min(total, route_cap)
     uint32_t pad[2];
 };
 static_assert(sizeof(RouteHeader) == 16, "RouteHeader must be 16 B");
@@ -201,7 +201,6 @@ struct DrawParams {
     uint32_t route_cap;       // entries per exchange block
     uint32_t* gids;           // records mode: the draw primitive at each dense position
     uint8_t* route_out;       // k_route: this rank's send blocks ([shard_count] x route_block_bytes(route_cap))
-    uint32_t* route_counts;   // [shard_count + 1] entries per destination, finished workgroups (zero between routes)
     uint32_t route_lo, route_hi, route_chunks;
     // scratch (binning without contended global atomics)
     TriCompact* records;      // [prims] compact records (every binned primitive)

@@ -742,11 +742,11 @@ __device__ __forceinline__ BBox receive_entry(const DrawParams& P, const uint32_
 // computes) and appends its RouteEntry -- compact record, bbox, draw id -- to the
 // block of every rank owning a tile row the bbox touches (ty % G == rank).  A
 // workgroup reserves its run in a block with one returning atomic per
-// destination (route_counts[d]), so runs land in any order: the receiver keys
-// records by the draw id, so block order carries no meaning.  Entries past a
-// block's capacity are dropped and the header says so (total > count).  The
-// last workgroup to finish writes the block headers, reports the largest total,
-// and re-zeroes the counters for the next draw (they start zeroed).
+// destination on the block header's `total` (zero before every route: this
+// rank's previous records-mode setup on the scratch set, or the runtime, resets
+// it), so runs land in any order -- the receiver keys records by the draw id,
+// so block order carries no meaning.  Entries past a block's capacity are
+// dropped; the receiver reads count = min(total, capacity) and sees the overflow.
 __device__ __forceinline__ uint32_t dest_mask(const DrawParams& P, const PrimGeom& g) {
     const uint32_t G = P.shard_count;
     const int ty0 = g.py0 >> kTileShift, ty1 = g.py1 >> kTileShift;
@@ -761,7 +761,6 @@ __global__ __launch_bounds__(kRouteThreads) void k_route(DrawParams P) {
     static_assert(kRouteChunk == kRouteThreads, "k_route: one primitive per thread");
     __shared__ uint32_t s_off[kWaves][kMaxShards];  // entries per (wave, destination) -> run offsets
     __shared__ uint32_t s_base[kMaxShards];
-    __shared__ uint32_t s_last;
     const uint32_t G = P.shard_count, c = blockIdx.x, tid = threadIdx.x;
     const uint32_t lane = tid & 63u, wave = tid >> 6;
     const uint32_t gid = P.route_lo + c * kRouteChunk + tid;
@@ -780,6 +779,7 @@ __global__ __launch_bounds__(kRouteThreads) void k_route(DrawParams P) {
         if (lane == 0) s_off[wave][d] = n;
     }
     __syncthreads();
+    const uint64_t block = route_block_bytes(P.route_cap);
     if (tid < G) {
         uint32_t run = 0;
         for (uint32_t i = 0; i < kWaves; ++i) {
@@ -787,11 +787,11 @@ __global__ __launch_bounds__(kRouteThreads) void k_route(DrawParams P) {
             s_off[i][tid] = run;
             run += n;
         }
-        s_base[tid] = run ? atomicAdd(&P.route_counts[tid], run) : 0u;
+        uint32_t* total = &reinterpret_cast<RouteHeader*>(P.route_out + (size_t)tid * block)->total;
+        s_base[tid] = run ? atomicAdd(total, run) : 0u;
     }
     __syncthreads();
     const unsigned long long below = (1ull << lane) - 1ull;
-    const uint64_t block = route_block_bytes(P.route_cap);
     for (uint32_t d = 0; d < G; ++d) {
         const bool on = (m >> d) & 1u;
         const unsigned long long b = __ballot(on);
@@ -802,27 +802,6 @@ __global__ __launch_bounds__(kRouteThreads) void k_route(DrawParams P) {
             e[0] = q[0];
             e[1] = q[1];
             e[2] = make_int4((int)box.bb0, (int)box.bb1, (int)gid, 0);
-        }
-    }
-    // every reservation of this workgroup has returned (s_base) before its arrival
-    if (tid == 0) s_last = atomicAdd(&P.route_counts[G], 1u) + 1u == gridDim.x;
-    __syncthreads();
-    if (s_last) {
-        uint32_t total = 0;
-        if (tid < G) {
-            total = atomicExch(&P.route_counts[tid], 0u);
-            RouteHeader* h = reinterpret_cast<RouteHeader*>(P.route_out + (size_t)tid * block);
-            h->count = min(total, P.route_cap);
-            h->total = total;
-        }
-        if (tid < 64) {  // wave 0 holds every destination (G <= 32)
-#pragma unroll
-            for (int o = 32; o > 0; o >>= 1) total = max(total, (uint32_t)__shfl_xor((int)total, o, 64));
-            if (tid == 0) {
-                atomicExch(&P.route_counts[G], 0u);
-                volatile uint32_t* st = P.status;  // route kernels of successive draws run in stream order
-                if (total > st[kStRouteMax]) st[kStRouteMax] = total;
-            }
         }
     }
 }
@@ -876,22 +855,34 @@ __global__ __launch_bounds__(kSetupThreads) void k_setup_bin(DrawParams P) {
     // Partitioned draws (records mode): the received blocks' counts, and whether
     // any block overflowed -- then this workgroup, like every other (they all read
     // the same headers), sets up every primitive of the draw instead.
-    if (P.rlist && tid == 0) {
-        uint32_t run = 0, over = 0;
-        for (uint32_t src = 0; src < P.shard_count; ++src) {
-            const RouteHeader* h = reinterpret_cast<const RouteHeader*>(P.rlist + (size_t)src * route_block_bytes(P.route_cap));
-            s_pre[src] = run;
-            run += h->count;
-            over |= h->total > h->count ? 1u : 0u;
+    if (P.rlist && tid < 64) {  // one lane per source block (G <= 32): the headers' loads in flight together
+        const uint32_t src = tid;
+        uint32_t total = 0;
+        if (src < P.shard_count)
+            total = reinterpret_cast<const RouteHeader*>(P.rlist + (size_t)src * route_block_bytes(P.route_cap))->total;
+        const uint32_t cnt = min(total, P.route_cap);
+        uint32_t inc = cnt, top = total;
+#pragma unroll
+        for (int d = 1; d < 64; d <<= 1) {
+            const uint32_t y = __shfl_up(inc, d, 64);
+            if ((int)tid >= d) inc += y;
+            top = max(top, (uint32_t)__shfl_xor((int)top, d, 64));
         }
-        s_pre[P.shard_count] = run;
-        s_misc[4] = over ? 0u : 1u;
-        if (over && w == 0) {
+        if (src <= P.shard_count) s_pre[src] = inc - cnt;  // exclusive prefix; s_pre[G] = all entries
+        const bool over = __ballot(total > cnt) != 0ull;
+        if (tid == 0) s_misc[4] = over ? 0u : 1u;
+        if (tid == 0 && w == 0) {  // the draw's route statistics (one writer: workgroup 0)
             volatile uint32_t* st = P.status;
-            st[kStRouteFallback] += 1u;
+            if (over) st[kStRouteFallback] += 1u;
+            if (top > st[kStRouteMax]) st[kStRouteMax] = top;
         }
     }
     __syncthreads();
+    // This rank's own send headers are k_route's counters: the exchange has
+    // consumed them (it precedes this kernel on the setup stream), so they are
+    // zeroed here for the next route into this scratch set.
+    if (P.rlist && w == 0 && tid < P.shard_count)
+        reinterpret_cast<RouteHeader*>(P.route_out + (size_t)tid * route_block_bytes(P.route_cap))->total = 0u;
     const bool rec_mode = s_misc[4] != 0u;
     // setup records: the draw's primitives, or (records mode) the dense positions
     // of the received entries, in units of 2^unit_shift

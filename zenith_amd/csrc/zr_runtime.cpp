@@ -203,8 +203,7 @@ struct ScratchSet {
     uint64_t xrecv_cap = 0;
     uint32_t* gids = nullptr;   // draw primitive per received position (records mode)
     uint64_t gids_cap = 0;
-    uint32_t* rcounts = nullptr;// route: entries per destination block + finished workgroups
-    uint64_t rcounts_cap = 0;
+    uint64_t xsend_layout = 0;  // (shard count, route capacity) the send headers were last zeroed for
     hipEvent_t setup_done = nullptr;  // k_setup_bin of the last draw that used this set
     hipEvent_t tile_done = nullptr;   // k_tile of the last draw that used this set
     bool tile_done_valid = false;
@@ -443,10 +442,12 @@ zr_result device_sync(zr_device* d) {
     d->overflowed_draws += st[kStOverflow];
     d->last.overflowed_draws = d->overflowed_draws;
     // partitioned draws since the previous sync point
-    d->last.route_max_entries = st[kStRouteMax];
+    if (st[kStRouteMax]) {  // kept from the last interval with partitioned draws
+        d->last.route_max_entries = st[kStRouteMax];
+        st[kStRouteMax] = 0;
+    }
     d->route_fallbacks += st[kStRouteFallback];
     d->last.route_fallback_draws = d->route_fallbacks;
-    st[kStRouteMax] = 0;
     st[kStRouteFallback] = 0;
     d->pending.clear();
     if (d->dbg_ts && !d->dbg_ts_path.empty()) dump_stamps(d);
@@ -820,12 +821,20 @@ zr_result exec_draw(zr_device* d, ExecState& s, const Cmd& c, bool indexed) {
         if ((rc = grow(d, S.xsend, S.xsend_cap, bytes, 1))) return rc;
         if ((rc = grow(d, S.xrecv, S.xrecv_cap, bytes, 1))) return rc;
         if ((rc = grow(d, S.gids, S.gids_cap, positions, 4))) return rc;
-        if (!S.rcounts) {  // k_route's block counters: zeroed once, re-zeroed by every route
-            if ((rc = grow(d, S.rcounts, S.rcounts_cap, kMaxShards + 1, 4))) return rc;
-            ZR_HIP(hipMemsetAsync(S.rcounts, 0, (kMaxShards + 1) * 4, ss));
+        // The send headers' totals are k_route's counters: zero when the block
+        // layout is new; afterwards this rank's records-mode setup re-zeroes them
+        // once the exchange has consumed them (a rank without rows: below).
+        const uint64_t block = route_block_bytes(P.route_cap);
+        const uint64_t layout = ((uint64_t)s.shard_count << 32) | P.route_cap;
+        auto zero_headers = [&]() -> zr_result {
+            ZR_HIP(hipMemset2DAsync(S.xsend, block, 0, sizeof(RouteHeader), s.shard_count, ss));
+            return ZR_SUCCESS;
+        };
+        if (S.xsend_layout != layout) {
+            if ((rc = zero_headers())) return rc;
+            S.xsend_layout = layout;
         }
         P.route_out = S.xsend;
-        P.route_counts = S.rcounts;
         P.gids = S.gids;
         timed_launch(d, "route", ss, [&] { launch_route(P, ss); });
         ZR_HIP(hipGetLastError());
@@ -836,6 +845,7 @@ zr_result exec_draw(zr_device* d, ExecState& s, const Cmd& c, bool indexed) {
         if (xr != ZR_SUCCESS) return fail(xr, "tile-shard exchange callback failed: " + g_last_error);
         P.rlist = S.xrecv;
         if (no_tiles) {  // routed and exchanged; nothing of this target to draw here
+            if ((rc = zero_headers())) return rc;  // (no records-mode setup to reset them)
             // joined back into the device stream like every other setup-stream pass, so
             // a fence (or a caller stream waiting on the device stream) covers the
             // route's reads of the caller's vertex and index buffers
@@ -1024,7 +1034,7 @@ ZR_API void zr_device_destroy(zr_device* d) {
     for (ScratchSet& S : d->sets) {
         for (void* p : {(void*)S.records, (void*)S.records_big, (void*)S.mesh_edges, (void*)S.bboxes, (void*)S.tile_counts,
                         (void*)S.draw_info, (void*)S.counters, (void*)S.bins, (void*)S.xsend, (void*)S.xrecv,
-                        (void*)S.gids, (void*)S.rcounts})
+                        (void*)S.gids})
             if (p) (void)hipFree(p);
         if (S.setup_done) (void)hipEventDestroy(S.setup_done);
         if (S.tile_done) (void)hipEventDestroy(S.tile_done);

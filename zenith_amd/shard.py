@@ -58,17 +58,17 @@ class TileRowGather:
 # draw.  Host model of the device layout (zr_internal.h RouteEntry / RouteHeader,
 # zr_runtime.cpp exec_draw): rank r routes primitives [r * span, (r + 1) * span)
 # with span = ceil(ceil(N / G) / ROUTE_CHUNK) * ROUTE_CHUNK; its block for one
-# destination is a 16-B header (u32 count, u32 total, 2 pad) then `cap` 48-B
+# destination is a 16-B header (u32 pad, u32 total, 2 pad) then `cap` 48-B
 # entries (32-B compact record, u32 bb0, u32 bb1, u32 draw id, pad).  The device
 # appends a workgroup's run of entries at an atomically reserved offset, so their
-# order in a block is unspecified: the receiver keys records by the draw id.  A
-# destination with more than `cap` entries gets the first `cap` and total > count.
+# order in a block is unspecified: the receiver keys records by the draw id.  The
+# block holds min(total, cap) entries; total > cap tells the receiver it overflowed.
 
 ROUTE_CHUNK = 512   # zr::kRouteChunk (primitives per k_route workgroup)
 HEADER_BYTES = 16   # sizeof(zr::RouteHeader)
 ENTRY_BYTES = 48    # sizeof(zr::RouteEntry)
 _ENTRY = np.dtype([("rec", "<i4", 8), ("bb0", "<u4"), ("bb1", "<u4"), ("gid", "<u4"), ("pad", "<u4")])
-_HEADER = np.dtype([("count", "<u4"), ("total", "<u4"), ("pad", "<u4", 2)])
+_HEADER = np.dtype([("pad0", "<u4"), ("total", "<u4"), ("pad", "<u4", 2)])
 assert _ENTRY.itemsize == ENTRY_BYTES and _HEADER.itemsize == HEADER_BYTES
 
 
@@ -115,7 +115,6 @@ def route_blocks(row_lo, row_hi, rank: int, world: int, cap: int = 0) -> torch.T
             if k < cap:
                 ent[d][k]["bb0"], ent[d][k]["bb1"], ent[d][k]["gid"] = a, b, p
             hdr[d]["total"] = k + 1
-    hdr["count"] = np.minimum(hdr["total"], cap)
     out = np.zeros((world, bb), dtype=np.uint8)
     for d in range(world):
         out[d, :HEADER_BYTES] = np.frombuffer(hdr[d:d + 1].tobytes(), dtype=np.uint8)
@@ -133,8 +132,8 @@ def received_primitives(recv: torch.Tensor, n_prims: int, world: int, cap: int =
     for s in range(world):
         h = np.frombuffer(raw[s, :HEADER_BYTES].tobytes(), dtype=_HEADER)[0]
         e = np.frombuffer(raw[s, HEADER_BYTES:].tobytes(), dtype=_ENTRY)
-        out += e["gid"][:int(h["count"])].tolist()
-        over |= int(h["total"]) > int(h["count"])
+        out += e["gid"][:min(int(h["total"]), cap)].tolist()
+        over |= int(h["total"]) > cap
     return out, over
 
 
