@@ -14,7 +14,7 @@ constexpr uint32_t kBigQueue = 512;     // k_tile: queued wave-path primitives p
 constexpr uint32_t kSortBuckets = 64;   // cost classes: the lane walk's pair steps over bbox ∩ tile, min((steps - 1) >> 1, 63)
 constexpr int kSetupThreads = 1024;  // setup / bin workgroups (one LDS histogram each)
 constexpr uint32_t kSetupLdsBudget = 160u * 1024u;     // one k_setup_bin workgroup per CU owns the LDS
-constexpr uint32_t kSetupBboxLdsBytes = 96u * 1024u;  // cap on the per-workgroup bbox + rank arrays in LDS
+constexpr uint32_t kSetupBboxLdsBytes = 96u * 1024u;  // cap on the per-workgroup bbox array in LDS
 
 enum Program : int32_t { kProgTriangle = 0, kProgFlat = 1, kProgBlinn = 2, kProgMesh = 3, kProgCount = 4 };
 

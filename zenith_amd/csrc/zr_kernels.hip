@@ -521,51 +521,22 @@ __device__ __forceinline__ int first_owned_row(uint32_t G, uint32_t rank, int ty
     return (int)(orow * G + rank);
 }
 
-// Pairs of a primitive with at most kRankedPairs owned tiles take their rank
-// within this workgroup's share of each tile list right here (a returning LDS
-// add on the ranked histogram), so phase 4 places them without an atomic; a
-// primitive with more pairs counts in the unranked histogram, whose cursors
-// phase 4 advances with atomics.  ranks: kRankedPairs u16 in (row, column)
-// order when `keep` (else none are kept: every pair unranked).
-constexpr uint32_t kRankedPairs = 4;
-
-__device__ __forceinline__ uint32_t owned_pairs(const DrawParams& P, int py0, int py1, int tx0, int tx1) {
-    const int ty0 = py0 >> kTileShift, ty1 = py1 >> kTileShift;
-    uint32_t orow;
-    const int first = first_owned_row(P.shard_count, P.shard_rank, ty0, orow);
-    const uint32_t rows = first > ty1 ? 0u : (uint32_t)(ty1 - first) / P.shard_count + 1u;
-    return rows * (uint32_t)(tx1 - tx0 + 1);
-}
-
 __device__ __forceinline__ uint32_t count_owned_box(const DrawParams& P, int px0, int py0, int px1, int py1,
-                                                    uint32_t* s_hist, uint32_t* s_hist2, bool keep, uint2& ranks) {
+                                                    uint32_t* s_hist) {
     const int tx0 = px0 >> kTileShift, tx1 = px1 >> kTileShift;
     const int ty0 = py0 >> kTileShift, ty1 = py1 >> kTileShift;
     const uint32_t G = P.shard_count, tiles_x = P.tiles_x;
-    const uint32_t n = owned_pairs(P, py0, py1, tx0, tx1);
-    const bool ranked = keep && n <= kRankedPairs;
-    uint32_t* hist = ranked ? s_hist : s_hist2;
-    uint32_t lo = 0, hi = 0, k = 0, orow;
+    uint32_t owned = 0, orow;
     for (int ty = first_owned_row(G, P.shard_rank, ty0, orow); ty <= ty1; ty += (int)G, ++orow) {
         const uint32_t row = orow * tiles_x;
-        for (int tx = tx0; tx <= tx1; ++tx) {
-            if (ranked) {
-                const uint32_t r = atomicAdd(&hist[row + tx], 1u) << ((k & 1u) * 16u);
-                lo |= k < 2u ? r : 0u;
-                hi |= k < 2u ? 0u : r;
-                ++k;
-            } else {
-                atomicAdd(&hist[row + tx], 1u);
-            }
-        }
+        for (int tx = tx0; tx <= tx1; ++tx) atomicAdd(&s_hist[row + tx], 1u);
+        owned += (uint32_t)(tx1 - tx0 + 1);
     }
-    ranks = make_uint2(lo, hi);
-    return n;
+    return owned;
 }
 
-__device__ __forceinline__ uint32_t count_owned(const DrawParams& P, const PrimGeom& g, uint32_t* s_hist,
-                                                uint32_t* s_hist2, bool keep, uint2& ranks) {
-    return count_owned_box(P, g.px0, g.py0, g.px1, g.py1, s_hist, s_hist2, keep, ranks);
+__device__ __forceinline__ uint32_t count_owned(const DrawParams& P, const PrimGeom& g, uint32_t* s_hist) {
+    return count_owned_box(P, g.px0, g.py0, g.px1, g.py1, s_hist);
 }
 
 // A compact record (as two 16-B words) whose primitive is too large for int16 deltas.
@@ -666,7 +637,7 @@ __device__ __forceinline__ uint32_t mesh_record(const DrawParams& P, uint32_t p,
 // The mesh program's setup of primitive `prim`: returns fan 0's bbox, stores fans
 // 1 and 2's in their global slots (empty when absent).
 __device__ __forceinline__ BBox setup_finish_mesh(const DrawParams& P, uint32_t prim, const PrimIn& in,
-                                                  uint32_t* s_hist2, int& nvalid, int& ndropped) {
+                                                  uint32_t* s_hist, int& nvalid, int& ndropped) {
     BBox box[kMeshFans];
 #pragma unroll
     for (uint32_t k = 0; k < kMeshFans; ++k) box[k] = BBox{kEmptyBox, 0u};
@@ -682,8 +653,7 @@ __device__ __forceinline__ BBox setup_finish_mesh(const DrawParams& P, uint32_t 
         PrimGeom g;
         if (mesh_geometry_unclipped(P, in, c, g, ndropped)) {
             ++nvalid;
-            uint2 rk;
-            if (count_owned(P, g, nullptr, s_hist2, false, rk)) {
+            if (count_owned(P, g, s_hist)) {
                 box[0] = write_record(P, prim, g);
                 float e[12];
                 mesh_edge_planes(P, in.p, e);
@@ -700,8 +670,7 @@ __device__ __forceinline__ BBox setup_finish_mesh(const DrawParams& P, uint32_t 
             bool owned = false;
             for (uint32_t k = 0; k < kMeshFans; ++k) {
                 if (!((m.valid >> k) & 1u)) continue;
-                uint2 rk;
-                if (count_owned(P, m.f[k], nullptr, s_hist2, false, rk)) {
+                if (count_owned(P, m.f[k], s_hist)) {
                     box[k] = write_record(P, mesh_record(P, prim, k), m.f[k]);
                     owned = true;
                 }
@@ -724,12 +693,12 @@ __device__ __forceinline__ BBox setup_finish_mesh(const DrawParams& P, uint32_t 
 // Setup of draw primitive `prim`; returns its tile bbox (empty when culled or
 // owning no tile).
 __device__ __forceinline__ BBox setup_finish(const DrawParams& P, uint32_t prim, const PrimIn& in, uint32_t* s_hist,
-                                             uint32_t* s_hist2, bool keep, uint2& ranks, int& nvalid, int& ndropped) {
+                                             int& nvalid, int& ndropped) {
     BBox box{kEmptyBox, 0u};
     PrimGeom g;
     if (prim_geometry(P, in, g, ndropped)) {
         ++nvalid;
-        if (count_owned(P, g, s_hist, s_hist2, keep, ranks)) box = write_record(P, prim, g);
+        if (count_owned(P, g, s_hist)) box = write_record(P, prim, g);
     }
     return box;
 }
@@ -740,8 +709,7 @@ __device__ __forceinline__ BBox setup_finish(const DrawParams& P, uint32_t prim,
 // and its bbox counted; a large primitive (no compact form) is set up again here
 // from the vertices every rank holds.  Returns the bbox; *gid = the draw id.
 __device__ __forceinline__ BBox receive_entry(const DrawParams& P, const uint32_t* s_pre, uint32_t pos, uint32_t* s_hist,
-                                              uint32_t* s_hist2, bool keep, uint2& ranks, int& nvalid,
-                                              int& ndropped, uint32_t& gid) {
+                                              int& nvalid, int& ndropped, uint32_t& gid) {
     uint32_t src = 0;
     while (src + 1u < P.shard_count && pos >= s_pre[src + 1u]) ++src;
     const int4* e = reinterpret_cast<const int4*>(P.rlist + (size_t)src * route_block_bytes(P.route_cap) +
@@ -755,14 +723,14 @@ __device__ __forceinline__ BBox receive_entry(const DrawParams& P, const uint32_
         r[0] = q0;
         r[1] = q1;
         count_owned_box(P, (int)(box.bb0 & 0xFFFFu), (int)(box.bb0 >> 16), (int)(box.bb1 & 0xFFFFu), (int)(box.bb1 >> 16),
-                        s_hist, s_hist2, keep, ranks);
+                        s_hist);
         return box;
     }
     PrimIn in;
     fetch_indices_gid(P, gid, in);
     fetch_positions(P, in);
     PrimGeom g;
-    if (prim_geometry(P, in, g, ndropped) && count_owned(P, g, s_hist, s_hist2, keep, ranks)) return write_record(P, gid, g);
+    if (prim_geometry(P, in, g, ndropped) && count_owned(P, g, s_hist)) return write_record(P, gid, g);
     return BBox{kEmptyBox, 0u};
 }
 
@@ -873,20 +841,16 @@ __device__ __forceinline__ uint32_t own_unit(uint32_t w, uint32_t G, uint32_t i)
 
 template <uint32_t KB, bool MESH>
 __global__ __launch_bounds__(kSetupThreads) void k_setup_bin(DrawParams P) {
-    // LDS: [2 x ntiles (16-B padded) + kSetupMiscWords] words, then bbox_lds BBox and bbox_lds uint2 ranks
-    extern __shared__ __attribute__((aligned(16))) uint32_t s_lds[];
+    extern __shared__ __attribute__((aligned(16))) uint32_t s_lds[];  // [ntiles (16-B padded) + kSetupMiscWords] + bboxes
     const uint32_t nt = P.ntiles, G = gridDim.x, w = blockIdx.x, tid = threadIdx.x;
-    const uint32_t ntp = (nt + 3u) & ~3u;
-    uint32_t* s_hist = s_lds;                       // ranked pairs' histogram -> their cursors
-    uint32_t* s_hist2 = s_hist + ntp;               // unranked pairs' histogram -> their cursors
-    uint32_t* s_misc = s_hist2 + ntp;               // [32]
+    uint32_t* s_hist = s_lds;                       // histogram -> cursors
+    uint32_t* s_misc = s_hist + ((nt + 3u) & ~3u);  // [32]
     uint32_t* s_pre = s_misc + 32;       // records mode: exclusive prefix of the received blocks' counts
-    // this workgroup's primitives' tile bboxes and pair ranks, indexed like phase
-    // 4's flattened (own unit, primitive in unit) space, when they fit (P.bbox_lds)
+    // this workgroup's primitives' tile bboxes, indexed like phase 4's flattened
+    // (own unit, primitive in unit) space, when they fit (P.bbox_lds)
     BBox* s_bbox = reinterpret_cast<BBox*>(s_misc + kSetupMiscWords);
-    uint2* s_rank = reinterpret_cast<uint2*>(s_bbox + P.bbox_lds);
     ZR_STAMP(0);
-    for (uint32_t t = tid; t < 2u * ntp; t += kSetupThreads) s_hist[t] = 0;
+    for (uint32_t t = tid; t < nt; t += kSetupThreads) s_hist[t] = 0;
     if (tid < 32) s_misc[tid] = 0;
     // Partitioned draws (records mode): the received blocks' counts, and whether
     // any block overflowed -- then this workgroup, like every other (they all read
@@ -944,16 +908,10 @@ __global__ __launch_bounds__(kSetupThreads) void k_setup_bin(DrawParams P) {
                 const uint32_t pos = (u << P.unit_shift) + r;
                 if (pos >= n_pos) break;
                 uint32_t gid;
-                const uint32_t l = (jw << P.unit_shift) + r;
-                uint2 rk;
-                const BBox box = receive_entry(P, s_pre, pos, s_hist, s_hist2, P.bbox_lds != 0u, rk, nvalid,
-                                               ndropped, gid);
+                const BBox box = receive_entry(P, s_pre, pos, s_hist, nvalid, ndropped, gid);
                 P.gids[pos] = gid;
                 P.bboxes[pos] = box;
-                if (P.bbox_lds) {
-                    s_bbox[l] = box;
-                    s_rank[l] = rk;
-                }
+                if (P.bbox_lds) s_bbox[(jw << P.unit_shift) + r] = box;
             }
         }
     } else {
@@ -977,17 +935,13 @@ __global__ __launch_bounds__(kSetupThreads) void k_setup_bin(DrawParams P) {
                     const uint32_t prim = pb + b * 64u;
                     if (prim >= n_pos) continue;
                     BBox box;
-                    uint2 rk;
                     if constexpr (MESH)
-                        box = setup_finish_mesh(P, prim, in[b], s_hist2, nvalid, ndropped);
+                        box = setup_finish_mesh(P, prim, in[b], s_hist, nvalid, ndropped);
                     else
-                        box = setup_finish(P, prim, in[b], s_hist, s_hist2, P.bbox_lds != 0u, rk, nvalid, ndropped);
+                        box = setup_finish(P, prim, in[b], s_hist, nvalid, ndropped);
                     // global: the overflow scan of any tile may need it; LDS: phase 4
                     P.bboxes[prim] = box;
-                    if (P.bbox_lds) {
-                        s_bbox[lb + b * 64u] = box;
-                        if (!MESH) s_rank[lb + b * 64u] = rk;
-                    }
+                    if (P.bbox_lds) s_bbox[lb + b * 64u] = box;
                 }
             }
         }
@@ -1008,10 +962,9 @@ __global__ __launch_bounds__(kSetupThreads) void k_setup_bin(DrawParams P) {
         uint32_t top = 0, sum = 0;  // the largest tile count this workgroup saw, its pairs
         for (uint32_t i = tid; i < nt; i += kSetupThreads) {
             const uint32_t t = i + rot < nt ? i + rot : i + rot - nt;
-            const uint32_t c1 = s_hist[t], c = c1 + s_hist2[t];
+            const uint32_t c = s_hist[t];
             const uint32_t o = c ? __hip_atomic_fetch_add(&P.tile_counts[t], c, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) : 0u;
-            s_hist[t] = t * P.slab + o;        // ranked pairs: base + their rank
-            s_hist2[t] = t * P.slab + o + c1;  // unranked pairs: an atomic cursor after them
+            s_hist[t] = t * P.slab + o;
             top = max(top, o + c);
             sum += c;
         }
@@ -1046,15 +999,11 @@ __global__ __launch_bounds__(kSetupThreads) void k_setup_bin(DrawParams P) {
         // per iteration)
         uint32_t* const bins = P.bins;
         const uint32_t slab = P.slab, sG = P.shard_count, srank = P.shard_rank, tiles_x = P.tiles_x;
-        // ranks: the packed ranks phase 1 took for this record's pairs (when `keep`)
-        auto scatter = [&](uint32_t rec, const BBox bb, bool keep, const uint2 ranks) {
+        auto scatter = [&](uint32_t rec, const BBox bb) {
             if (bb.bb0 == kEmptyBox) return;
             const int tx0 = (int)(bb.bb0 & 0xFFFFu) >> kTileShift, tx1 = (int)(bb.bb1 & 0xFFFFu) >> kTileShift;
             const int ty0 = (int)(bb.bb0 >> 16) >> kTileShift, ty1 = (int)(bb.bb1 >> 16) >> kTileShift;
-            // the same test phase 1 made (count_owned_box)
-            const bool ranked = keep && owned_pairs(P, (int)(bb.bb0 >> 16), (int)(bb.bb1 >> 16), tx0, tx1) <= kRankedPairs;
-            const uint32_t rlo = ranks.x, rhi = ranks.y;
-            uint32_t k = 0, orow;
+            uint32_t orow;
             for (int ty = first_owned_row(sG, srank, ty0, orow); ty <= ty1; ty += (int)sG, ++orow) {
                 const uint32_t r = orow * tiles_x;
                 const int cy0 = max((int)(bb.bb0 >> 16), ty << kTileShift);
@@ -1067,9 +1016,7 @@ __global__ __launch_bounds__(kSetupThreads) void k_setup_bin(DrawParams P) {
                     const uint32_t steps = (uint32_t)(((cx1 - cx0 + 2) >> 1) * (cy1 - cy0 + 1));
                     const uint32_t bucket = min((steps - 1u) >> 1, kSortBuckets - 1u);
                     const uint32_t t = r + (uint32_t)tx;
-                    const uint32_t rk = ((k < 2u ? rlo : rhi) >> ((k & 1u) * 16u)) & 0xFFFFu;
-                    ++k;
-                    const uint32_t pos = ranked ? s_hist[t] + rk : atomicAdd(&s_hist2[t], 1u);
+                    const uint32_t pos = atomicAdd(&s_hist[t], 1u);
                     if (pos - t * slab < slab) bins[pos] = rec | (bucket << kBinPrimBits);
                 }
             }
@@ -1080,11 +1027,10 @@ __global__ __launch_bounds__(kSetupThreads) void k_setup_bin(DrawParams P) {
             const uint32_t prim = (own_unit(w, G, j >> P.unit_shift) << P.unit_shift) + (j & (usz - 1u));
             if (prim >= n_pos) continue;
             const BBox bb = P.bbox_lds ? s_bbox[j] : P.bboxes[prim];
-            const uint2 rk = (!MESH && P.bbox_lds) ? s_rank[j] : make_uint2(0u, 0u);
-            scatter(rec_mode && bb.bb0 != kEmptyBox ? P.gids[prim] : prim, bb, !MESH && P.bbox_lds, rk);
+            scatter(rec_mode && bb.bb0 != kEmptyBox ? P.gids[prim] : prim, bb);
             if (MESH) {  // fans 1 and 2 (bboxes stored by this workgroup in phase 1)
-                scatter(mesh_record(P, prim, 1), P.bboxes[mesh_record(P, prim, 1)], false, rk);
-                scatter(mesh_record(P, prim, 2), P.bboxes[mesh_record(P, prim, 2)], false, rk);
+                scatter(mesh_record(P, prim, 1), P.bboxes[mesh_record(P, prim, 1)]);
+                scatter(mesh_record(P, prim, 2), P.bboxes[mesh_record(P, prim, 2)]);
             }
         }
     }
@@ -2165,8 +2111,7 @@ __global__ __launch_bounds__(kTileThreads) void k_clear(DrawParams P) {
 static inline uint32_t blocks_for(uint32_t n, uint32_t per) { return (n + per - 1) / per; }
 
 size_t setup_bin_lds_bytes(uint32_t ntiles, uint32_t bbox_entries) {
-    return (2u * (((size_t)ntiles + 3u) / 4u * 4u) + kSetupMiscWords) * sizeof(uint32_t) +
-           (size_t)bbox_entries * (sizeof(BBox) + sizeof(uint2));
+    return (((size_t)ntiles + 3u) / 4u * 4u + kSetupMiscWords) * sizeof(uint32_t) + (size_t)bbox_entries * sizeof(BBox);
 }
 
 const void* setup_bin_kernel(uint32_t batch, bool mesh) {

@@ -769,14 +769,13 @@ zr_result exec_draw(zr_device* d, ExecState& s, const Cmd& c, bool indexed) {
         while (((positions + (1ull << shift) - 1) >> shift) > 64ull * P.setup_wgs) ++shift;
         P.unit_shift = shift;
         P.units = (uint32_t)std::max<uint64_t>(1, (positions + (1ull << shift) - 1) >> shift);
-        // a workgroup's bboxes live in LDS when they fit beside the two histograms
+        // a workgroup's bboxes live in LDS when they fit beside the histograms
         const uint64_t own_max = ((uint64_t)P.units + P.setup_wgs - 1) / P.setup_wgs;
         const uint64_t entries = own_max << shift;
         const uint64_t hist = setup_bin_lds_bytes(P.ntiles, 0);
         const uint64_t budget = std::min<uint64_t>(kSetupBboxLdsBytes, hist < kSetupLdsBudget ? kSetupLdsBudget - hist : 0);
         // (mesh: fans 1 and 2 keep their bboxes in global memory, so all of them do)
-        // (each with its pairs' ranks: k_setup_bin places them in phase 4 without atomics)
-        P.bbox_lds = (!mesh && entries * (sizeof(BBox) + sizeof(uint2)) <= budget) ? (uint32_t)entries : 0u;
+        P.bbox_lds = (!mesh && entries * sizeof(BBox) <= budget) ? (uint32_t)entries : 0u;
     }
     // k_setup_bin on the setup stream with two scratch sets (zr_device_t::setup_overlap);
     // not while debugging or with graph replay, whose captures bake in set 0
