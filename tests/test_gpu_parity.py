@@ -158,6 +158,40 @@ def test_slab_overflow_one_tile():
         dev.close()
 
 
+@pytest.mark.parametrize("table", [0, 1])
+def test_record_table(monkeypatch, table):
+    """k_tile's 512-thread resolve with its LDS record table forced on or off
+    (ZR_REC_TABLE; the runtime enables it from 256 primitives per tile): exact on
+    every program and depth op, with large primitives among small ones, a tile-row
+    shard, a tile list longer than the table (1024 slots: lookups that miss fall
+    back to the gathered record) and the spill path."""
+    monkeypatch.setenv("ZR_REC_TABLE", str(table))
+    monkeypatch.setenv("ZR_TILE_NT", "512")
+    dev = rhi.RenderDevice(0)
+    try:
+        for prog in (scenes.PROGRAM_TRIANGLE, scenes.PROGRAM_FLAT_COLOR, scenes.PROGRAM_BLINN_PHONG):
+            assert_parity(dev, scenes.soup_scene(80 + prog, 6000, 320, 240, 6.0, prog))
+        assert_parity(dev, scenes.soup_scene(84, 400, 512, 384, 150.0, scenes.PROGRAM_BLINN_PHONG))
+        for op, write in ((scenes.OP_LEQUAL, True), (scenes.OP_GREATER, True), (scenes.OP_LESS, False)):
+            s = scenes.soup_scene(85, 4000, 256, 192, 8.0, scenes.PROGRAM_BLINN_PHONG)
+            s.depth_op, s.depth_write = op, write
+            if op == scenes.OP_GREATER:
+                s.depth_clear = 0.0
+            assert_parity(dev, s)
+        assert_parity(dev, scenes.soup_scene(86, 6000, 320, 240, 6.0, scenes.PROGRAM_BLINN_PHONG), shard=(2, 3))
+        # ~2900 entries per 32x32 tile: three segments, the table full after the first
+        dense = scenes.soup_scene(87, 40000, 96, 96, 5.0, scenes.PROGRAM_BLINN_PHONG)
+        assert_parity(dev, dense)
+    finally:
+        dev.close()
+    monkeypatch.setenv("ZR_BIN_CAPACITY", "1024")  # the spill path (records set up again, not read)
+    dev = rhi.RenderDevice(0)
+    try:
+        assert_parity(dev, scenes.soup_scene(88, 6000, 320, 240, 12.0, scenes.PROGRAM_BLINN_PHONG))
+    finally:
+        dev.close()
+
+
 @pytest.mark.parametrize("nt", [256, 512])
 def test_tile_workgroup_sizes(monkeypatch, nt):
     """k_tile at each workgroup size (4 or 8 waves per tile; the runtime picks by

@@ -3,7 +3,7 @@
 # each under its own time limit).  A pass that fails with an ordinary error (an
 # unknown counter name) is skipped; a pass that times out, aborts or faults ends
 # the script.
-#   gpurun -- 'bash tools/pmc_probe.sh <tag> [bench args...]'
+#   gpurun -- 'bash tools/pmc_probe.sh <tag> [bench args...]'   (PMC_SET=mem: the memory-pipeline set)
 # Output: gpurun_out/pmc_<tag>/<pass>/run_counter_collection.csv, summarised by
 # tools/pmc_table.py into gpurun_out/pmc_<tag>/summary.txt.
 set -o pipefail
@@ -12,6 +12,17 @@ T=${1:?tag}; shift
 O=gpurun_out/pmc_$T
 mkdir -p $O
 timeout -s KILL 60 rocprofv3 -L > $O/counters.txt 2>&1
+if [ "${PMC_SET:-sq}" = mem ]; then
+PASSES=(
+  "TA_BUSY_avr TA_ADDR_STALLED_BY_TC_CYCLES_sum GRBM_GUI_ACTIVE GRBM_COUNT"
+  "TA_DATA_STALLED_BY_TC_CYCLES_sum TA_FLAT_READ_WAVEFRONTS_sum"
+  "TD_BUSY_avr TD_TC_STALL_sum"
+  "TCP_PENDING_STALL_CYCLES_sum TCP_TCR_TCP_STALL_CYCLES_sum TCP_READ_TAGCONFLICT_STALL_CYCLES_sum TCP_TCC_READ_REQ_LATENCY_sum"
+  "TCC_EA0_RDREQ_LEVEL_sum TCC_EA0_RDREQ_sum TCC_HIT_sum TCC_MISS_sum"
+  "TCP_TOTAL_CACHE_ACCESSES_sum TCP_TCC_READ_REQ_sum TCP_TOTAL_READ_sum TCP_UTCL1_TRANSLATION_MISS_sum"
+  "SQ_INSTS_VMEM_RD SQ_INST_CYCLES_VMEM_RD SQ_WAIT_INST_ANY SQ_ACTIVE_INST_VMEM SQ_INSTS_LDS SQ_ACTIVE_INST_LDS SQ_LDS_BANK_CONFLICT SQ_WAVE_CYCLES"
+)
+else
 PASSES=(
   "SQ_WAVES SQ_WAVE_CYCLES SQ_BUSY_CYCLES SQ_WAIT_ANY SQ_WAIT_INST_ANY SQ_ACTIVE_INST_ANY SQ_ACTIVE_INST_VALU SQ_ACTIVE_INST_LDS"
   "SQ_INSTS_VALU SQ_INSTS_SALU SQ_INSTS_LDS SQ_INSTS_VMEM_RD SQ_INSTS_VMEM_WR SQ_LDS_BANK_CONFLICT SQ_WAIT_INST_LDS SQ_ACTIVE_INST_SCA"
@@ -20,6 +31,7 @@ PASSES=(
   "TCP_TCC_READ_REQ_sum TCP_TCC_WRITE_REQ_sum TCP_TOTAL_CACHE_ACCESSES_sum TCP_TCP_TA_DATA_STALL_CYCLES_sum"
   "TA_BUSY_avr TA_TA_BUSY_sum GRBM_GUI_ACTIVE GRBM_COUNT"
 )
+fi
 i=0
 for p in "${PASSES[@]}"; do
   i=$((i+1))

@@ -115,7 +115,11 @@ constexpr uint32_t kMaxShards = 32;  // destination masks are u32
 // Timing-experiment switches (ZR_DEBUG env var); never set in production runs.
 enum : uint32_t { kDebugSkipRaster = 1u, kDebugSkipShade = 2u, kDebugLoadOnly = 16u,
                   kDebugPhase1Only = 32u, kDebugStamps = 128u,
-                  kDebugReverseTiles = 256u, kDebugSkipLanePath = 512u, kDebugSkipWavePath = 1024u };
+                  kDebugReverseTiles = 256u, kDebugSkipLanePath = 512u, kDebugSkipWavePath = 1024u,
+                  // timing only (ZR_TILE_DEBUG builds; wrong images): the resolve without one
+                  // of its gathers -- vertex ids as 3t..3t+2, every attribute from vertex 0,
+                  // every record from record 0 (docs/EXPERIMENTS.md, round 3)
+                  kDebugIdentityVids = 2048u, kDebugSameVids = 4096u, kDebugSameRecord = 8192u };
 
 // Status words in host-mapped pinned memory (read by the runtime at sync points).
 enum StatusWord : uint32_t {
@@ -191,6 +195,7 @@ struct DrawParams {
     // tiling / sharding
     uint32_t tiles_x, tiles_y, shard_rank, shard_count, owned_rows, ntiles;
     uint32_t tile_threads;    // k_tile workgroup size: 256 or 512 (tile_threads_for)
+    uint32_t rec_table;       // k_tile (512 threads): keep the record table for the resolve (use_record_table)
     // partitioned setup (records mode).  In records mode `prims` is
     // max(draw primitives, shard_count * route_cap); the setup pass runs over the
     // dense positions [0, sum of the blocks' counts) of the received entries and
@@ -249,6 +254,17 @@ inline uint32_t tile_threads_for(uint32_t ntiles, uint32_t cus, uint64_t prims, 
     const uint32_t per_cu = ntiles / c;
     if (partitioned) return 2ull * ntiles >= 7ull * c ? (uint32_t)kTileThreads : 512u;
     return (per_cu >= 6u && prims >= 32ull * ntiles && prims < 80ull * ntiles) ? (uint32_t)kTileThreads : 512u;
+}
+
+// Whether k_tile's 512-thread resolve reads its winners' records from the tile's
+// LDS record table (zr_kernels.hip rec_table_insert): for draws of >= 256
+// primitives per screen tile.  There most winners are distinct small primitives
+// and the table saves one gather each (C2, 490 per tile: tile pass 72.4 -> 65.8
+// us); with fewer, larger primitives per tile their pixels' record requests
+// already merge and the inserts and lookups cost more than they save (C3, 122
+// per tile: 174.6 -> 181.8 us).
+inline bool use_record_table(uint64_t prims, uint32_t tiles_x, uint32_t tiles_y) {
+    return prims >= 256ull * tiles_x * tiles_y;
 }
 
 // Launchers (zr_kernels.hip).  All enqueue on `stream`; no host synchronisation.

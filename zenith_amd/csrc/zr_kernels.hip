@@ -38,6 +38,18 @@ namespace zr {
 // code costs k_tile 5 VGPRs, one wave per SIMD at 512 threads).
 #define ZR_TILE_WORK_STATS 0
 #endif
+#ifndef ZR_XCD_TILES
+#define ZR_XCD_TILES 8       // tiles per XCD run (xcd_tile); 0 or 1: blockIdx order
+#endif
+#ifndef ZR_TAB
+#define ZR_TAB 1
+#endif
+#ifndef ZR_TAB_INSERT
+#define ZR_TAB_INSERT 1
+#endif
+#ifndef ZR_TAB_LOOKUP
+#define ZR_TAB_LOOKUP 1
+#endif
 #ifndef ZR_TILE_DEBUG
 #define ZR_TILE_DEBUG 0      // 1: k_tile honours the ZR_DEBUG timing switches and stamps
                              // (the checks cost the production kernel SGPRs)
@@ -1074,6 +1086,20 @@ __device__ __forceinline__ void store_color(const DrawParams& P, int px, int py,
 
 __device__ __forceinline__ int rl(int v, uint32_t lane) { return __builtin_amdgcn_readlane(v, lane); }
 
+// XCD-aware tile order.  Blocks are dealt round-robin over the 8 XCDs, so blocks b
+// and b + 8 share an XCD and its L2 (MI355X_MICROARCH.md; affinity only, nothing
+// depends on it).  Runs of ZR_XCD_TILES consecutive (row-major) tiles go to one
+// XCD, the runs round-robin over the XCDs: a primitive straddling two tiles of a
+// run has its record and vertices read through one L2, and a dense screen region
+// still spreads over every XCD.  A bijection: blocks past the last whole round of
+// runs keep their own tile.
+__device__ __forceinline__ uint32_t xcd_tile(uint32_t b, uint32_t n) {
+    constexpr uint32_t K = ZR_XCD_TILES;
+    if (K <= 1u || b >= n / (8u * K) * (8u * K)) return b;
+    const uint32_t x = b & 7u, l = b >> 3;
+    return ((l / K) * 8u + x) * K + l % K;
+}
+
 // Rasterize one primitive (wave-uniform record) into the tile's LDS keys: lanes
 // sweep the primitive's bbox ∩ tile, packed power-of-two rows per pass.
 // Expands a compact record (two 16-B words, TriCompact) into the TriRecord fields
@@ -1371,6 +1397,48 @@ __device__ __forceinline__ void resolve_vids(const DrawParams& P, uint32_t prim,
     }
 }
 
+// Record table of a 512-thread tile (LDS): the small primitives of its list,
+// hashed by visibility sequence, with the part of the compact record the resolve
+// reads (vertex 0 relative to the tile origin as int16 pairs, the deltas, +-1/A2).
+// The raster inserts each entry as it loads it; the resolve looks its winners up
+// there instead of gathering their records (a lookup that fails -- a full table,
+// a long probe, a large primitive -- gathers the record as before).  Every winner
+// request the pass saves is worth ~20 ns of a C2 tile pass (docs/EXPERIMENTS.md).
+constexpr uint32_t kRecTabSlots = 1024;
+constexpr uint32_t kRecTabProbes = 8;
+__device__ __forceinline__ uint32_t rec_hash(uint32_t seq) { return (seq * 0x9E3779B1u) >> 22; }  // 10 bits
+
+__device__ __forceinline__ void rec_table_insert(uint32_t* s_tseq, int4* s_trec, uint32_t seq, const int4 q0,
+                                                 const int4 q1, int x0, int y0) {
+    uint32_t h = rec_hash(seq);
+    for (uint32_t p = 0; p < kRecTabProbes; ++p) {
+        if (atomicCAS(&s_tseq[h], 0u, seq) == 0u) {
+            const uint32_t rel = ((uint32_t)(q0.x - x0 * 256) & 0xFFFFu) | ((uint32_t)(q0.y - y0 * 256) << 16);
+            s_trec[h] = make_int4((int)rel, q0.z, q0.w, q1.w);
+            return;
+        }
+        h = (h + 1u) & (kRecTabSlots - 1u);
+    }
+}
+
+// The compact record words (q1: only 1/A2) of the primitive with sequence `seq`.
+__device__ __forceinline__ bool rec_table_find(const uint32_t* s_tseq, const int4* s_trec, uint32_t seq, int x0, int y0,
+                                               int4& q0, int4& q1) {
+    uint32_t h = rec_hash(seq);
+    for (uint32_t p = 0; p < kRecTabProbes; ++p) {
+        const uint32_t s = s_tseq[h];
+        if (s == seq) {
+            const int4 e = s_trec[h];
+            q0 = make_int4(x0 * 256 + (int)(int16_t)(e.x & 0xFFFF), y0 * 256 + (e.x >> 16), e.y, e.z);
+            q1 = make_int4(0, 0, 0, e.w);
+            return true;
+        }
+        if (s == 0u) return false;
+        h = (h + 1u) & (kRecTabSlots - 1u);
+    }
+    return false;
+}
+
 // Per-pixel resolve (512-thread tiles: two pixels per thread, one batch): per
 // pixel the winning primitive is read from its key, its compact record and vertex
 // ids are gathered, its edges evaluated once and the program shaded once
@@ -1381,9 +1449,9 @@ __device__ __forceinline__ void resolve_vids(const DrawParams& P, uint32_t prim,
 // thread in two batches; C1 49 vs 44 us, C3 223 vs 204 us).  A wave with no
 // winner skips the gathers; other pixels without a winner load the wave's first
 // winner (in-bounds addresses) and discard it.
-template <int PROG, int MODE, bool IDX32, int NT>
+template <int PROG, int MODE, bool IDX32, int NT, bool TAB>
 __device__ __forceinline__ void resolve_pixels(const DrawParams& P, int x0, int y0, const unsigned long long* s_key,
-                                               const float* s_srgb) {
+                                               const float* s_srgb, const uint32_t* s_tseq, const int4* s_trec) {
     constexpr int kPer = kTilePixels / NT;
     constexpr int kB = kPer < (int)kResolveBatch ? kPer : (int)kResolveBatch;
     // recomputed here, not reused from the tile's init: a pixel coordinate kept
@@ -1430,11 +1498,28 @@ __device__ __forceinline__ void resolve_pixels(const DrawParams& P, int x0, int 
         float zw[kB];
         if (anyw) {
 #pragma unroll
-            for (int b = 0; b < kB; ++b) {  // gathers of the batch
-                const int4* cp = reinterpret_cast<const int4*>(P.records + prim[b]);
-                c0[b] = cp[0];
-                c1[b] = cp[1];
-                resolve_vids<IDX32>(P, gp[b], vid[b]);
+            for (int b = 0; b < kB; ++b) {  // the index gathers first: the table lookups run under them
+                if (tile_debug(P) & kDebugIdentityVids) {
+                    const uint32_t v = P.first + tri_of(P, gp[b]) * 3u + (uint32_t)P.vertex_offset;
+                    vid[b][0] = v; vid[b][1] = v + 1u; vid[b][2] = v + 2u;
+                } else {
+                    resolve_vids<IDX32>(P, gp[b], vid[b]);
+                }
+                if (tile_debug(P) & kDebugSameVids) vid[b][0] = vid[b][1] = vid[b][2] = 0u;
+            }
+#pragma unroll
+            for (int b = 0; b < kB; ++b) {
+                // the record: from the tile's record table, else gathered (mesh
+                // programs read it only for a last-wins depth)
+                bool tab = false;
+                if (TAB && ZR_TAB_LOOKUP && P.rec_table) tab = rec_table_find(s_tseq, s_trec, prim[b] + 1u, x0, y0, c0[b], c1[b]);
+                if (!tab && (PROG != kProgMesh || MODE == kDepthLastWins)) {
+                    const int4* cp = reinterpret_cast<const int4*>(P.records + ((tile_debug(P) & kDebugSameRecord) ? 0u : prim[b]));
+                    c0[b] = cp[0];
+                    c1[b] = cp[1];
+                } else if (!tab) {
+                    c0[b] = c1[b] = make_int4(0, 0, 1, 1);
+                }
             }
 #pragma unroll
             for (int b = 0; b < kB; ++b) {
@@ -1787,7 +1872,9 @@ __global__ __launch_bounds__(NT, kTileWgs * kTileThreads / 256) void k_tile(Draw
     constexpr uint32_t kBudget = 160u * 1024u / kWgsPerCu;
     constexpr uint32_t kMiscWords = 16;
     constexpr uint32_t kUnionWords = (kBudget - kTilePixels * 8u - 256u * 4u - kMiscWords * 4u) / 4u;
-    static_assert(kSortCap + kBigQueue + kSortBuckets + (INITD ? kTilePixels : 0u) <= kUnionWords,
+    static_assert(kSortCap + kBigQueue + kSortBuckets + (INITD ? kTilePixels : 0u) +
+                          ((NT >= 512 && MODE != kDepthLastWins && PROG != kProgMesh) ? 5u * kRecTabSlots : 0u) <=
+                      kUnionWords,
                   "k_tile raster scratch exceeds the workgroup's LDS share");
     __shared__ unsigned long long s_key[kTilePixels];
     __shared__ float s_srgb[256];
@@ -1800,12 +1887,18 @@ __global__ __launch_bounds__(NT, kTileWgs * kTileThreads / 256) void k_tile(Draw
     uint32_t* s_big = s_u + kSortCap;               // [kBigQueue]
     uint32_t* s_bucket = s_big + kBigQueue;         // [kSortBuckets]
     float* s_initd = reinterpret_cast<float*>(s_bucket + kSortBuckets);  // [kTilePixels] (INITD)
+    // 512-thread tiles: the record table of the resolve (rec_table_insert); last-wins
+    // modes need the records' depth terms, which it does not hold
+    constexpr bool kTab = ZR_TAB && NT >= 512 && MODE != kDepthLastWins && PROG != kProgMesh;
+    int4* s_trec = reinterpret_cast<int4*>(s_bucket + kSortBuckets + (INITD ? kTilePixels : 0u));  // [kRecTabSlots]
+    uint32_t* s_tseq = reinterpret_cast<uint32_t*>(s_trec + kRecTabSlots);                        // [kRecTabSlots]
     uint32_t& s_claim = s_misc[0];   // next 64-entry chunk of the segment to rasterize
     uint32_t& s_nbig = s_misc[1];
     uint32_t& s_bclaim = s_misc[2];
     uint32_t* s_dbg = s_misc + 3;    // [2] kDebugStamps: lane-walk steps of the chunks, wave-path sweeps
     uint32_t* s_nwin = s_misc + 5;   // resolve: distinct winners of the tile
-    const uint32_t t = (tile_debug(P) & kDebugReverseTiles) ? P.ntiles - 1u - blockIdx.x : blockIdx.x;
+    const uint32_t b = (tile_debug(P) & kDebugReverseTiles) ? P.ntiles - 1u - blockIdx.x : blockIdx.x;
+    const uint32_t t = xcd_tile(b, P.ntiles);
     const uint32_t oy = t / P.tiles_x, tx = t - oy * P.tiles_x;
     const uint32_t ty = oy * P.shard_count + P.shard_rank;
     const int x0 = (int)tx * kTile, y0 = (int)ty * kTile;
@@ -1849,6 +1942,9 @@ __global__ __launch_bounds__(NT, kTileWgs * kTileThreads / 256) void k_tile(Draw
         if (INITD) s_initd[i] = d;
     }
     if (threadIdx.x < 255) s_srgb[threadIdx.x] = c_srgbT[threadIdx.x];
+    const bool tab = kTab && P.rec_table != 0u;  // (runtime: draws dense enough to gain from it)
+    if (tab)
+        for (uint32_t i = threadIdx.x; i < kRecTabSlots; i += NT) s_tseq[i] = 0u;
     if (threadIdx.x < 2) s_dbg[threadIdx.x] = 0u;
     // tile 0 reports the draw's setup and binning stats (k_setup_bin's counters,
     // complete before this launch) and flags a slab overflow to the runtime
@@ -1974,6 +2070,7 @@ __global__ __launch_bounds__(NT, kTileWgs * kTileThreads / 256) void k_tile(Draw
                 const bool valid = j < n && !(tile_debug(P) & kDebugLoadOnly);
                 if (tile_debug(P) & kDebugLoadOnly) asm volatile("" ::"v"(q0.x), "v"(q1.x), "v"(my_prim));
                 const bool large = compact_is_large(q0);
+                if (ZR_TAB_INSERT && tab && valid && !large && sub == 0) rec_table_insert(s_tseq, s_trec, entry_seq<PROG>(P, my_prim), q0, q1, x0, y0);
                 if (valid && !large && !(tile_debug(P) & kDebugSkipLanePath)) {
                     const TriRecord r = decode_compact(P, q0, q1, true);
                     raster_lane<MODE, INITD>(P, r, entry_seq<PROG>(P, my_prim), x0, y0, s_key, s_initd, sub, (int)ksh);
@@ -2076,9 +2173,9 @@ __global__ __launch_bounds__(NT, kTileWgs * kTileThreads / 256) void k_tile(Draw
     // index loads are issued back to back).
     if (NT >= 512) {
         if (P.index_size == 4)
-            resolve_pixels<PROG, MODE, true, NT>(kernarg_params(), x0, y0, s_key, s_srgb);
+            resolve_pixels<PROG, MODE, true, NT, kTab>(kernarg_params(), x0, y0, s_key, s_srgb, s_tseq, s_trec);
         else
-            resolve_pixels<PROG, MODE, false, NT>(kernarg_params(), x0, y0, s_key, s_srgb);
+            resolve_pixels<PROG, MODE, false, NT, kTab>(kernarg_params(), x0, y0, s_key, s_srgb, s_tseq, s_trec);
     } else if (P.index_size == 4) {
         resolve_tile<PROG, MODE, true, NT>(kernarg_params(), x0, y0, s_key, s_u, kUnionWords, s_nwin, s_srgb,
                                           stamp ? ts : nullptr);

@@ -235,6 +235,7 @@ struct zr_device_t {
     // tile pass leaves most CUs idle: C2 G=2/4/8 +2.8/+2.3/+0.7 %, C3 G=8 +7 %).
     // ZR_SETUP_OVERLAP=0 / 1 forces it off / on.
     int setup_overlap = -1;
+    int rec_table = -1;        // ZR_REC_TABLE=0/1 forces k_tile's record table (A/B); -1: use_record_table
     int cu_count = 0;
     uint32_t occupancy_checked_tiles = 0;
     bool occupancy_checked_mesh = false;
@@ -783,6 +784,7 @@ zr_result exec_draw(zr_device* d, ExecState& s, const Cmd& c, bool indexed) {
                        !d->use_graphs && !d->debug;
     P.tile_threads = d->tile_threads ? d->tile_threads
                                      : tile_threads_for(P.ntiles, (uint32_t)std::max(d->cu_count, 1), prims, partitioned);
+    P.rec_table = (d->rec_table < 0 ? use_record_table(prims, P.tiles_x, P.tiles_y) : d->rec_table != 0) ? 1u : 0u;
     P.debug = d->debug;
     if (d->debug & kDebugStamps) {
         if (!d->dbg_ts) ZR_HIP(hipMalloc((void**)&d->dbg_ts, (8192 + kMaxTilesPerPass) * 8 * sizeof(unsigned long long)));
@@ -998,6 +1000,7 @@ ZR_API zr_result zr_device_create(int32_t hip_device, zr_device** out) {
     if (const char* cap = getenv("ZR_BIN_CAPACITY")) d->initial_bins = std::max<uint64_t>(64, strtoull(cap, nullptr, 0));
     if (const char* g = getenv("ZR_GRAPH")) d->use_graphs = strtoul(g, nullptr, 0) != 0;
     if (const char* o = getenv("ZR_SETUP_OVERLAP")) d->setup_overlap = strtoul(o, nullptr, 0) != 0 ? 1 : 0;
+    if (const char* rt = getenv("ZR_REC_TABLE")) d->rec_table = strtoul(rt, nullptr, 0) != 0 ? 1 : 0;
     if (const char* nt = getenv("ZR_TILE_NT")) {
         const unsigned long v = strtoul(nt, nullptr, 0);
         d->tile_threads = v >= 512 ? 512u : v ? 256u : 0u;
