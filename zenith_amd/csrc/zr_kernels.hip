@@ -44,12 +44,6 @@ namespace zr {
 #ifndef ZR_TAB
 #define ZR_TAB 1
 #endif
-#ifndef ZR_TAB_INSERT
-#define ZR_TAB_INSERT 1
-#endif
-#ifndef ZR_TAB_LOOKUP
-#define ZR_TAB_LOOKUP 1
-#endif
 #ifndef ZR_TILE_DEBUG
 #define ZR_TILE_DEBUG 0      // 1: k_tile honours the ZR_DEBUG timing switches and stamps
                              // (the checks cost the production kernel SGPRs)
@@ -1397,44 +1391,45 @@ __device__ __forceinline__ void resolve_vids(const DrawParams& P, uint32_t prim,
     }
 }
 
-// Record table of a 512-thread tile (LDS): the small primitives of its list,
-// hashed by visibility sequence, with the part of the compact record the resolve
-// reads (vertex 0 relative to the tile origin as int16 pairs, the deltas, +-1/A2).
+// Record table of a 512-thread tile (LDS): the small primitives of its current
+// segment, with the part of the compact record the resolve reads (vertex 0
+// relative to the tile origin as int16 pairs, the deltas, +-1/A2), stored at the
+// entry's sorted position j (no collisions), and a 2048-slot hash from the setup
+// record to j + 1 (load factor <= 1/2: short probes).  A lookup is valid when the
+// sorted array still holds that record at j (a later segment reuses positions).
 // The raster inserts each entry as it loads it; the resolve looks its winners up
-// there instead of gathering their records (a lookup that fails -- a full table,
-// a long probe, a large primitive -- gathers the record as before).  Every winner
-// request the pass saves is worth ~20 ns of a C2 tile pass (docs/EXPERIMENTS.md).
-constexpr uint32_t kRecTabSlots = 1024;
+// and gathers the record only when that fails (a table overwritten by a later
+// segment, a long probe, a large primitive).  Every winner request the pass saves
+// is worth ~20 ns of a C2 tile pass (docs/EXPERIMENTS.md).
+constexpr uint32_t kRecHashSlots = 2048;
 constexpr uint32_t kRecTabProbes = 8;
-__device__ __forceinline__ uint32_t rec_hash(uint32_t seq) { return (seq * 0x9E3779B1u) >> 22; }  // 10 bits
+__device__ __forceinline__ uint32_t rec_hash(uint32_t rec) { return (rec * 0x9E3779B1u) >> 21; }  // 11 bits
 
-__device__ __forceinline__ void rec_table_insert(uint32_t* s_tseq, int4* s_trec, uint32_t seq, const int4 q0,
-                                                 const int4 q1, int x0, int y0) {
-    uint32_t h = rec_hash(seq);
+__device__ __forceinline__ void rec_table_insert(uint32_t* s_thash, int4* s_trec, uint32_t rec, uint32_t j,
+                                                 const int4 q0, const int4 q1, int x0, int y0) {
+    const uint32_t rel = ((uint32_t)(q0.x - x0 * 256) & 0xFFFFu) | ((uint32_t)(q0.y - y0 * 256) << 16);
+    s_trec[j] = make_int4((int)rel, q0.z, q0.w, q1.w);
+    uint32_t h = rec_hash(rec);
     for (uint32_t p = 0; p < kRecTabProbes; ++p) {
-        if (atomicCAS(&s_tseq[h], 0u, seq) == 0u) {
-            const uint32_t rel = ((uint32_t)(q0.x - x0 * 256) & 0xFFFFu) | ((uint32_t)(q0.y - y0 * 256) << 16);
-            s_trec[h] = make_int4((int)rel, q0.z, q0.w, q1.w);
-            return;
-        }
-        h = (h + 1u) & (kRecTabSlots - 1u);
+        if (atomicCAS(&s_thash[h], 0u, j + 1u) == 0u) return;
+        h = (h + 1u) & (kRecHashSlots - 1u);
     }
 }
 
-// The compact record words (q1: only 1/A2) of the primitive with sequence `seq`.
-__device__ __forceinline__ bool rec_table_find(const uint32_t* s_tseq, const int4* s_trec, uint32_t seq, int x0, int y0,
-                                               int4& q0, int4& q1) {
-    uint32_t h = rec_hash(seq);
+// The compact record words (q1: only 1/A2) of setup record `rec`.
+__device__ __forceinline__ bool rec_table_find(const uint32_t* s_thash, const int4* s_trec, const uint32_t* s_sorted,
+                                               uint32_t rec, int x0, int y0, int4& q0, int4& q1) {
+    uint32_t h = rec_hash(rec);
     for (uint32_t p = 0; p < kRecTabProbes; ++p) {
-        const uint32_t s = s_tseq[h];
-        if (s == seq) {
-            const int4 e = s_trec[h];
+        const uint32_t v = s_thash[h];
+        if (v == 0u) return false;
+        if (s_sorted[v - 1u] == rec) {
+            const int4 e = s_trec[v - 1u];
             q0 = make_int4(x0 * 256 + (int)(int16_t)(e.x & 0xFFFF), y0 * 256 + (e.x >> 16), e.y, e.z);
             q1 = make_int4(0, 0, 0, e.w);
             return true;
         }
-        if (s == 0u) return false;
-        h = (h + 1u) & (kRecTabSlots - 1u);
+        h = (h + 1u) & (kRecHashSlots - 1u);
     }
     return false;
 }
@@ -1451,7 +1446,8 @@ __device__ __forceinline__ bool rec_table_find(const uint32_t* s_tseq, const int
 // winner (in-bounds addresses) and discard it.
 template <int PROG, int MODE, bool IDX32, int NT, bool TAB>
 __device__ __forceinline__ void resolve_pixels(const DrawParams& P, int x0, int y0, const unsigned long long* s_key,
-                                               const float* s_srgb, const uint32_t* s_tseq, const int4* s_trec) {
+                                               const float* s_srgb, const uint32_t* s_thash, const int4* s_trec,
+                                               const uint32_t* s_sorted) {
     constexpr int kPer = kTilePixels / NT;
     constexpr int kB = kPer < (int)kResolveBatch ? kPer : (int)kResolveBatch;
     // recomputed here, not reused from the tile's init: a pixel coordinate kept
@@ -1512,7 +1508,7 @@ __device__ __forceinline__ void resolve_pixels(const DrawParams& P, int x0, int 
                 // the record: from the tile's record table, else gathered (mesh
                 // programs read it only for a last-wins depth)
                 bool tab = false;
-                if (TAB && ZR_TAB_LOOKUP && P.rec_table) tab = rec_table_find(s_tseq, s_trec, prim[b] + 1u, x0, y0, c0[b], c1[b]);
+                if (TAB && P.rec_table) tab = rec_table_find(s_thash, s_trec, s_sorted, prim[b], x0, y0, c0[b], c1[b]);
                 if (!tab && (PROG != kProgMesh || MODE == kDepthLastWins)) {
                     const int4* cp = reinterpret_cast<const int4*>(P.records + ((tile_debug(P) & kDebugSameRecord) ? 0u : prim[b]));
                     c0[b] = cp[0];
@@ -1873,7 +1869,9 @@ __global__ __launch_bounds__(NT, kTileWgs * kTileThreads / 256) void k_tile(Draw
     constexpr uint32_t kMiscWords = 16;
     constexpr uint32_t kUnionWords = (kBudget - kTilePixels * 8u - 256u * 4u - kMiscWords * 4u) / 4u;
     static_assert(kSortCap + kBigQueue + kSortBuckets + (INITD ? kTilePixels : 0u) +
-                          ((NT >= 512 && MODE != kDepthLastWins && PROG != kProgMesh) ? 5u * kRecTabSlots : 0u) <=
+                          ((NT >= 512 && MODE != kDepthLastWins && PROG != kProgMesh && !INITD)
+                               ? 4u * kSortCap + kRecHashSlots
+                               : 0u) <=
                       kUnionWords,
                   "k_tile raster scratch exceeds the workgroup's LDS share");
     __shared__ unsigned long long s_key[kTilePixels];
@@ -1889,9 +1887,9 @@ __global__ __launch_bounds__(NT, kTileWgs * kTileThreads / 256) void k_tile(Draw
     float* s_initd = reinterpret_cast<float*>(s_bucket + kSortBuckets);  // [kTilePixels] (INITD)
     // 512-thread tiles: the record table of the resolve (rec_table_insert); last-wins
     // modes need the records' depth terms, which it does not hold
-    constexpr bool kTab = ZR_TAB && NT >= 512 && MODE != kDepthLastWins && PROG != kProgMesh;
-    int4* s_trec = reinterpret_cast<int4*>(s_bucket + kSortBuckets + (INITD ? kTilePixels : 0u));  // [kRecTabSlots]
-    uint32_t* s_tseq = reinterpret_cast<uint32_t*>(s_trec + kRecTabSlots);                        // [kRecTabSlots]
+    constexpr bool kTab = ZR_TAB && NT >= 512 && MODE != kDepthLastWins && PROG != kProgMesh && !INITD;
+    int4* s_trec = reinterpret_cast<int4*>(s_bucket + kSortBuckets);        // [kSortCap]
+    uint32_t* s_thash = reinterpret_cast<uint32_t*>(s_trec + kSortCap);      // [kRecHashSlots]
     uint32_t& s_claim = s_misc[0];   // next 64-entry chunk of the segment to rasterize
     uint32_t& s_nbig = s_misc[1];
     uint32_t& s_bclaim = s_misc[2];
@@ -1944,7 +1942,7 @@ __global__ __launch_bounds__(NT, kTileWgs * kTileThreads / 256) void k_tile(Draw
     if (threadIdx.x < 255) s_srgb[threadIdx.x] = c_srgbT[threadIdx.x];
     const bool tab = kTab && P.rec_table != 0u;  // (runtime: draws dense enough to gain from it)
     if (tab)
-        for (uint32_t i = threadIdx.x; i < kRecTabSlots; i += NT) s_tseq[i] = 0u;
+        for (uint32_t i = threadIdx.x; i < kRecHashSlots; i += NT) s_thash[i] = 0u;
     if (threadIdx.x < 2) s_dbg[threadIdx.x] = 0u;
     // tile 0 reports the draw's setup and binning stats (k_setup_bin's counters,
     // complete before this launch) and flags a slab overflow to the runtime
@@ -2070,7 +2068,7 @@ __global__ __launch_bounds__(NT, kTileWgs * kTileThreads / 256) void k_tile(Draw
                 const bool valid = j < n && !(tile_debug(P) & kDebugLoadOnly);
                 if (tile_debug(P) & kDebugLoadOnly) asm volatile("" ::"v"(q0.x), "v"(q1.x), "v"(my_prim));
                 const bool large = compact_is_large(q0);
-                if (ZR_TAB_INSERT && tab && valid && !large && sub == 0) rec_table_insert(s_tseq, s_trec, entry_seq<PROG>(P, my_prim), q0, q1, x0, y0);
+                if (tab && valid && !large && sub == 0) rec_table_insert(s_thash, s_trec, my_prim, j, q0, q1, x0, y0);
                 if (valid && !large && !(tile_debug(P) & kDebugSkipLanePath)) {
                     const TriRecord r = decode_compact(P, q0, q1, true);
                     raster_lane<MODE, INITD>(P, r, entry_seq<PROG>(P, my_prim), x0, y0, s_key, s_initd, sub, (int)ksh);
@@ -2173,9 +2171,9 @@ __global__ __launch_bounds__(NT, kTileWgs * kTileThreads / 256) void k_tile(Draw
     // index loads are issued back to back).
     if (NT >= 512) {
         if (P.index_size == 4)
-            resolve_pixels<PROG, MODE, true, NT, kTab>(kernarg_params(), x0, y0, s_key, s_srgb, s_tseq, s_trec);
+            resolve_pixels<PROG, MODE, true, NT, kTab>(kernarg_params(), x0, y0, s_key, s_srgb, s_thash, s_trec, s_sorted);
         else
-            resolve_pixels<PROG, MODE, false, NT, kTab>(kernarg_params(), x0, y0, s_key, s_srgb, s_tseq, s_trec);
+            resolve_pixels<PROG, MODE, false, NT, kTab>(kernarg_params(), x0, y0, s_key, s_srgb, s_thash, s_trec, s_sorted);
     } else if (P.index_size == 4) {
         resolve_tile<PROG, MODE, true, NT>(kernarg_params(), x0, y0, s_key, s_u, kUnionWords, s_nwin, s_srgb,
                                           stamp ? ts : nullptr);
