@@ -58,7 +58,7 @@ def parse():
                         "enqueued from C++), or torch.distributed's (Python callbacks)")
     p.add_argument("--force-dist", action="store_true",
                    help="run the multi-GPU code path (RCCL process group, exchange, gather) even at 1 GPU")
-    p.add_argument("--pmc", default=os.path.join(ROOT, "profiles", "r03_pmc_c2.json"),
+    p.add_argument("--pmc", default=os.path.join(ROOT, "profiles", "r03_v3_pmc_c2.json"),
                    help="rocprofv3 PMC summary for roofline.traffic (tools/pmc_summary.py)")
     return p.parse_args()
 
