@@ -10,6 +10,11 @@ max-over-ranks wall time.
 
   python bench.py [--gpus N] [--steps K] [--warmup W] [--config c2]
   torchrun --nproc-per-node N bench.py --gpus N ...      (N > 1, RCCL gather)
+
+Without a launcher (WORLD_SIZE unset) and N > 1 (or --force-dist), this process
+touches no GPU: it starts N worker processes of itself (one per GPU, ranks and a
+127.0.0.1 rendezvous in their environment), relays rank 0's JSON line and exits
+non-zero when any worker fails (launch_workers).
 """
 import argparse
 import json
@@ -58,6 +63,8 @@ def parse():
                         "enqueued from C++), or torch.distributed's (Python callbacks)")
     p.add_argument("--force-dist", action="store_true",
                    help="run the multi-GPU code path (RCCL process group, exchange, gather) even at 1 GPU")
+    p.add_argument("--worker-timeout", type=float, default=0.0,
+                   help="launcher-less N>1 run: stop the workers after this many seconds (0: no limit)")
     p.add_argument("--pmc", default=os.path.join(ROOT, "profiles", "r03_v3_pmc_c2.json"),
                    help="rocprofv3 PMC summary for roofline.traffic (tools/pmc_summary.py)")
     return p.parse_args()
@@ -267,8 +274,90 @@ def emulate(a, scene, cuda):
     return out
 
 
+# ------------------------------------------------------------ worker launcher
+def worker_commands(n, argv, port, base_env=None, script=None):
+    """The N worker processes of a launcher-less multi-GPU run: this script with
+    the same arguments, one rank per GPU (LOCAL_RANK = RANK = device index) and
+    the rendezvous in the environment, as torch.distributed.run would set it."""
+    base = dict(os.environ if base_env is None else base_env)
+    cmds = []
+    for r in range(n):
+        env = dict(base, RANK=str(r), LOCAL_RANK=str(r), WORLD_SIZE=str(n), LOCAL_WORLD_SIZE=str(n),
+                   GROUP_RANK="0", MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+        cmds.append(([sys.executable, "-u", script or os.path.abspath(__file__)] + list(argv), env))
+    return cmds
+
+
+def free_port():
+    import socket
+    with socket.socket(socket.AF_INET, socket.SOCK_STREAM) as sk:
+        sk.bind(("127.0.0.1", 0))
+        return sk.getsockname()[1]
+
+
+def run_workers(cmds, out=None, timeout=None, poll=0.2):
+    """Starts every (cmd, env) as a child process (never exec: the parent may not
+    replace itself), rank 0's stdout into a file that is relayed to ``out`` when
+    all are done, the others' stdout onto stderr.  When a worker fails (non-zero
+    exit) or ``timeout`` seconds pass, the rest are stopped -- their own process
+    groups, SIGTERM then SIGKILL -- since they may sit in a collective waiting for
+    the failed one.  Returns 0 or the first failure's exit status (124 on timeout)."""
+    import signal
+    import subprocess
+    import tempfile
+    out = out or sys.stdout
+    procs = []
+    with tempfile.TemporaryFile("w+") as rank0_out:
+        for i, (cmd, env) in enumerate(cmds):
+            procs.append(subprocess.Popen(cmd, env=env, cwd=ROOT, stdout=rank0_out if i == 0 else sys.stderr,
+                                          start_new_session=True))
+        t0 = time.monotonic()
+        rc = 0
+        while True:
+            codes = [p.poll() for p in procs]
+            bad = [c for c in codes if c not in (None, 0)]
+            if bad:
+                rc = bad[0] if bad[0] > 0 else 128 - bad[0]  # -N: killed by signal N
+                break
+            if all(c == 0 for c in codes):
+                break
+            if timeout is not None and time.monotonic() - t0 > timeout:
+                rc = 124
+                break
+            time.sleep(poll)
+        if rc:
+            for sig, grace in ((signal.SIGTERM, 10.0), (signal.SIGKILL, 5.0)):
+                for p in procs:
+                    if p.poll() is None:
+                        try:
+                            os.killpg(p.pid, sig)
+                        except ProcessLookupError:
+                            pass
+                t1 = time.monotonic()
+                while any(p.poll() is None for p in procs) and time.monotonic() - t1 < grace:
+                    time.sleep(0.1)
+            for p in procs:
+                if p.poll() is None:
+                    p.wait()
+            print(f"bench: worker exit codes {[p.returncode for p in procs]}", file=sys.stderr)
+        rank0_out.seek(0)
+        text = rank0_out.read()
+    if text:
+        out.write(text)
+        out.flush()
+    return rc
+
+
+def launch_workers(a, argv):
+    cmds = worker_commands(a.gpus, argv, free_port())
+    return run_workers(cmds, timeout=a.worker_timeout or None)
+
+
 def main():
     a = parse()
+    if "WORLD_SIZE" not in os.environ and (a.gpus > 1 or a.force_dist):
+        # no launcher: this process stays off the GPU and runs one worker per GPU
+        raise SystemExit(launch_workers(a, sys.argv[1:]))
     # The JSON line is the only thing on stdout: libraries that print to fd 1
     # (RCCL's version banner) are sent to stderr.
     json_out = os.fdopen(os.dup(1), "w")
@@ -283,9 +372,6 @@ def main():
     cuda = torch.device("cuda", local)
     distributed = world > 1 or a.force_dist
     if distributed:
-        if "MASTER_ADDR" not in os.environ:  # --force-dist without a launcher
-            os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=os.environ.get("MASTER_PORT", "29533"),
-                              RANK="0", WORLD_SIZE="1")
         dist.init_process_group("nccl", device_id=cuda)
 
     scene = scenes.config_scene(a.config)

@@ -125,9 +125,11 @@ ZR_API int32_t zr_device_kernel_times(zr_device *dev, zr_kernel_time *out, int32
 typedef struct zr_draw_stats {
     uint64_t triangles_in, triangles_setup, triangles_dropped_clip;
     uint64_t bin_pairs, bin_capacity, overflowed_draws;
-    /* partitioned tile shards (zr_cmd_set_tile_shard_exchange): the largest number
-     * of entries this rank routed to one destination in the draws since the
-     * previous sync point, and the draws (so far) whose received blocks overflowed
+    /* partitioned tile shards (zr_cmd_set_tile_shard_exchange): the largest block
+     * total this rank RECEIVED (the entries one source rank routed to this rank,
+     * counted before the block capacity cuts them) in the draws since the previous
+     * sync point -- size zr_cmd_set_route_capacity from the maximum over ranks --
+     * and the draws (so far) whose received blocks overflowed
      * zr_cmd_set_route_capacity and were set up in full instead */
     uint64_t route_max_entries, route_fallback_draws;
 } zr_draw_stats;
@@ -198,12 +200,18 @@ typedef struct zr_vertex_input_attr {
 /* Shader::from_file (shader.rs:38-64): maps (file, entry, stage) onto a built-in
  * HIP stage variant and returns its reflection (ShaderReflection, shader.rs:211-270).
  * Known files (matched on basename): triangle.slang (reference),
- * flat_color.slang and blinn_phong.slang (this repo, content/shaders/). */
+ * flat_color.slang, blinn_phong.slang, mesh.slang (camera matrix in the View
+ * uniform) and mesh_push.slang (the same program, matrix in push constants)
+ * (this repo, content/shaders/). */
 ZR_API zr_result zr_shader_lookup(zr_device *dev, const char *path, const char *entry, uint32_t stage,
                                   zr_shader **out);
 ZR_API void zr_shader_destroy(zr_shader *sh);
 ZR_API int32_t zr_shader_bindings(const zr_shader *sh, zr_shader_binding *out, int32_t capacity);
 ZR_API int32_t zr_shader_vertex_inputs(const zr_shader *sh, zr_vertex_input_attr *out, int32_t capacity);
+/* ShaderReflection::push_constant_size (shader.rs:214; reflected from the SPIR-V
+ * push-constant block at shader.rs:408-413): bytes of the stage's push-constant
+ * block, 0 when it has none.  mesh_push.slang's vsmain: 64 (View.view_proj). */
+ZR_API uint32_t zr_shader_push_constant_size(const zr_shader *sh);
 
 /* ---------------------------------------------------------------- pipelines */
 
@@ -241,6 +249,13 @@ typedef struct zr_rasterization_state {
     float depth_bias_constant, depth_bias_slope, line_width;
 } zr_rasterization_state;
 
+/* vk::PushConstantRange of a pipeline layout (pipeline.rs:112-128). */
+typedef struct zr_push_constant_range {
+    uint32_t stage_flags; /* VkShaderStageFlags; ALL_GRAPHICS = 0x1F */
+    uint32_t offset, size;
+} zr_push_constant_range;
+enum { ZR_SHADER_STAGE_ALL_GRAPHICS = 0x1F, ZR_MAX_PUSH_CONSTANTS_SIZE = 128 };
+
 /* GraphicPipelineDesc = GraphicShaderInput + GraphicPipelineState +
  * GraphicPipelineAttachments (pipeline.rs:18-132, 714-737, 877-920). */
 typedef struct zr_graphic_pipeline_desc {
@@ -259,6 +274,17 @@ typedef struct zr_graphic_pipeline_desc {
     const zr_color_attachment_desc *color_attachments;
     const int32_t *color_formats;     /* color_attachment_count VkFormats         */
     int32_t depth_format;             /* 0 = none                                 */
+    /* The layout's push-constant ranges.  0 ranges: derived as
+     * GraphicShaderInput::create_pipeline_layout does (pipeline.rs:112-128) --
+     * one {ALL_GRAPHICS, 0, merged push_constant_size} range when the merged
+     * reflection's size (ShaderReflection::merge, shader.rs:224-228: the max over
+     * the stages) is > 0, none otherwise.  Given ranges are validated as
+     * vkCreatePipelineLayout + vkCreateGraphicsPipelines would: offset and size
+     * multiples of 4, size > 0, offset + size <= ZR_MAX_PUSH_CONSTANTS_SIZE, a
+     * stage in at most one range, and every stage's push-constant block covered by
+     * a range holding that stage (else ZR_ERROR_VALIDATION_FAILED). */
+    uint32_t push_constant_range_count;
+    const zr_push_constant_range *push_constant_ranges;
 } zr_graphic_pipeline_desc;
 
 /* Details of a pipeline validation failure (validate_vertex_inputs,
@@ -274,6 +300,10 @@ typedef struct zr_pipeline_error {
 ZR_API zr_result zr_pipeline_create(zr_device *dev, const zr_graphic_pipeline_desc *desc, zr_pipeline **out,
                                     zr_pipeline_error *err);
 ZR_API void zr_pipeline_destroy(zr_pipeline *p);
+/* The pipeline layout's push-constant ranges (derived or given, see the desc);
+ * returns their number, writes at most `capacity`. */
+ZR_API int32_t zr_pipeline_push_constant_ranges(const zr_pipeline *p, zr_push_constant_range *out,
+                                                int32_t capacity);
 
 /* ------------------------------------------------------------ command buffers */
 
@@ -295,7 +325,9 @@ typedef struct zr_rendering_info {
     const zr_rendering_attachment *depth_attachment; /* nullable */
 } zr_rendering_info;
 
-/* CommandPool::allocate + CommandEncoder::new/begin (command.rs:44-62, 99-113). */
+/* CommandPool::allocate + CommandEncoder::new/begin (command.rs:44-62, 99-113).
+ * dev may be NULL: the list records and validates on the host but zr_submit
+ * rejects it (a list is submitted only to the device it was created for). */
 ZR_API zr_result zr_cmd_create(zr_device *dev, zr_cmd **out);
 ZR_API void zr_cmd_destroy(zr_cmd *cmd);
 ZR_API zr_result zr_cmd_begin(zr_cmd *cmd); /* resets previous contents */
@@ -319,6 +351,19 @@ ZR_API void zr_cmd_bind_uniform_buffer(zr_cmd *cmd, uint32_t set, uint32_t bindi
  * ZR_ERROR_BINDING_TYPE_MISMATCH immediately like bind_buffer does. */
 ZR_API zr_result zr_cmd_bind_uniform_by_name(zr_cmd *cmd, const zr_pipeline *p, const char *name,
                                              const zr_buffer *buf, uint64_t offset, uint64_t range);
+/* CommandEncoder::push_constants (command.rs:180-185): `layout` is the pipeline
+ * whose layout the reference passes (CommonPipeline::layout); `size` bytes of
+ * `data` are copied at record time (vkCmdPushConstants semantics) into the
+ * push-constant state at `offset`, and later draws read them from their kernel
+ * arguments.  Latched ZR_ERROR_VALIDATION_FAILED (the vkCmdPushConstants valid
+ * usage): offset or size not a multiple of 4, size 0, offset + size >
+ * ZR_MAX_PUSH_CONSTANTS_SIZE, stage_flags 0, a byte of the update outside a range
+ * of `layout` holding every stage in stage_flags, or stage_flags missing a stage
+ * of a range the update overlaps.  A draw whose pipeline reads push constants
+ * fails (VALIDATION_FAILED) if the bytes it reads were not pushed, or were pushed
+ * with a layout whose ranges differ from its own. */
+ZR_API void zr_cmd_push_constants(zr_cmd *cmd, const zr_pipeline *layout, uint32_t stage_flags, uint32_t offset,
+                                  uint32_t size, const void *data);
 /* command.rs:171-177 */
 ZR_API void zr_cmd_set_viewport(zr_cmd *cmd, uint32_t first, uint32_t count, const zr_viewport *vps);
 ZR_API void zr_cmd_set_scissor(zr_cmd *cmd, uint32_t first, uint32_t count, const zr_rect2d *rects);

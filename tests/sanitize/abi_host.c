@@ -99,11 +99,60 @@ int main(void) {
     EXPECT(pipeline(sh[0][0], sh[0][1], ok, 2, 0, 4, NULL) == ZR_ERROR_FEATURE_NOT_PRESENT); /* MSAA */
     EXPECT(pipeline(sh[0][0], sh[1][1], ok, 2, 0, 1, NULL) == ZR_ERROR_FEATURE_NOT_PRESENT); /* mixed programs */
 
-    /* recording with a NULL command list is a no-op; a NULL device cannot record */
+    /* recording with a NULL command list is a no-op */
     zr_cmd_set_tile_shard(NULL, 0, 1);
     zr_cmd_set_route_capacity(NULL, 0);
-    zr_cmd* cmd = NULL;
-    EXPECT(zr_cmd_create(NULL, &cmd) != ZR_SUCCESS);
+    zr_cmd_push_constants(NULL, NULL, 0, 0, 0, NULL);
+
+    /* push constants (command.rs:180-185) on a device-less list: host validation */
+    {
+        zr_shader *mvs = NULL, *mps = NULL;
+        EXPECT(zr_shader_lookup(NULL, "content/shaders/mesh_push.slang", "vsmain", ZR_SHADER_STAGE_VERTEX, &mvs) == 0);
+        EXPECT(zr_shader_lookup(NULL, "content/shaders/mesh_push.slang", "psmain", ZR_SHADER_STAGE_FRAGMENT, &mps) == 0);
+        EXPECT(zr_shader_push_constant_size(mvs) == 64 && zr_shader_push_constant_size(mps) == 0);
+        const zr_vertex_binding mvb = {0, 32, 0};
+        const zr_vertex_attribute mat[3] = {{0, 0, ZR_FORMAT_R32G32B32_SFLOAT, 0}, {1, 0, ZR_FORMAT_R32G32B32_SFLOAT, 12},
+                                            {2, 0, ZR_FORMAT_R32G32_SFLOAT, 24}};
+        zr_graphic_pipeline_desc d;
+        memset(&d, 0, sizeof d);
+        d.vertex_shader = mvs;
+        d.fragment_shader = mps;
+        d.vertex_binding_count = 1;
+        d.vertex_bindings = &mvb;
+        d.vertex_attribute_count = 3;
+        d.vertex_attributes = mat;
+        d.topology = 3;
+        d.samples = 1;
+        zr_pipeline* mp = NULL;
+        EXPECT(zr_pipeline_create(NULL, &d, &mp, NULL) == ZR_SUCCESS);
+        zr_push_constant_range rg[2];
+        EXPECT(zr_pipeline_push_constant_ranges(mp, rg, 2) == 1 && rg[0].stage_flags == ZR_SHADER_STAGE_ALL_GRAPHICS &&
+               rg[0].offset == 0 && rg[0].size == 64);
+        const zr_push_constant_range short_range = {ZR_SHADER_STAGE_VERTEX, 0, 32};
+        d.push_constant_range_count = 1;
+        d.push_constant_ranges = &short_range;
+        zr_pipeline* bad = NULL;
+        EXPECT(zr_pipeline_create(NULL, &d, &bad, NULL) == ZR_ERROR_VALIDATION_FAILED && bad == NULL);
+        float view[16];
+        for (int i = 0; i < 16; ++i) view[i] = (float)i;
+        zr_cmd* cmd = NULL;
+        EXPECT(zr_cmd_create(NULL, &cmd) == ZR_SUCCESS && cmd != NULL);
+        EXPECT(zr_cmd_begin(cmd) == ZR_SUCCESS);
+        zr_cmd_push_constants(cmd, mp, ZR_SHADER_STAGE_ALL_GRAPHICS, 0, 64, view);
+        zr_cmd_push_constants(cmd, mp, ZR_SHADER_STAGE_ALL_GRAPHICS, 16, 16, view);
+        EXPECT(zr_cmd_end(cmd) == ZR_SUCCESS);
+        EXPECT(zr_submit((zr_device*)view, cmd, NULL) == ZR_ERROR_VALIDATION_FAILED); /* not its device */
+        EXPECT(zr_cmd_begin(cmd) == ZR_SUCCESS);
+        zr_cmd_push_constants(cmd, mp, ZR_SHADER_STAGE_VERTEX, 0, 64, view); /* misses the range's stages */
+        EXPECT(zr_cmd_end(cmd) == ZR_ERROR_VALIDATION_FAILED);
+        EXPECT(zr_cmd_begin(cmd) == ZR_SUCCESS);
+        zr_cmd_push_constants(cmd, mp, ZR_SHADER_STAGE_ALL_GRAPHICS, 60, 8, view); /* past the range */
+        EXPECT(zr_cmd_end(cmd) == ZR_ERROR_VALIDATION_FAILED);
+        zr_cmd_destroy(cmd);
+        zr_pipeline_destroy(mp);
+        zr_shader_destroy(mvs);
+        zr_shader_destroy(mps);
+    }
 
     /* the collectives' host plans (tests/test_abi.py checks their content) */
     zr_transfer_op ops[80];

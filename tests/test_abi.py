@@ -10,6 +10,7 @@ import ctypes as C
 import os
 import re
 
+import numpy as np
 import pytest
 
 from zenith_amd import rhi, zr
@@ -216,3 +217,165 @@ def test_exchange_plan_pairs_every_peer(world):
         assert all(off == p * bpr and nb == bpr for p, _, off, nb in ops)
     assert lib.zr_exchange_plan(33, 0, bpr, None, 0) == -1
     assert lib.zr_gather_plan(1080, 7680, 2, 2, 0, None, 0) == -1
+
+
+# ------------------------------------------------- push constants (host only)
+# CommandEncoder::push_constants (command.rs:180-185), ShaderReflection::
+# push_constant_size (shader.rs:214, :224-228, :408-413) and the pipeline
+# layout's push-constant range (pipeline.rs:78, :105, :112-128).
+MESH_FIELDS = (("position", 3), ("normal", 3), ("uv", 2))  # zenith-asset Vertex (render.rs:12-16)
+
+
+def _mesh_input(path="content/shaders/mesh_push.slang"):
+    vs = shader(path, "vsmain", rhi.ShaderStage.Vertex)
+    ps = shader(path, "psmain", rhi.ShaderStage.Fragment)
+    return vs, ps, rhi.GraphicShaderInputBuilder().vertex_shader(vs).fragment_shader(ps) \
+        .vertex_layout(MESH_FIELDS).build()
+
+
+def _mesh_pipeline(path="content/shaders/mesh_push.slang", ranges=None):
+    _, _, inp = _mesh_input(path)
+    st = rhi.GraphicPipelineState()
+    st.color_attachments = [rhi.ColorAttachmentDesc()]
+    return rhi.GraphicPipeline(None, inp, st, [zr.FORMAT_B8G8R8A8_SRGB], zr.FORMAT_D32_SFLOAT, ranges)
+
+
+def test_push_constant_reflection_and_layout():
+    vs, ps, inp = _mesh_input()
+    assert vs.reflection()["push_constant_size"] == 64 and vs.reflection()["bindings"] == []
+    assert ps.reflection()["push_constant_size"] == 0
+    assert inp.push_constant_size == 64  # merged: the max over the stages
+    # the uniform form of the program reflects no push constants
+    assert shader("content/shaders/mesh.slang", "vsmain", rhi.ShaderStage.Vertex).reflection()["push_constant_size"] == 0
+    assert _mesh_input("content/shaders/mesh.slang")[2].push_constant_size == 0
+    p = _mesh_pipeline()
+    assert p.push_constant_ranges() == [(zr.SHADER_STAGE_ALL_GRAPHICS, 0, 64)]  # derived (pipeline.rs:112-120)
+    p.destroy()
+    q = _mesh_pipeline("content/shaders/mesh.slang")
+    assert q.push_constant_ranges() == []  # size 0: no range
+    q.destroy()
+    r = _mesh_pipeline(ranges=[(zr.SHADER_STAGE_VERTEX, 0, 128)])  # a caller's range covering the block
+    assert r.push_constant_ranges() == [(zr.SHADER_STAGE_VERTEX, 0, 128)]
+    r.destroy()
+
+
+@pytest.mark.parametrize("ranges", [
+    [(zr.SHADER_STAGE_VERTEX, 0, 60)],                                   # block [0, 64) not covered
+    [(zr.SHADER_STAGE_FRAGMENT, 0, 64)],                                 # no range holds the vertex stage
+    [(zr.SHADER_STAGE_VERTEX, 2, 64)],                                   # offset not a multiple of 4
+    [(zr.SHADER_STAGE_VERTEX, 0, 66)],                                   # size not a multiple of 4
+    [(zr.SHADER_STAGE_VERTEX, 0, 132)],                                  # past maxPushConstantsSize
+    [(zr.SHADER_STAGE_VERTEX, 0, 0)],                                    # empty
+    [(0, 0, 64)],                                                        # no stage
+    [(zr.SHADER_STAGE_VERTEX, 0, 32), (zr.SHADER_STAGE_VERTEX, 32, 32)],  # a stage in two ranges
+])
+def test_push_constant_range_validation(ranges):
+    with pytest.raises(zr.ZrError) as e:
+        _mesh_pipeline(ranges=ranges)
+    assert e.value.code == zr.ERROR_VALIDATION_FAILED
+
+
+def test_push_constant_ranges_split_by_stage():
+    # two ranges, one per stage, covering the vertex block: valid layout
+    p = _mesh_pipeline(ranges=[(zr.SHADER_STAGE_VERTEX, 0, 64), (zr.SHADER_STAGE_FRAGMENT, 64, 16)])
+    assert len(p.push_constant_ranges()) == 2
+    p.destroy()
+
+
+class _DevicelessEncoder(rhi.CommandEncoder):
+    """A command list without a device (zr_cmd_create(NULL)): records and
+    validates on the host; zr_submit would reject it."""
+
+    def __init__(self):
+        h = C.c_void_p()
+        zr.check(zr.lib().zr_cmd_create(None, C.byref(h)), "zr_cmd_create")
+        self.handle, self.device, self._keep = h, None, []
+
+
+VIEW = np.arange(16, dtype=np.float32)
+
+
+@pytest.mark.parametrize("stages,offset,data,ok", [
+    (zr.SHADER_STAGE_ALL_GRAPHICS, 0, VIEW, True),                   # the whole block, the range's stages
+    (zr.SHADER_STAGE_ALL_GRAPHICS, 32, VIEW[:8], True),              # a sub-range at an offset
+    (zr.SHADER_STAGE_VERTEX, 0, VIEW, False),                        # misses stages of the range (01796)
+    (zr.SHADER_STAGE_ALL_GRAPHICS, 4, VIEW, False),                  # bytes past the range (01795)
+    (zr.SHADER_STAGE_ALL_GRAPHICS, 2, VIEW[:4], False),              # offset not a multiple of 4
+    (zr.SHADER_STAGE_ALL_GRAPHICS, 0, b"\0" * 6, False),             # size not a multiple of 4
+    (zr.SHADER_STAGE_ALL_GRAPHICS, 0, b"", False),                   # empty
+    (zr.SHADER_STAGE_ALL_GRAPHICS, 124, VIEW[:2], False),            # past maxPushConstantsSize
+    (0, 0, VIEW, False),                                             # no stage flags
+])
+def test_push_constants_recording_validation(stages, offset, data, ok):
+    p = _mesh_pipeline()
+    enc = _DevicelessEncoder()
+    try:
+        enc.begin()
+        enc.push_constants(p.layout(), stages, offset, data)
+        if ok:
+            enc.end()
+        else:
+            with pytest.raises(zr.ZrError) as e:
+                enc.end()  # the recording error is latched (vkCmd* return void)
+            assert e.value.code == zr.ERROR_VALIDATION_FAILED
+    finally:
+        enc.destroy()
+        p.destroy()
+
+
+def test_push_constants_without_layout_range():
+    # mesh.slang has no push-constant block, so its layout has no range at all
+    q = _mesh_pipeline("content/shaders/mesh.slang")
+    enc = _DevicelessEncoder()
+    try:
+        enc.begin()
+        enc.push_constants(q.layout(), zr.SHADER_STAGE_ALL_GRAPHICS, 0, VIEW)
+        with pytest.raises(zr.ZrError) as e:
+            enc.end()
+        assert e.value.code == zr.ERROR_VALIDATION_FAILED
+    finally:
+        enc.destroy()
+        q.destroy()
+
+
+def test_deviceless_list_is_not_submittable():
+    enc = _DevicelessEncoder()
+    try:
+        enc.begin()
+        enc.end()
+        # (the device pointer is never dereferenced: the list's own device is checked first)
+        rc = zr.lib().zr_submit(C.c_void_p(0x10), enc.handle, None)
+        assert rc == zr.ERROR_VALIDATION_FAILED
+    finally:
+        enc.destroy()
+
+
+@pytest.mark.parametrize("fields,fmts", [
+    ((("position", 3), ("id", 1, "u32")), [zr.FORMAT_R32G32B32_SFLOAT, zr.FORMAT_R32_UINT]),
+    ((("p", 2), ("q", 4, "i32"), ("r", 3, "u32"), ("s", 1, "i32"), ("t", 1)),
+     [zr.FORMAT_R32G32_SFLOAT, zr.FORMAT_R32G32B32A32_SINT, zr.FORMAT_R32G32B32_UINT, zr.FORMAT_R32_SINT,
+      zr.FORMAT_R32_SFLOAT]),
+])
+def test_vertex_layout_integer_fields(fields, fmts):
+    """The derive's u32 / i32 mapping (zenith-rhi-derive/src/lib.rs:175-231)."""
+    b, attrs = rhi.vertex_layout(fields)
+    assert [a.format for a in attrs] == fmts
+    assert b.stride == 4 * sum(f[1] for f in fields)
+    assert [a.offset for a in attrs] == list(np.cumsum([0] + [4 * f[1] for f in fields[:-1]]))
+
+
+def test_vertex_layout_rejects_what_the_derive_rejects():
+    for bad in ((("x", 5),), (("x", 2, "f64"),), (("x", 3, "u16"),)):
+        with pytest.raises(TypeError):
+            rhi.vertex_layout(bad)
+
+
+def test_integer_field_mismatch_is_reported():
+    """A Vertex whose colour is [u32; 3] against triangle.slang (float3 color):
+    VertexAttributeFormatMismatch at location 1, as validate_vertex_inputs
+    reports it (pipeline.rs:259-270)."""
+    with pytest.raises(rhi.GraphicShaderInputBuildError) as e:
+        _builder().vertex_layout((("position", 3), ("color", 3, "u32"))).build()
+    assert e.value.code == zr.ERROR_VERTEX_ATTRIBUTE_FORMAT_MISMATCH
+    assert (e.value.location, e.value.expected, e.value.provided) == (1, zr.FORMAT_R32G32B32_SFLOAT,
+                                                                      zr.FORMAT_R32G32B32_UINT)

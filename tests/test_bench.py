@@ -80,3 +80,83 @@ def test_bench_emulate_shard(setup):
     if setup == "partitioned":
         assert d["route_capacity"] > 0 and all(r["route_fallback_draws"] == 0 for r in d["ranks"])
         assert sum(r["triangles_setup"] for r in d["ranks"]) >= 100_000 * 0.9
+
+
+# ------------------------------------------------ launcher-less multi-GPU runs
+def test_worker_commands():
+    """bench.py --gpus N without a launcher: N children of the same script with the
+    same arguments, ranks / device ids / a 127.0.0.1 rendezvous in their env."""
+    import bench
+    argv = ["--gpus", "4", "--steps", "5", "--config", "c3"]
+    cmds = bench.worker_commands(4, argv, 29777, base_env={"PATH": "/usr/bin", "HSA_ENABLE_IPC_MODE_LEGACY": "0"})
+    assert len(cmds) == 4
+    for r, (cmd, env) in enumerate(cmds):
+        assert cmd[0] == sys.executable and cmd[-len(argv):] == argv
+        assert os.path.basename(cmd[-len(argv) - 1]) == "bench.py"
+        assert (env["RANK"], env["LOCAL_RANK"], env["WORLD_SIZE"]) == (str(r), str(r), "4")
+        assert env["MASTER_ADDR"] == "127.0.0.1" and env["MASTER_PORT"] == "29777"
+        assert env["HSA_ENABLE_IPC_MODE_LEGACY"] == "0" and env["PATH"] == "/usr/bin"  # inherited
+
+
+def _py(code):
+    return ([sys.executable, "-c", code], dict(os.environ))
+
+
+def test_run_workers_relays_rank0_line():
+    import io
+    import bench
+    buf = io.StringIO()
+    rc = bench.run_workers([_py("print('{\"value\": 1}')"), _py("print('rank1 noise')")], out=buf)
+    assert rc == 0 and buf.getvalue().strip() == '{"value": 1}'  # rank 1's stdout is not relayed
+
+
+def test_run_workers_propagates_failure_and_stops_the_rest():
+    """A failing worker ends the run with its exit status; the others (which would
+    wait in a collective for it) are stopped instead of waited for."""
+    import io
+    import time
+    import bench
+    t0 = time.monotonic()
+    rc = bench.run_workers([_py("import time; time.sleep(60)"), _py("import sys; sys.exit(3)"),
+                            _py("import time; time.sleep(60)")], out=io.StringIO())
+    assert rc == 3 and time.monotonic() - t0 < 30
+    rc = bench.run_workers([_py("import os, signal; os.kill(os.getpid(), signal.SIGKILL)")], out=io.StringIO())
+    assert rc == 128 + 9
+    t0 = time.monotonic()
+    rc = bench.run_workers([_py("import time; time.sleep(60)")], out=io.StringIO(), timeout=1.0)
+    assert rc == 124 and time.monotonic() - t0 < 30
+
+
+def test_launcherless_parent_never_touches_the_gpu(monkeypatch):
+    """The launcher path returns before any HIP call: main() with WORLD_SIZE unset
+    and --gpus 2 only builds worker commands (here intercepted)."""
+    import bench
+    seen = {}
+
+    def fake_launch(a, argv):
+        seen["gpus"], seen["argv"] = a.gpus, argv
+        return 0
+    monkeypatch.delenv("WORLD_SIZE", raising=False)
+    monkeypatch.setattr(bench, "launch_workers", fake_launch)
+    monkeypatch.setattr(sys, "argv", ["bench.py", "--gpus", "2", "--steps", "3"])
+    monkeypatch.setattr(bench.torch.cuda, "set_device", lambda *x: (_ for _ in ()).throw(AssertionError("GPU")))
+    with pytest.raises(SystemExit) as e:
+        bench.main()
+    assert e.value.code == 0 and seen == {"gpus": 2, "argv": ["--gpus", "2", "--steps", "3"]}
+
+
+@pytest.mark.gpu
+def test_bench_force_dist_worker_path():
+    """bench.py --gpus 1 --force-dist without a launcher runs through the worker
+    launcher (one RCCL rank, the runtime's exchange + row gather) and prints one
+    JSON line."""
+    cmd = [sys.executable, os.path.join(ROOT, "bench.py"), "--gpus", "1", "--force-dist", "--config", "c1",
+           "--steps", "4", "--warmup", "2", "--cold-copies", "0", "--setup", "partitioned", "--worker-timeout", "100"]
+    env = dict(os.environ)
+    env.pop("WORLD_SIZE", None)
+    out = subprocess.run(cmd, cwd=ROOT, capture_output=True, text=True, timeout=115, env=env)
+    assert out.returncode == 0, out.stderr[-2000:]
+    lines = [ln for ln in out.stdout.splitlines() if ln.strip()]
+    assert len(lines) == 1, out.stdout
+    d = json.loads(lines[0])
+    assert d["n_gpus"] == 1 and d["value"] > 0 and "RCCL" in d["config"]["parallelism"]

@@ -163,8 +163,9 @@ def test_record_table(monkeypatch, table):
     """k_tile's 512-thread resolve with its LDS record table forced on or off
     (ZR_REC_TABLE; the runtime enables it from 256 primitives per tile): exact on
     every program and depth op, with large primitives among small ones, a tile-row
-    shard, a tile list longer than the table (1024 slots: lookups that miss fall
-    back to the gathered record) and the spill path."""
+    shard, tile lists of several 1024-entry segments (the 2048-slot hash keeps the
+    earlier segments' slots; lookups that miss fall back to the gathered record),
+    large primitives in the later segments of such lists, and the spill path."""
     monkeypatch.setenv("ZR_REC_TABLE", str(table))
     monkeypatch.setenv("ZR_TILE_NT", "512")
     dev = rhi.RenderDevice(0)
@@ -182,6 +183,18 @@ def test_record_table(monkeypatch, table):
         # ~2900 entries per 32x32 tile: three segments, the table full after the first
         dense = scenes.soup_scene(87, 40000, 96, 96, 5.0, scenes.PROGRAM_BLINN_PHONG)
         assert_parity(dev, dense)
+        # large primitives in every segment of ~5000-entry tiles: a large entry's
+        # sorted position held an earlier segment's small record, and a hash slot
+        # that segment inserted for the position must not resolve to it
+        small = scenes.soup_arrays(89, 30000, 96, 96, 5.0, True).reshape(-1, 3, 9)
+        big = scenes.soup_arrays(90, 1200, 96, 96, 150.0, True).reshape(-1, 3, 9)
+        v = np.concatenate([np.concatenate([small[25 * i:25 * i + 25], big[i:i + 1]]) for i in range(1200)])
+        mixed = scenes.Scene("segments_with_large", 96, 96, scenes.PROGRAM_BLINN_PHONG, v.reshape(-1, 9),
+                             np.arange(3 * len(v), dtype=np.uint32), depth=True)
+        assert_parity(dev, mixed)
+        for op in (scenes.OP_LEQUAL, scenes.OP_GREATER):
+            mixed.depth_op, mixed.depth_clear = op, (0.0 if op == scenes.OP_GREATER else 1.0)
+            assert_parity(dev, mixed)
     finally:
         dev.close()
     monkeypatch.setenv("ZR_BIN_CAPACITY", "1024")  # the spill path (records set up again, not read)
@@ -589,6 +602,59 @@ def test_mesh_cerberus(device):
     """The reference's cerberus asset (33,543 triangles) through the camera."""
     assert_parity(device, scenes.cerberus_scene(640, 480))
     assert_parity(device, scenes.cerberus_scene(1920, 1080))
+
+
+@pytest.mark.parametrize("scene", ["cerberus", "soup"])
+def test_mesh_push_constants(device, scene):
+    """View.view_proj recorded with CommandEncoder::push_constants (command.rs:180-185;
+    mesh_push.slang) instead of bound as the View uniform: bit-exact with the
+    oracle and with the uniform render of the same scene."""
+    s = scenes.cerberus_scene(640, 480) if scene == "cerberus" else scenes.mesh_soup_scene(36, 3000, 320, 240)
+    uc, ud = renderer.render_scene(device, s)
+    s.push_view = True
+    pc, pd = assert_parity(device, s)
+    assert np.array_equal(pc, uc) and np.array_equal(pd.view(np.uint32), ud.view(np.uint32))
+
+
+def test_mesh_push_constants_errors(device):
+    """A draw whose pipeline reads push constants that were not pushed, or were
+    pushed with a layout of other ranges, fails at submit (VALIDATION_FAILED)."""
+    s = scenes.mesh_soup_scene(37, 200, 64, 64)
+    s.push_view = True
+    r = renderer.SceneRenderer(device, s)
+    color = rhi.Texture(device, rhi.TextureDesc.new_color("rt", 64, 64, s.color_format))
+    depth = rhi.Texture(device, rhi.TextureDesc.new_depth("ds", 64, 64))
+    other = rhi.GraphicPipeline(device, r.pipeline.shader, r.pipeline.state, [s.color_format], zr.FORMAT_D32_SFLOAT,
+                                push_constant_ranges=[(zr.SHADER_STAGE_VERTEX, 0, 64)])
+    try:
+        for push in (None, "half", "other_layout"):
+            enc = rhi.CommandEncoder(device)
+
+            def job(ctx):
+                e = ctx.encoder()
+                ctx.begin_rendering((64, 64))
+                ctx.bind_pipeline()
+                vp = np.asarray(s.view_proj, np.float32)
+                if push == "half":
+                    e.push_constants(ctx.pipeline.layout(), zr.SHADER_STAGE_ALL_GRAPHICS, 0, vp[:8])
+                elif push == "other_layout":
+                    e.push_constants(other, zr.SHADER_STAGE_VERTEX, 0, vp)
+                e.set_viewport(0, [rhi.Viewport(0.0, 0.0, 64.0, 64.0)])
+                e.set_scissor(0, [rhi.Rect2D(0, 0, 64, 64)])
+                e.bind_vertex_buffers(0, [r.vertex_buffer], [0])
+                e.bind_index_buffer(r.index_buffer, 0, s.index_type)
+                e.draw_indexed(s.draw_count, 1, 0, 0, 0)
+                ctx.end_rendering()
+
+            rhi.execute_graphic_node(device, enc, r.pipeline, [color], depth, job)
+            with pytest.raises(zr.ZrError) as e:
+                device.submit_and_wait(enc)
+            assert e.value.code == zr.ERROR_VALIDATION_FAILED
+            enc.destroy()
+    finally:
+        other.destroy()
+        color.destroy()
+        depth.destroy()
 
 
 def test_mesh_shards_and_spill(monkeypatch, device):

@@ -83,6 +83,8 @@ struct alignas(8) BBox {
     uint32_t bb0, bb1;  // as TriRecord::bb0/bb1
 };
 constexpr uint32_t kMaxTilesPerPass = 16384;  // LDS histogram of the setup pass (64 KB)
+constexpr uint32_t kMaxPushBytes = 128;       // ZR_MAX_PUSH_CONSTANTS_SIZE (Vulkan's guaranteed minimum)
+constexpr uint32_t kMaxPushWords = kMaxPushBytes / 4;
 
 // Partitioned setup for tile-row shards.  Rank r sets up the
 // primitives of its range [r * span, (r + 1) * span), kRouteChunk per workgroup
@@ -190,6 +192,7 @@ struct DrawParams {
     uint32_t depth_write_out; // write the winner's depth
     // shading
     int32_t program;
+    uint32_t view_push;       // mesh program: the matrix is push[0, 16) instead of *view_proj (mesh_push.slang)
     const float* time_ptr;    // Time.time uniform (device) or nullptr
     const float* view_proj;   // mesh program: View.view_proj, 16 floats column-major (device)
     // tiling / sharding
@@ -225,6 +228,10 @@ struct DrawParams {
     uint32_t debug;           // kDebug* bits (timing experiments only)
     unsigned long long* dbg_ts; // [setup_wgs][8] s_memrealtime stamps (kDebugStamps only)
     uint32_t* status;         // host-mapped
+    // push-constant state at the draw (zr_cmd_push_constants): the bytes ride in
+    // the launch's kernel arguments, as Vulkan push constants ride in user SGPRs
+    // (last, so the fields above keep their kernarg offsets)
+    float push[kMaxPushWords];
 };
 
 // k_tile workgroup size for a pass of `ntiles` tiles on `cus` CUs: 4 waves per

@@ -382,6 +382,18 @@ __device__ __forceinline__ void mesh_transform(const float* M, const float3 p, f
     }
 }
 
+// The camera matrix of the draw: the View uniform (device memory), or for a
+// pipeline whose vertex stage takes it as push constants (mesh_push.slang) the
+// bytes zr_cmd_push_constants recorded, carried in this launch's kernel arguments
+// (DrawParams::push; every kernel here takes the one DrawParams at offset 0).
+__device__ __forceinline__ const float* view_matrix(const DrawParams& P) {
+    if (P.view_push) {
+        const KernargParams kp = (KernargParams)__builtin_amdgcn_kernarg_segment_ptr();
+        return (const float*)kp->push;
+    }
+    return P.view_proj;
+}
+
 // Sutherland-Hodgman against the Vulkan depth planes z >= 0, then z <= w (x / y
 // use the guard band), vertex order kept from v0: new vertex a + t (b - a),
 // t = da / (da - db).  Returns the polygon size (0, 3, 4 or 5).  Only primitives
@@ -431,7 +443,7 @@ __device__ __forceinline__ bool mesh_geometry(const DrawParams& P, const PrimIn&
     if (!in.ok) return false;
     float c[3][4];
 #pragma unroll
-    for (int k = 0; k < 3; ++k) mesh_transform(P.view_proj, in.p[k], c[k]);
+    for (int k = 0; k < 3; ++k) mesh_transform(view_matrix(P), in.p[k], c[k]);
     bool inside = true;
 #pragma unroll
     for (int k = 0; k < 3; ++k) inside = inside && c[k][2] >= 0.0f && c[k][3] - c[k][2] >= 0.0f;
@@ -603,7 +615,7 @@ __device__ __forceinline__ void mesh_edge_planes(const DrawParams& P, const floa
 #pragma unroll
     for (int k = 0; k < 3; ++k) {
         float c[4];
-        mesh_transform(P.view_proj, p[k], c);
+        mesh_transform(view_matrix(P), p[k], c);
         hX[k] = (double)c[0] * (double)P.hw + (double)c[3] * (double)P.cx;
         hY[k] = (double)c[1] * (double)P.hh + (double)c[3] * (double)P.cy;
         hW[k] = (double)c[3];
@@ -651,7 +663,7 @@ __device__ __forceinline__ BBox setup_finish_mesh(const DrawParams& P, uint32_t 
     float c[3][4];
     if (fast) {
 #pragma unroll
-        for (int k = 0; k < 3; ++k) mesh_transform(P.view_proj, in.p[k], c[k]);
+        for (int k = 0; k < 3; ++k) mesh_transform(view_matrix(P), in.p[k], c[k]);
 #pragma unroll
         for (int k = 0; k < 3; ++k) fast = fast && c[k][2] >= 0.0f && c[k][3] - c[k][2] >= 0.0f;
     }
@@ -1399,7 +1411,10 @@ __device__ __forceinline__ void resolve_vids(const DrawParams& P, uint32_t prim,
 // sorted array still holds that record at j (a later segment reuses positions).
 // The raster inserts each entry as it loads it; the resolve looks its winners up
 // and gathers the record only when that fails (a table overwritten by a later
-// segment, a long probe, a large primitive).  Every winner request the pass saves
+// segment, a long probe, a large primitive).  A large primitive is not hashed, but
+// its position's slot gets the large marker, so a stale hash slot an earlier
+// segment left for that position decodes as large (records_big), never as the
+// earlier segment's small record.  Every winner request the pass saves
 // is worth ~20 ns of a C2 tile pass (docs/EXPERIMENTS.md).
 constexpr uint32_t kRecHashSlots = 2048;
 constexpr uint32_t kRecTabProbes = 8;
@@ -2068,7 +2083,18 @@ __global__ __launch_bounds__(NT, kTileWgs * kTileThreads / 256) void k_tile(Draw
                 const bool valid = j < n && !(tile_debug(P) & kDebugLoadOnly);
                 if (tile_debug(P) & kDebugLoadOnly) asm volatile("" ::"v"(q0.x), "v"(q1.x), "v"(my_prim));
                 const bool large = compact_is_large(q0);
-                if (tab && valid && !large && sub == 0) rec_table_insert(s_thash, s_trec, my_prim, j, q0, q1, x0, y0);
+                if (tab && valid && sub == 0) {
+                    if (!large) {
+                        rec_table_insert(s_thash, s_trec, my_prim, j, q0, q1, x0, y0);
+                    } else {
+                        // not hashed, but position j must not keep an earlier segment's
+                        // small record: a hash slot that segment inserted for j would
+                        // pass rec_table_find's s_sorted[j] check for this primitive.
+                        // The large marker (dx1 == kCompactLarge in q0.z) sends such a
+                        // lookup to records_big.
+                        s_trec[j] = make_int4(0, q0.z, 0, 0);
+                    }
+                }
                 if (valid && !large && !(tile_debug(P) & kDebugSkipLanePath)) {
                     const TriRecord r = decode_compact(P, q0, q1, true);
                     raster_lane<MODE, INITD>(P, r, entry_seq<PROG>(P, my_prim), x0, y0, s_key, s_initd, sub, (int)ksh);

@@ -51,6 +51,7 @@ struct ShaderEntry {
     zr_shader_binding bind[1];
     int ninputs;
     zr_vertex_input_attr inputs[4];
+    uint32_t push_size;  // ShaderReflection::push_constant_size (shader.rs:214)
 };
 
 // Built-in stage variants.  triangle.slang is the reference's
@@ -73,6 +74,11 @@ const ShaderEntry kShaders[] = {
      {{"View", 0, 0, ZR_DESCRIPTOR_TYPE_UNIFORM_BUFFER, 1, ZR_SHADER_STAGE_VERTEX}},
      3, {{0, ZR_FORMAT_R32G32B32_SFLOAT}, {1, ZR_FORMAT_R32G32B32_SFLOAT}, {2, ZR_FORMAT_R32G32_SFLOAT}}},
     {"mesh.slang", "psmain", ZR_SHADER_STAGE_FRAGMENT, kProgMesh, 0, {}, 0, {}},
+    // mesh_push.slang: the same program with view_proj in a 64-B push-constant
+    // block (CommandEncoder::push_constants, command.rs:180-185) instead of View
+    {"mesh_push.slang", "vsmain", ZR_SHADER_STAGE_VERTEX, kProgMesh, 0, {},
+     3, {{0, ZR_FORMAT_R32G32B32_SFLOAT}, {1, ZR_FORMAT_R32G32B32_SFLOAT}, {2, ZR_FORMAT_R32G32_SFLOAT}}, 64},
+    {"mesh_push.slang", "psmain", ZR_SHADER_STAGE_FRAGMENT, kProgMesh, 0, {}, 0, {}},
 };
 
 std::string basename_of(const char* path) {
@@ -91,6 +97,7 @@ struct zr_shader_t {
     std::string file, entry;
     std::vector<zr_shader_binding> bindings;
     std::vector<zr_vertex_input_attr> inputs;
+    uint32_t push_constant_size = 0;
 };
 
 struct zr_buffer_t {
@@ -123,6 +130,9 @@ struct zr_pipeline_t {
     uint32_t attr_offset[4];
     uint32_t attr_size[4];
     std::vector<zr_shader_binding> bindings;  // merged reflection
+    uint32_t push_size = 0;                   // merged push_constant_size (shader.rs:224-228)
+    std::vector<zr_push_constant_range> push_ranges;  // the layout's (pipeline.rs:112-128)
+    bool view_push = false;                   // mesh program reading view_proj from push constants
     uint32_t cull_mode;
     int32_t front_face;
     bool has_depth_state;
@@ -134,7 +144,7 @@ struct zr_pipeline_t {
 };
 
 enum CmdType { C_BEGIN_RENDERING, C_END_RENDERING, C_BIND_PIPELINE, C_BIND_UNIFORM, C_SET_VIEWPORT, C_SET_SCISSOR,
-               C_BIND_VB, C_BIND_IB, C_DRAW, C_SET_SHARD, C_CLEAR_IMAGE, C_SET_ROUTE_CAP };
+               C_BIND_VB, C_BIND_IB, C_DRAW, C_SET_SHARD, C_CLEAR_IMAGE, C_SET_ROUTE_CAP, C_PUSH_CONSTANTS };
 
 struct RenderingState {
     zr_rect2d area;
@@ -159,6 +169,7 @@ struct Cmd {
 struct zr_cmd_t {
     zr_device* dev;
     std::vector<Cmd> cmds;
+    std::vector<uint8_t> push_data;  // C_PUSH_CONSTANTS payloads (Cmd::offset indexes it)
     zr_result err = ZR_SUCCESS;
     std::string err_msg;
     bool in_rendering = false;
@@ -500,6 +511,11 @@ struct ExecState {
     zr_exchange_fn exchange = nullptr;
     void* exchange_user = nullptr;
     uint32_t route_cap = 0;  // entries per exchange block (zr_cmd_set_route_capacity; 0: route_capacity_default)
+    // push-constant state (vkCmdPushConstants): bytes, which 4-byte words were
+    // written, and the layout they were written with
+    float push[kMaxPushWords] = {};
+    uint32_t push_written = 0;
+    const zr_pipeline* push_layout = nullptr;
 };
 
 // Entries per exchange block when the caller sets none: every primitive of the
@@ -745,7 +761,24 @@ zr_result exec_draw(zr_device* d, ExecState& s, const Cmd& c, bool indexed) {
             P.view_proj = (const float*)((const uint8_t*)it->second.first->ptr + it->second.second);
         }
     }
-    if (mesh && !P.view_proj) return fail(ZR_ERROR_VALIDATION_FAILED, "descriptor 'View' not bound");
+    if (pp->view_push) {
+        // mesh_push.slang: View.view_proj is push-constant bytes [0, 64)
+        if ((s.push_written & 0xFFFFu) != 0xFFFFu)
+            return fail(ZR_ERROR_VALIDATION_FAILED, "push constants [0, 64) (View.view_proj) not pushed before the draw");
+        if (s.push_layout != pp && (!s.push_layout || s.push_layout->push_ranges.size() != pp->push_ranges.size() ||
+                                    !std::equal(pp->push_ranges.begin(), pp->push_ranges.end(),
+                                                s.push_layout->push_ranges.begin(),
+                                                [](const zr_push_constant_range& a, const zr_push_constant_range& b) {
+                                                    return a.stage_flags == b.stage_flags && a.offset == b.offset &&
+                                                           a.size == b.size;
+                                                })))
+            return fail(ZR_ERROR_VALIDATION_FAILED,
+                        "push constants were pushed with a layout whose ranges differ from the bound pipeline's");
+        memcpy(P.push, s.push, sizeof P.push);
+        P.view_push = 1;
+        P.view_proj = nullptr;
+    }
+    if (mesh && !P.view_proj && !P.view_push) return fail(ZR_ERROR_VALIDATION_FAILED, "descriptor 'View' not bound");
     // binning geometry: k_setup_bin runs one kSetupThreads workgroup per CU at most
     // (its LDS histogram of all tiles; workgroups never wait for each other)
     if (P.ntiles > kMaxTilesPerPass)
@@ -844,7 +877,12 @@ zr_result exec_draw(zr_device* d, ExecState& s, const Cmd& c, bool indexed) {
         timed_launch(d, "exchange", ss, [&] {
             xr = s.exchange(s.exchange_user, (void*)ss, S.xsend, S.xrecv, route_block_bytes(P.route_cap));
         });
-        if (xr != ZR_SUCCESS) return fail(xr, "tile-shard exchange callback failed: " + g_last_error);
+        if (xr != ZR_SUCCESS) {
+            // the route's totals stay in the send headers (no records-mode setup will
+            // consume and re-zero them): the next draw on this set memsets them first
+            S.xsend_layout = 0;
+            return fail(xr, "tile-shard exchange callback failed: " + g_last_error);
+        }
         P.rlist = S.xrecv;
         if (no_tiles) {  // routed and exchanged; nothing of this target to draw here
             if ((rc = zero_headers())) return rc;  // (no records-mode setup to reset them)
@@ -959,6 +997,11 @@ zr_result execute(zr_device* d, zr_cmd* cmd) {
             s.exchange_user = c.exchange_user;
             break;
         case C_SET_ROUTE_CAP: s.route_cap = c.a; break;
+        case C_PUSH_CONSTANTS:
+            memcpy((uint8_t*)s.push + c.a, cmd->push_data.data() + c.offset, c.b);
+            for (uint32_t w = c.a / 4u; w < (c.a + c.b) / 4u; ++w) s.push_written |= 1u << w;
+            s.push_layout = c.pipeline;
+            break;
         }
         if (rc) return rc;
     }
@@ -1255,6 +1298,7 @@ ZR_API zr_result zr_shader_lookup(zr_device* d, const char* path, const char* en
             sh->entry = s.entry;
             sh->bindings.assign(s.bind, s.bind + s.nbind);
             sh->inputs.assign(s.inputs, s.inputs + s.ninputs);
+            sh->push_constant_size = s.push_size;
             *out = sh;
             return ZR_SUCCESS;
         }
@@ -1270,6 +1314,8 @@ ZR_API int32_t zr_shader_bindings(const zr_shader* sh, zr_shader_binding* out, i
     for (int32_t i = 0; out && i < std::min(n, capacity); ++i) out[i] = sh->bindings[i];
     return n;
 }
+
+ZR_API uint32_t zr_shader_push_constant_size(const zr_shader* sh) { return sh ? sh->push_constant_size : 0u; }
 
 ZR_API int32_t zr_shader_vertex_inputs(const zr_shader* sh, zr_vertex_input_attr* out, int32_t capacity) {
     if (!sh) return 0;
@@ -1320,6 +1366,50 @@ static zr_result validate_vertex_inputs(const zr_shader* vs, const zr_vertex_att
             if (err) *err = {kv.first, 0, kv.second};
             return fail(ZR_ERROR_UNEXPECTED_VERTEX_ATTRIBUTE,
                         "unexpected vertex attribute at location " + std::to_string(kv.first));
+        }
+    }
+    return ZR_SUCCESS;
+}
+
+// The pipeline layout's push-constant ranges.  None given: one {ALL_GRAPHICS, 0,
+// merged size} range when the size is > 0 (GraphicShaderInput::create_pipeline_layout,
+// pipeline.rs:112-128).  Given: the VkPushConstantRange / VkPipelineLayoutCreateInfo
+// valid usage (offset and size multiples of 4, size > 0, within
+// maxPushConstantsSize, no stage in two ranges), and each stage's push-constant
+// block [0, size) covered by ranges holding that stage (the pipeline's layout
+// must match its shaders).
+static zr_result push_constant_layout(const zr_graphic_pipeline_desc* desc, const zr_shader* vs, const zr_shader* fs,
+                                      uint32_t merged, std::vector<zr_push_constant_range>& out) {
+    out.clear();
+    if (desc->push_constant_range_count == 0) {
+        if (merged > kMaxPushBytes) return fail(ZR_ERROR_FEATURE_NOT_PRESENT, "push-constant block larger than 128 bytes");
+        if (merged) out.push_back(zr_push_constant_range{ZR_SHADER_STAGE_ALL_GRAPHICS, 0u, merged});
+        return ZR_SUCCESS;
+    }
+    if (!desc->push_constant_ranges) return fail(ZR_ERROR_VALIDATION_FAILED, "push_constant_ranges is NULL");
+    uint32_t stages_seen = 0;
+    for (uint32_t i = 0; i < desc->push_constant_range_count; ++i) {
+        const zr_push_constant_range& r = desc->push_constant_ranges[i];
+        if ((r.offset & 3u) || (r.size & 3u) || r.size == 0 || r.offset >= kMaxPushBytes || r.size > kMaxPushBytes - r.offset)
+            return fail(ZR_ERROR_VALIDATION_FAILED, "push-constant range " + std::to_string(i) +
+                                                        ": offset/size not multiples of 4, empty, or past 128 bytes");
+        if (r.stage_flags == 0 || (r.stage_flags & ~(uint32_t)ZR_SHADER_STAGE_ALL_GRAPHICS))
+            return fail(ZR_ERROR_VALIDATION_FAILED, "push-constant range " + std::to_string(i) + ": bad stage flags");
+        if (stages_seen & r.stage_flags)
+            return fail(ZR_ERROR_VALIDATION_FAILED, "a shader stage is in more than one push-constant range");
+        stages_seen |= r.stage_flags;
+        out.push_back(r);
+    }
+    for (const zr_shader* sh : {vs, fs}) {
+        if (!sh || sh->push_constant_size == 0) continue;
+        for (uint32_t w = 0; w < sh->push_constant_size / 4u; ++w) {
+            bool covered = false;
+            for (const auto& r : out)
+                covered = covered || ((r.stage_flags & sh->stage) && w * 4u >= r.offset && w * 4u < r.offset + r.size);
+            if (!covered)
+                return fail(ZR_ERROR_VALIDATION_FAILED, "the layout's push-constant ranges do not cover the " +
+                                                            std::string(sh->stage == ZR_SHADER_STAGE_VERTEX ? "vertex" : "fragment") +
+                                                            " stage's push-constant block");
         }
     }
     return ZR_SUCCESS;
@@ -1421,16 +1511,34 @@ ZR_API zr_result zr_pipeline_create(zr_device* d, const zr_graphic_pipeline_desc
         }
     }
     for (const auto& kv : merged) p->bindings.push_back(kv.second);
+    // push constants: the merged size (the max over the stages, shader.rs:224-228)
+    // and the layout's ranges -- derived as create_pipeline_layout does
+    // (pipeline.rs:112-128), or the caller's, validated
+    p->push_size = std::max(vs->push_constant_size, fs ? fs->push_constant_size : 0u);
+    if ((rc = push_constant_layout(desc, vs, fs, p->push_size, p->push_ranges))) {
+        delete p;
+        return rc;
+    }
+    p->view_push = p->program == kProgMesh && vs->push_constant_size >= 64u;
     *out = p;
     return ZR_SUCCESS;
 }
 
 ZR_API void zr_pipeline_destroy(zr_pipeline* p) { delete p; }
 
+ZR_API int32_t zr_pipeline_push_constant_ranges(const zr_pipeline* p, zr_push_constant_range* out, int32_t capacity) {
+    if (!p) return 0;
+    const int32_t n = (int32_t)p->push_ranges.size();
+    for (int32_t i = 0; out && i < std::min(n, capacity); ++i) out[i] = p->push_ranges[i];
+    return n;
+}
+
 // ----------------------------------------------------------------- commands
 
 ZR_API zr_result zr_cmd_create(zr_device* d, zr_cmd** out) {
-    if (!d || !out) return fail(ZR_ERROR_VALIDATION_FAILED, "NULL argument");
+    // d may be NULL: a list recorded without a device (host-side validation of the
+    // recording calls, e.g. on a machine without a GPU); zr_submit rejects it
+    if (!out) return fail(ZR_ERROR_VALIDATION_FAILED, "NULL argument");
     zr_cmd* c = new (std::nothrow) zr_cmd_t();
     if (!c) return fail(ZR_ERROR_OUT_OF_HOST_MEMORY, "cmd alloc");
     c->dev = d;
@@ -1440,20 +1548,25 @@ ZR_API zr_result zr_cmd_create(zr_device* d, zr_cmd** out) {
 
 ZR_API void zr_cmd_destroy(zr_cmd* c) {
     if (!c) return;
-    auto& pend = c->dev->pending;
-    if (std::find(pend.begin(), pend.end(), c) != pend.end()) device_sync(c->dev);
+    if (c->dev) {
+        auto& pend = c->dev->pending;
+        if (std::find(pend.begin(), pend.end(), c) != pend.end()) device_sync(c->dev);
+    }
     c->drop_graph();
     delete c;
 }
 
 ZR_API zr_result zr_cmd_begin(zr_cmd* c) {
     if (!c) return fail(ZR_ERROR_VALIDATION_FAILED, "cmd is NULL");
-    auto& pend = c->dev->pending;
-    if (std::find(pend.begin(), pend.end(), c) != pend.end()) {
-        zr_result rc = device_sync(c->dev);
-        if (rc) return rc;
+    if (c->dev) {
+        auto& pend = c->dev->pending;
+        if (std::find(pend.begin(), pend.end(), c) != pend.end()) {
+            zr_result rc = device_sync(c->dev);
+            if (rc) return rc;
+        }
     }
     c->cmds.clear();
+    c->push_data.clear();
     c->err = ZR_SUCCESS;
     c->err_msg.clear();
     c->in_rendering = false;
@@ -1550,6 +1663,40 @@ ZR_API zr_result zr_cmd_bind_uniform_by_name(zr_cmd* c, const zr_pipeline* p, co
         }
     }
     return fail(ZR_ERROR_BINDING_NOT_FOUND, std::string("binding '") + name + "' not found");
+}
+
+ZR_API void zr_cmd_push_constants(zr_cmd* c, const zr_pipeline* layout, uint32_t stage_flags, uint32_t offset,
+                                  uint32_t size, const void* data) {
+    if (!c) return;
+    if (!layout || !data) return latch(c, ZR_ERROR_VALIDATION_FAILED, "push_constants: NULL layout or data");
+    if ((offset & 3u) || (size & 3u) || size == 0 || offset >= kMaxPushBytes || size > kMaxPushBytes - offset)
+        return latch(c, ZR_ERROR_VALIDATION_FAILED,
+                     "push_constants: offset/size not multiples of 4, empty, or past maxPushConstantsSize (128)");
+    if (stage_flags == 0) return latch(c, ZR_ERROR_VALIDATION_FAILED, "push_constants: no stage flags");
+    // VUID-vkCmdPushConstants-offset-01795 / -01796: every byte of the update lies in
+    // a range holding every stage of stage_flags, and stage_flags holds every stage
+    // of each range the update overlaps
+    for (uint32_t b = offset; b < offset + size; b += 4u) {
+        uint32_t stages = 0;
+        for (const auto& r : layout->push_ranges) {
+            if (b < r.offset || b >= r.offset + r.size) continue;
+            stages |= r.stage_flags;
+            if ((r.stage_flags & stage_flags) != r.stage_flags)
+                return latch(c, ZR_ERROR_VALIDATION_FAILED,
+                             "push_constants: stage_flags miss a stage of a push-constant range the update overlaps");
+        }
+        if ((stages & stage_flags) != stage_flags)
+            return latch(c, ZR_ERROR_VALIDATION_FAILED,
+                         "push_constants: bytes outside the layout's push-constant ranges for these stages");
+    }
+    Cmd k;
+    k.type = C_PUSH_CONSTANTS;
+    k.pipeline = layout;
+    k.a = offset;
+    k.b = size;
+    k.offset = c->push_data.size();
+    c->push_data.insert(c->push_data.end(), (const uint8_t*)data, (const uint8_t*)data + size);
+    c->cmds.push_back(k);
 }
 
 ZR_API void zr_cmd_set_viewport(zr_cmd* c, uint32_t first, uint32_t count, const zr_viewport* vps) {
@@ -1677,11 +1824,14 @@ zr_result rccl_exchange(void* user, void* stream, const void* send, void* recv, 
     }
     zr_transfer_op plan[2 * kMaxShards];
     const int32_t n = zr_exchange_plan(d->comm_size, d->comm_rank, bytes_per_rank, plan, 2 * (int32_t)kMaxShards);
-    bool ok = n >= 0 && rccl_group_start(err);
+    if (n < 0) return fail(ZR_ERROR_VALIDATION_FAILED, "bad exchange plan (rank / rank count)");
+    if (!rccl_group_start(err)) return fail(ZR_ERROR_DEVICE_LOST, err);
+    bool ok = true;
     for (int32_t i = 0; ok && i < n; ++i)
         ok = plan[i].send ? rccl_send((const uint8_t*)send + plan[i].offset, plan[i].bytes, plan[i].peer, d->comm_x, s, err)
                           : rccl_recv((uint8_t*)recv + plan[i].offset, plan[i].bytes, plan[i].peer, d->comm_x, s, err);
-    if (!rccl_group_end(err) || !ok) return fail(ZR_ERROR_DEVICE_LOST, err.empty() ? "bad exchange plan" : err);
+    const bool ended = rccl_group_end(err);  // closes the group whatever the sends returned
+    if (!ended || !ok) return fail(ZR_ERROR_DEVICE_LOST, err);
     return ZR_SUCCESS;
 }
 
@@ -1863,6 +2013,7 @@ static zr_result submit_graph_or_eager(zr_device* d, zr_cmd* c) {
 
 ZR_API zr_result zr_submit(zr_device* d, zr_cmd* c, zr_fence* f) {
     if (!d || !c) return fail(ZR_ERROR_VALIDATION_FAILED, "NULL argument");
+    if (c->dev != d) return fail(ZR_ERROR_VALIDATION_FAILED, "command list was created for another device (or none)");
     if (c->err) return fail(c->err, c->err_msg);
     if (c->in_rendering) return fail(ZR_ERROR_VALIDATION_FAILED, "submitted inside a render pass");
     zr_result rc = set_device(d);

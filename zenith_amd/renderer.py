@@ -107,6 +107,8 @@ class SceneRenderer:
             self.index_buffer = rhi.Buffer(device, rhi.BufferDesc.index(f"{scene.name}.index", len(idata)))
             self.index_buffer.as_range().write(idata)
         path = PROGRAM_FILES[scene.program]
+        if scene.push_view:  # the camera matrix as push constants (command.rs:180-185)
+            path = "content/shaders/mesh_push.slang"
         self.vs = rhi.Shader.from_file(f"{scene.name}.vs", device, path, "vsmain", rhi.ShaderStage.Vertex)
         self.fs = rhi.Shader.from_file(f"{scene.name}.ps", device, path, "psmain", rhi.ShaderStage.Fragment)
         fields = [("position", 3)] + [(f"a{i}", n) for i, n in enumerate(scene.layout[1:], 1)]
@@ -129,7 +131,7 @@ class SceneRenderer:
         if scene.program == 0:
             self.time_buffer = rhi.Buffer(device, rhi.BufferDesc.uniform(f"{scene.name}.time", 4))
         self.view_buffer = None
-        if scene.view_proj is not None:  # mesh.slang's View { float4x4 view_proj }
+        if scene.view_proj is not None and not scene.push_view:  # mesh.slang's View { float4x4 view_proj }
             self.view_buffer = rhi.Buffer(device, rhi.BufferDesc.uniform(f"{scene.name}.view", 64))
         self.encoder = rhi.CommandEncoder(device)
 
@@ -158,6 +160,9 @@ class SceneRenderer:
                 ctx.bind_descriptor_sets(binder)
             ctx.begin_rendering((W, H))
             ctx.bind_pipeline()
+            if s.push_view:  # mesh_push.slang: View.view_proj at push-constant offset 0
+                enc.push_constants(ctx.pipeline.layout(), zr.SHADER_STAGE_ALL_GRAPHICS, 0,
+                                   np.asarray(s.view_proj, np.float32))
             vp = viewport or (0.0, 0.0, float(W), float(H), 0.0, 1.0)
             sc = scissor or (0, 0, W, H)
             enc.set_viewport(0, [rhi.Viewport(*vp)])

@@ -304,6 +304,7 @@ class Shader:
                               descriptor_type=b[i].descriptor_type, stage_flags=b[i].stage_flags)
                          for i in range(nb)],
             "vertex_inputs": [(v[i].location, v[i].format) for i in range(nv)],
+            "push_constant_size": int(lib().zr_shader_push_constant_size(self.handle)),
         }
 
 
@@ -323,15 +324,32 @@ class VertexAttribute:
     offset: int
 
 
+# vk_format_for_type / vk_format_for_scalar_array (zenith-rhi-derive/src/lib.rs:175-231):
+# scalars f32/u32/i32 (n = 1) and arrays [T; 2..4] of them
+_VERTEX_FORMATS = {
+    ("f32", 1): zr.FORMAT_R32_SFLOAT, ("u32", 1): zr.FORMAT_R32_UINT, ("i32", 1): zr.FORMAT_R32_SINT,
+    ("f32", 2): zr.FORMAT_R32G32_SFLOAT, ("f32", 3): zr.FORMAT_R32G32B32_SFLOAT,
+    ("f32", 4): zr.FORMAT_R32G32B32A32_SFLOAT,
+    ("u32", 2): zr.FORMAT_R32G32_UINT, ("u32", 3): zr.FORMAT_R32G32B32_UINT, ("u32", 4): zr.FORMAT_R32G32B32A32_UINT,
+    ("i32", 2): zr.FORMAT_R32G32_SINT, ("i32", 3): zr.FORMAT_R32G32B32_SINT, ("i32", 4): zr.FORMAT_R32G32B32A32_SINT,
+}
+
+
 def vertex_layout(fields: Sequence[tuple]) -> tuple:
     """#[derive(VertexLayout)] (zenith-rhi-derive/src/lib.rs:61-140) for a repr(C)
-    struct of [f32; n] fields: location = field index, offset = running sum,
-    binding 0, stride = size_of, per-vertex rate."""
-    fmt = {1: zr.FORMAT_R32_SFLOAT, 2: zr.FORMAT_R32G32_SFLOAT, 3: zr.FORMAT_R32G32B32_SFLOAT,
-           4: zr.FORMAT_R32G32B32A32_SFLOAT}
+    struct of 4-byte scalar or [T; n] fields, T in f32/u32/i32 (lib.rs:175-231):
+    each field is ``(name, n)`` (f32) or ``(name, n, "u32" | "i32" | "f32")``, n = 1
+    for a scalar.  location = field index, offset = running sum, binding 0,
+    stride = size_of, per-vertex rate.  Types the derive rejects (other scalars,
+    arrays of 1 or more than 4) raise TypeError, as the derive fails to compile."""
     attrs, off = [], 0
-    for i, (_, n) in enumerate(fields):
-        attrs.append(VertexAttribute(i, 0, fmt[n], off))
+    for i, f in enumerate(fields):
+        n, kind = f[1], (f[2] if len(f) > 2 else "f32")
+        key = (kind, n) if n != 1 else (kind, 1)
+        if key not in _VERTEX_FORMATS:
+            raise TypeError(f"unsupported vertex field type for `{f[0]}`: {kind} x {n} "
+                            "(supported: f32/u32/i32 scalars and [T; 2..4])")
+        attrs.append(VertexAttribute(i, 0, _VERTEX_FORMATS[key], off))
         off += 4 * n
     return VertexBinding(0, off, 0), attrs
 
@@ -342,6 +360,7 @@ class GraphicShaderInput:
     fragment_shader: Optional[Shader]
     vertex_bindings: list
     vertex_attributes: list
+    push_constant_size: int = 0  # merged reflection's (pipeline.rs:78, :105)
 
 
 class GraphicShaderInputBuilder:
@@ -375,6 +394,9 @@ class GraphicShaderInputBuilder:
         """GraphicShaderInput::new (pipeline.rs:82-109): strict vertex-input
         validation, performed by the C ABI's pipeline validator."""
         inp = GraphicShaderInput(self._vs, self._fs, list(self._bindings), list(self._attrs))
+        # ShaderReflection::merge (shader.rs:224-228): the largest stage block
+        inp.push_constant_size = max([lib().zr_shader_push_constant_size(sh.handle)
+                                      for sh in (self._vs, self._fs) if sh is not None] + [0])
         dev_free_desc = _pipeline_desc(inp, GraphicPipelineState(), [], None)
         h = C.c_void_p()
         err = zr.zr_pipeline_error()
@@ -439,7 +461,8 @@ class GraphicPipelineState:
     color_attachments: list = dataclasses.field(default_factory=list)
 
 
-def _pipeline_desc(inp: GraphicShaderInput, state: GraphicPipelineState, color_formats, depth_format):
+def _pipeline_desc(inp: GraphicShaderInput, state: GraphicPipelineState, color_formats, depth_format,
+                   push_constant_ranges=None):
     nb, na = len(inp.vertex_bindings), len(inp.vertex_attributes)
     vbs = (zr.zr_vertex_binding * max(nb, 1))(*[zr.zr_vertex_binding(b.binding, b.stride, b.input_rate)
                                                  for b in inp.vertex_bindings])
@@ -470,6 +493,12 @@ def _pipeline_desc(inp: GraphicShaderInput, state: GraphicPipelineState, color_f
         nb, vbs, na, vas, state.topology, 0,
         zr.zr_rasterization_state(r.polygon_mode, r.cull_mode, r.front_face, 0, 0, 0.0, 0.0, 1.0),
         state.samples, ds_ptr, ncol, cols, fmts, depth_format or 0)
+    if push_constant_ranges:  # else derived from the reflection (pipeline.rs:112-128)
+        pcr = (zr.zr_push_constant_range * len(push_constant_ranges))(
+            *[zr.zr_push_constant_range(*r) for r in push_constant_ranges])
+        keep.append(pcr)
+        desc.push_constant_range_count = len(push_constant_ranges)
+        desc.push_constant_ranges = pcr
     return desc, keep
 
 
@@ -477,8 +506,12 @@ class GraphicPipeline:
     """CommonPipeline::new_graphic (pipeline.rs:931-1052) over zr_pipeline_create."""
 
     def __init__(self, device: Optional[RenderDevice], shader: GraphicShaderInput, state: GraphicPipelineState,
-                 color_formats: Sequence[int], depth_format: Optional[int]):
-        desc, self._keep = _pipeline_desc(shader, state, color_formats, depth_format)
+                 color_formats: Sequence[int], depth_format: Optional[int],
+                 push_constant_ranges: Optional[Sequence[tuple]] = None):
+        """``push_constant_ranges``: (stage_flags, offset, size) tuples of the
+        layout; None derives them from the shaders' reflection as
+        GraphicShaderInput::create_pipeline_layout does (pipeline.rs:112-128)."""
+        desc, self._keep = _pipeline_desc(shader, state, color_formats, depth_format, push_constant_ranges)
         h = C.c_void_p()
         err = zr.zr_pipeline_error()
         check(lib().zr_pipeline_create(device.handle if device else None, C.byref(desc), C.byref(h),
@@ -486,6 +519,17 @@ class GraphicPipeline:
         self.handle = h
         self.shader = shader
         self.state = state
+
+    def push_constant_ranges(self) -> list:
+        """The layout's vk::PushConstantRange list as (stage_flags, offset, size)."""
+        arr = (zr.zr_push_constant_range * 8)()
+        n = lib().zr_pipeline_push_constant_ranges(self.handle, arr, 8)
+        return [(arr[i].stage_flags, arr[i].offset, arr[i].size) for i in range(min(n, 8))]
+
+    def layout(self) -> "GraphicPipeline":
+        """CommonPipeline::layout: the pipeline stands in for its layout in
+        push_constants / bind_descriptor_sets."""
+        return self
 
     def destroy(self):
         lib().zr_pipeline_destroy(self.handle)
@@ -541,6 +585,14 @@ class CommandEncoder:
         hs = (C.c_void_p * n)(*[b.handle.value for b in buffers])
         offs = (C.c_uint64 * n)(*offsets)
         lib().zr_cmd_bind_vertex_buffers(self.handle, first_binding, n, hs, offs)
+
+    def push_constants(self, layout: "GraphicPipeline", stages: int, offset: int, data) -> None:
+        """CommandEncoder::push_constants (command.rs:180-185): the bytes of ``data``
+        (bytes, a numpy array or any buffer) are copied now, at ``offset`` of the
+        push-constant state; errors latch until end()/submit."""
+        b = bytes(memoryview(data).cast("B")) if not isinstance(data, (bytes, bytearray)) else bytes(data)
+        buf = (C.c_uint8 * max(len(b), 1)).from_buffer_copy(b or b"\0")
+        lib().zr_cmd_push_constants(self.handle, layout.handle, stages, offset, len(b), buf)
 
     def bind_index_buffer(self, buffer: Buffer, offset: int, index_type: int):
         lib().zr_cmd_bind_index_buffer(self.handle, buffer.handle, offset, index_type)

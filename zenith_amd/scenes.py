@@ -70,6 +70,7 @@ class Scene:
     vertex_offset: int = 0
     count: int | None = None                         # default: all indices / vertices
     view_proj: tuple | None = None                   # mesh program: View.view_proj, 16 floats column-major
+    push_view: bool = False                          # mesh program: view_proj as push constants (mesh_push.slang)
 
     @property
     def layout(self) -> tuple:

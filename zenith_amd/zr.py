@@ -45,7 +45,14 @@ FORMAT_R32G32_SFLOAT = 103
 FORMAT_R32G32B32_SFLOAT = 106
 FORMAT_R32G32B32A32_SFLOAT = 109
 FORMAT_D32_SFLOAT = 126
+# the derive's integer vertex formats (zenith-rhi-derive/src/lib.rs:175-231)
+FORMAT_R32_UINT, FORMAT_R32_SINT = 98, 99
+FORMAT_R32G32_UINT, FORMAT_R32G32_SINT = 101, 102
+FORMAT_R32G32B32_UINT, FORMAT_R32G32B32_SINT = 104, 105
+FORMAT_R32G32B32A32_UINT, FORMAT_R32G32B32A32_SINT = 107, 108
 SHADER_STAGE_VERTEX, SHADER_STAGE_FRAGMENT = 0x1, 0x10
+SHADER_STAGE_ALL_GRAPHICS = 0x1F
+MAX_PUSH_CONSTANTS_SIZE = 128
 DESCRIPTOR_TYPE_UNIFORM_BUFFER = 6
 INDEX_TYPE_UINT16, INDEX_TYPE_UINT32 = 0, 1
 LOAD_OP_LOAD, LOAD_OP_CLEAR, LOAD_OP_DONT_CARE = 0, 1, 2
@@ -127,6 +134,10 @@ class zr_rasterization_state(C.Structure):
                 ("depth_bias_constant", C.c_float), ("depth_bias_slope", C.c_float), ("line_width", C.c_float)]
 
 
+class zr_push_constant_range(C.Structure):
+    _fields_ = [("stage_flags", C.c_uint32), ("offset", C.c_uint32), ("size", C.c_uint32)]
+
+
 class zr_graphic_pipeline_desc(C.Structure):
     _fields_ = [("vertex_shader", C.c_void_p), ("fragment_shader", C.c_void_p),
                 ("vertex_binding_count", C.c_uint32), ("vertex_bindings", C.POINTER(zr_vertex_binding)),
@@ -136,7 +147,9 @@ class zr_graphic_pipeline_desc(C.Structure):
                 ("depth_stencil", C.POINTER(zr_depth_stencil_desc)),
                 ("color_attachment_count", C.c_uint32),
                 ("color_attachments", C.POINTER(zr_color_attachment_desc)),
-                ("color_formats", C.POINTER(C.c_int32)), ("depth_format", C.c_int32)]
+                ("color_formats", C.POINTER(C.c_int32)), ("depth_format", C.c_int32),
+                ("push_constant_range_count", C.c_uint32),
+                ("push_constant_ranges", C.POINTER(zr_push_constant_range))]
 
 
 class zr_pipeline_error(C.Structure):
@@ -197,9 +210,11 @@ _SIGS = {
     "zr_shader_destroy": (None, [_P]),
     "zr_shader_bindings": (C.c_int32, [_P, C.POINTER(zr_shader_binding), C.c_int32]),
     "zr_shader_vertex_inputs": (C.c_int32, [_P, C.POINTER(zr_vertex_input_attr), C.c_int32]),
+    "zr_shader_push_constant_size": (C.c_uint32, [_P]),
     "zr_pipeline_create": (_R, [_P, C.POINTER(zr_graphic_pipeline_desc), C.POINTER(_P),
                                 C.POINTER(zr_pipeline_error)]),
     "zr_pipeline_destroy": (None, [_P]),
+    "zr_pipeline_push_constant_ranges": (C.c_int32, [_P, C.POINTER(zr_push_constant_range), C.c_int32]),
     "zr_cmd_create": (_R, [_P, C.POINTER(_P)]),
     "zr_cmd_destroy": (None, [_P]),
     "zr_cmd_begin": (_R, [_P]),
@@ -209,6 +224,7 @@ _SIGS = {
     "zr_cmd_bind_pipeline": (None, [_P, _P]),
     "zr_cmd_bind_uniform_buffer": (None, [_P, C.c_uint32, C.c_uint32, _P, C.c_uint64, C.c_uint64]),
     "zr_cmd_bind_uniform_by_name": (_R, [_P, _P, C.c_char_p, _P, C.c_uint64, C.c_uint64]),
+    "zr_cmd_push_constants": (None, [_P, _P, C.c_uint32, C.c_uint32, C.c_uint32, _P]),
     "zr_cmd_set_viewport": (None, [_P, C.c_uint32, C.c_uint32, C.POINTER(zr_viewport)]),
     "zr_cmd_set_scissor": (None, [_P, C.c_uint32, C.c_uint32, C.POINTER(zr_rect2d)]),
     "zr_cmd_bind_vertex_buffers": (None, [_P, C.c_uint32, C.c_uint32, C.POINTER(_P), C.POINTER(C.c_uint64)]),
