@@ -70,18 +70,36 @@ def parse():
     return p.parse_args()
 
 
+SETUP_IN_BYTES = 12 + 3 * 12    # what k_setup_bin loads per triangle: 3 u32 indices + 3 float3 positions
+
+
+def winner_bytes(program, index_size=4):
+    """Bytes the resolve gathers per winning primitive: its vertex
+    ids, then the fragment program's attributes of its three vertices -- flat: the
+    provoking colour; triangle: 3 colours; Blinn-Phong: 3 x (normal + colour), 24
+    contiguous bytes per vertex; mesh: 3 x (normal + uv) plus the 48-B barycentric
+    planes setup stored."""
+    attrs = {scenes.PROGRAM_FLAT_COLOR: 12, scenes.PROGRAM_TRIANGLE: 36, scenes.PROGRAM_BLINN_PHONG: 72,
+             scenes.PROGRAM_MESH: 3 * 20 + 48}[program]
+    return 3 * index_size + attrs
+
+
 def algorithmic_bytes(kernel, n_tris, b_in, pairs, pixels, n_route=0):
     """Per-launch algorithmic bytes of each pass.
 
-    setup_bin: read index+vertex data once (b_in per triangle), write one 32-B
-               record per triangle and one 4-B bin entry per (tile, triangle) pair.
+    setup_bin: read what setup loads once (b_in per triangle: indices + positions,
+               SETUP_IN_BYTES; the interleaved vertex lines also carry the other
+               attributes, which the tile pass reads again for its winners),
+               write one 32-B record per triangle and one 4-B bin entry per
+               (tile, triangle) pair.
                With a partitioned setup n_tris is the rank's received records:
                read each 48-B route entry, write its 32-B record.
     route:     (partitioned setup) read indices + positions of the rank's range
                (12 + 3 * 12 B per triangle; the 48-B entries it writes are the
                receivers' reads).
     tile:      read each pair's bin entry + record once, write the colour + depth
-               texel of every owned pixel (4 + 4 B).
+               texel of every owned pixel (4 + 4 B).  (The winners' gathers are
+               added by design_tile_bytes.)
     """
     if kernel == "setup_bin":
         if n_route:
@@ -92,6 +110,13 @@ def algorithmic_bytes(kernel, n_tris, b_in, pairs, pixels, n_route=0):
     if kernel == "tile":
         return pairs * (BIN_ENTRY_BYTES + RECORD_BYTES) + pixels * 8
     return 0
+
+
+def design_tile_bytes(pairs, winners, per_winner, pixels):
+    """The tile pass's design bytes, by request class: pairs x (4-B bin entry +
+    32-B record) + winners x (vertex ids + attributes) + pixels x 8."""
+    return {"bins": pairs * BIN_ENTRY_BYTES, "records": pairs * RECORD_BYTES,
+            "winner_gathers": winners * per_winner, "stores": pixels * 8}
 
 
 def host_cpus():
@@ -521,10 +546,20 @@ def main():
     dev.set_profiling(False)
     kt = dev.kernel_times()
     stats = dev.last_draw_stats()
+    # winner census: one more (untimed) frame whose resolve marks each primitive
+    # that wins a pixel, for the tile pass's per-winner gather bytes
+    dev.set_profiling(True, census=True)
+    frame[0] = 0
+    step(1)
+    dev.wait_idle()
+    winners = dev.last_draw_stats()["winners"]
+    dev.set_profiling(False)
+    dev.kernel_times(reset=True)
     pairs = stats["bin_pairs"]
     pixels = int(shard.owned_rows(H, rank, shard_g).numel()) * W
     b_in = scenes.config_bytes_per_triangle(a.config)
     n_setup, n_route = N, 0
+    index_size = 4 if scene.index_type == scenes.INDEX_U32 else (2 if scene.index_type == scenes.INDEX_U16 else 0)
     if exchange is not None:  # this rank's range and the triangles it received
         lo, hi = shard.route_range(N, rank, shard_g)
         n_route = hi - lo
@@ -532,24 +567,31 @@ def main():
     kernels = {}
     for name, (ms, n) in kt.items():
         avg_us = ms * 1e3 / max(n, 1)
-        by = algorithmic_bytes(name, n_setup, b_in, pairs, pixels, n_route)
+        by = algorithmic_bytes(name, n_setup, SETUP_IN_BYTES, pairs, pixels, n_route)
         kernels[name] = {"avg_us": round(avg_us, 2), "launches": n, "alg_bytes": by,
                          "gbps": round(by / (avg_us * 1e-6) / 1e9, 1) if by and avg_us > 0 else None}
     launches = {k: v for k, v in kt.items() if k != "exchange"}  # "exchange": the all-to-all, not a kernel
     dom = max(launches, key=lambda k: launches[k][0]) if launches else "tile"
     dk = kernels.get(dom, {})
     traffic = None
+    traffic_classes = None
     if os.path.exists(a.pmc):  # measured on the warm pass's single copy, like `achieved`
         with open(a.pmc) as fh:
             pmc = json.load(fh)
         if pmc.get("config") == a.config and dom in pmc.get("kernels", {}):
             traffic = pmc["kernels"][dom]["hbm_bytes_per_launch"]
+            traffic_classes = pmc["kernels"][dom].get("classes")
     achieved = dk.get("gbps") or 0.0
     # SURVEY.md §8d's own fragment-pass figure (64-B records: 68 B per pair) beside
     # this design's minimum (32-B compact records: 36 B per pair)
     survey_bytes = pairs * SURVEY_PAIR_BYTES + pixels * 8
     tile_us = kernels.get("tile", {}).get("avg_us") or 0.0
     achieved_survey = round(survey_bytes / (tile_us * 1e-6) / 1e9, 1) if tile_us > 0 else None
+    # the design's own request classes (bins, records, winners' gathers, stores)
+    per_winner = winner_bytes(scene.program, index_size)
+    design = design_tile_bytes(pairs, winners, per_winner, pixels)
+    design_total = sum(design.values())
+    achieved_design = round(design_total / (tile_us * 1e-6) / 1e9, 1) if tile_us > 0 else None
 
     ms_per_step = elapsed / a.steps * 1e3
     value = N * a.steps / elapsed / 1e6
@@ -588,7 +630,11 @@ def main():
                      "alg_bytes_per_pair": BIN_ENTRY_BYTES + RECORD_BYTES,
                      "survey_bytes_per_pair": SURVEY_PAIR_BYTES,
                      "achieved_survey": achieved_survey,
-                     "frac_survey": round(achieved_survey / HBM_PEAK_GBPS, 4) if achieved_survey else None},
+                     "frac_survey": round(achieved_survey / HBM_PEAK_GBPS, 4) if achieved_survey else None,
+                     "design": {"bytes": design_total, "classes": design, "winners": winners,
+                                "bytes_per_winner": per_winner, "achieved": achieved_design,
+                                "frac": round(achieved_design / HBM_PEAK_GBPS, 4) if achieved_design else None},
+                     "traffic_classes": traffic_classes},
         "kernels": kernels,
         "bin_pairs": pairs,
         "triangles_setup": stats["triangles_setup"],

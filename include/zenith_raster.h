@@ -110,7 +110,10 @@ ZR_API zr_result zr_device_wait_idle(zr_device *dev);
  * the device first.  No reference counterpart (the reference has one queue). */
 ZR_API zr_result zr_device_set_stream(zr_device *dev, void *hip_stream);
 ZR_API void *zr_device_stream(const zr_device *dev);
-/* Per-kernel HIP-event timing of every draw (off by default). */
+/* Per-kernel HIP-event timing of every draw (off by default).  enable = 2 also
+ * takes a winner census of every draw (zr_draw_stats.winners): the resolve marks
+ * each primitive that wins a pixel in a bitmap -- extra atomics, so level 2 is
+ * for a separate untimed frame, never for the timing passes. */
 ZR_API zr_result zr_device_set_profiling(zr_device *dev, int32_t enable);
 /* Accumulated timings since the last reset: for each kernel name (setup_bin,
  * tile, clear) total ms and launch count.  Returns the number of
@@ -132,6 +135,10 @@ typedef struct zr_draw_stats {
      * and the draws (so far) whose received blocks overflowed
      * zr_cmd_set_route_capacity and were set up in full instead */
     uint64_t route_max_entries, route_fallback_draws;
+    /* distinct draw primitives that won at least one pixel in the last draw taken
+     * with zr_device_set_profiling(dev, 2) (0 otherwise): the resolve's per-winner
+     * gathers (vertex ids, attributes) are counted against it (bench.py) */
+    uint64_t winners;
 } zr_draw_stats;
 ZR_API zr_result zr_device_last_draw_stats(zr_device *dev, zr_draw_stats *out);
 /* Last error message recorded on this thread (for logging; never NULL). */

@@ -33,6 +33,20 @@ def test_algorithmic_bytes():
     assert bench.algorithmic_bytes("exchange", n, 120, pairs, px) == 0
     # C2's frame = 120 MB of input + 16.6 MB of colour + depth
     assert n * 120 + px * 8 == 136_588_800
+    # setup is credited with what it loads: 3 u32 indices + 3 float3 positions
+    assert bench.SETUP_IN_BYTES == 48
+
+
+def test_design_bytes_by_request_class():
+    import bench
+    from zenith_amd import scenes
+    # per winner: 12-B vertex ids + the program's attributes of its 3 vertices
+    assert bench.winner_bytes(scenes.PROGRAM_BLINN_PHONG) == 12 + 3 * 24
+    assert bench.winner_bytes(scenes.PROGRAM_FLAT_COLOR) == 12 + 12
+    assert bench.winner_bytes(scenes.PROGRAM_TRIANGLE, 2) == 6 + 36
+    assert bench.winner_bytes(scenes.PROGRAM_MESH) == 12 + 60 + 48
+    d = bench.design_tile_bytes(1_000, 300, 84, 2_000)
+    assert d == {"bins": 4_000, "records": 32_000, "winner_gathers": 25_200, "stores": 16_000}
 
 
 @pytest.mark.gpu
@@ -57,6 +71,9 @@ def test_bench_json_line():
     assert r["kernel"] in d["kernels"] and abs(r["frac"] - r["achieved"] / r["peak"]) < 1e-3
     assert r["survey_bytes_per_pair"] == 68 and r["achieved_survey"] > d["kernels"]["tile"]["gbps"]
     assert r["traffic"] is None  # the committed PMC summary is C2's, not C1's
+    dz = r["design"]  # winner census: distinct winners <= primitives, > 0 on a soup
+    assert 0 < dz["winners"] <= 100_000 and dz["bytes_per_winner"] == 24
+    assert dz["bytes"] == sum(dz["classes"].values()) and dz["achieved"] > r["achieved"]
     cb = d["cpu_baseline"]
     assert cb["kind"] == "port" and cb["cores"] >= 1 and cb["value"] > 0
     assert cb["nproc"] == cb["cores"] and cb["nproc_all"] >= cb["nproc"] and cb["cpu_model"]

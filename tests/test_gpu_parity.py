@@ -720,3 +720,27 @@ def test_depth_range_discard(device, program):
     s.vertices[:, 2] = z * np.float32(1.6) - np.float32(0.3)
     assert (s.vertices[:, 2] < 0).any() and (s.vertices[:, 2] > 1).any()
     assert_parity(device, s)
+
+
+@pytest.mark.parametrize("nt", [256, 512])
+def test_winner_census(monkeypatch, nt):
+    """zr_device_set_profiling(dev, 2): zr_draw_stats.winners counts the distinct
+    primitives that won a pixel (bench.py's per-winner bytes).  Each triangle's
+    provoking colour encodes its id in UNORM8, so the frame itself gives the
+    exact count; both resolve forms (256 / 512 threads) are checked."""
+    monkeypatch.setenv("ZR_TILE_NT", str(nt))
+    dev = rhi.RenderDevice(0)
+    try:
+        s = scenes.soup_scene(38, 3000, 256, 192, 10.0, scenes.PROGRAM_FLAT_COLOR)
+        ids = np.arange(1, 3001)
+        s.vertices[0::3, 3:6] = np.stack([ids & 255, (ids >> 8) & 255, (ids >> 16) & 255], 1).astype(np.float32) / 255
+        s.color_format, s.clear_color = zr.FORMAT_R8G8B8A8_UNORM, (0.0, 0.0, 0.0, 0.0)
+        dev.set_profiling(True, census=True)
+        gc, _ = assert_parity(dev, s)
+        dev.set_profiling(False)
+        got = gc[..., 0].astype(np.int64) + (gc[..., 1].astype(np.int64) << 8) + (gc[..., 2].astype(np.int64) << 16)
+        expected = len(np.unique(got[got > 0]))
+        assert 1000 < expected < 3000
+        assert dev.last_draw_stats()["winners"] == expected
+    finally:
+        dev.close()

@@ -59,6 +59,25 @@ def per_kernel_raw(path, counter):
     return {k: sum(v) / len(v) for k, v in out.items()}, None
 
 
+def tile_classes(paths, tile):
+    """The tile pass's read bytes per request class, from FETCH_SIZE passes of the
+    ZR_TILE_DEBUG variant: each ZR_DEBUG switch removes one class of reads
+    (pmc_classes.sh), so a class is the drop it causes; "lists_records" (the
+    raster's bin-list and record reads) is what remains above the no-raster pass.
+    Bytes per launch at the tile pass's fetch factor; stores are WRITE_SIZE."""
+    kib = [per_kernel(p, "FETCH_SIZE")[0].get("tile", 0.0) for p in paths]
+    dbg0, ids, attrs, recs, noraster = kib
+    f = tile["fetch_factor"] * 1024
+    c = {"winner_ids": max(dbg0 - ids, 0.0) * f, "winner_attributes": max(dbg0 - attrs, 0.0) * f,
+         "resolve_records": max(dbg0 - recs, 0.0) * f}
+    c["lists_records"] = max(dbg0 - noraster, 0.0) * f - sum(c.values())
+    c["rest"] = noraster * f
+    c = {k: int(v) for k, v in c.items()}
+    c["stores"] = int(tile["write_kib_per_launch"] * 1024 * tile["write_factor"])
+    c["debug_variant_fetch_kib"] = round(dbg0, 1)
+    return c
+
+
 def main():
     p = argparse.ArgumentParser()
     p.add_argument("--fetch", required=True)
@@ -66,6 +85,9 @@ def main():
     p.add_argument("--calib", nargs=2, metavar=("FETCH_CSV", "WRITE_CSV"))
     p.add_argument("--calib-known", help="JSON line printed by pmc_calib (bytes moved per kernel)")
     p.add_argument("--config", default="c2")
+    p.add_argument("--classes", nargs=5, metavar=("DBG0", "IDS", "ATTRS", "RECS", "NORASTER"),
+                   help="FETCH_SIZE csvs of the tile-debug variant (tools/pmc_classes.sh): the tile pass's "
+                        "reads split by request class")
     p.add_argument("-o", "--output", required=True)
     a = p.parse_args()
     fetch, nf = per_kernel(a.fetch, "FETCH_SIZE")
@@ -90,6 +112,8 @@ def main():
             "write_shape": WRITE_SHAPE[k], "write_factor": round(wfac, 3),
             "hbm_bytes_per_launch": int(fkb * 1024 * ff + wkb * 1024 * wfac),
         }
+    if a.classes and "tile" in out["kernels"]:
+        out["kernels"]["tile"]["classes"] = tile_classes(a.classes, out["kernels"]["tile"])
     with open(a.output, "w") as fh:
         json.dump(out, fh, indent=1)
     print(json.dumps(out))

@@ -227,6 +227,7 @@ struct DrawParams {
     uint32_t bbox_lds;        // 0: bboxes in global memory; else LDS entries per workgroup (own units * unit size)
     uint32_t debug;           // kDebug* bits (timing experiments only)
     unsigned long long* dbg_ts; // [setup_wgs][8] s_memrealtime stamps (kDebugStamps only)
+    uint32_t* win_bits;       // winner census (zr_device_set_profiling level 2): bit p = draw primitive p won a pixel
     uint32_t* status;         // host-mapped
     // push-constant state at the draw (zr_cmd_push_constants): the bytes ride in
     // the launch's kernel arguments, as Vulkan push constants ride in user SGPRs

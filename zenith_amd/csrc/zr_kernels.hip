@@ -1488,6 +1488,11 @@ __device__ __forceinline__ void resolve_pixels(const DrawParams& P, int x0, int 
             prim[b] = have[b] ? seq_record<PROG>(P, seq - 1u) : 0u;
             gp[b] = have[b] ? seq_prim<PROG>(seq - 1u) : 0u;
         }
+        if (P.win_bits) {  // winner census (profiling level 2 only; never in a timed pass)
+#pragma unroll
+            for (int b = 0; b < kB; ++b)
+                if (have[b]) atomicOr(&P.win_bits[gp[b] >> 5], 1u << (gp[b] & 31u));
+        }
         unsigned long long anyw = 0;
 #pragma unroll
         for (int b = 0; b < kB; ++b) anyw |= __ballot(have[b]);
@@ -1841,8 +1846,13 @@ __device__ __forceinline__ void resolve_tile(const DrawParams& P, int x0, int y0
     for (uint32_t base = 0; base < nwin; base += cap) {
         const uint32_t nb = min(cap, nwin - base);
         if (base) __syncthreads();  // the previous batch's pixels are done with s_win
-        for (uint32_t j = threadIdx.x; j < nb; j += NT)
+        for (uint32_t j = threadIdx.x; j < nb; j += NT) {
             fetch_winner<PROG, MODE, IDX32>(P, s_list[base + j], s_win + (size_t)j * L::kWords);
+            if (P.win_bits) {  // winner census (profiling level 2 only)
+                const uint32_t g = record_prim<PROG>(P, s_list[base + j]);
+                atomicOr(&P.win_bits[g >> 5], 1u << (g & 31u));
+            }
+        }
         __syncthreads();
         if (ts && !base) ts[6] = __builtin_amdgcn_s_memrealtime();  // first batch fetched
         auto shade_pixel = [&](int k, uint32_t dk) {

@@ -274,8 +274,12 @@ struct zr_device_t {
     hipEvent_t frame_done = nullptr;
     zr_draw_stats last{};
     uint64_t last_prims = 0;
-    // profiling
+    // profiling (zr_device_set_profiling): 1 = per-kernel events, 2 = also the winner census
     bool profiling = false;
+    int32_t census = 0;
+    uint32_t* win_bits = nullptr;   // census bitmap of the last census draw (one bit per draw primitive)
+    uint64_t win_bits_cap = 0;      // words
+    uint64_t census_words = 0;      // words of the last census draw, read at the next sync point
     bool use_graphs = false;    // ZR_GRAPH=1: replay resubmitted command lists as HIP graphs
     bool capturing = false;     // inside hipStreamBeginCapture: no allocation allowed
     uint64_t scratch_gen = 0;   // bumped whenever a scratch buffer is reallocated
@@ -484,6 +488,14 @@ zr_result device_sync(zr_device* d) {
         d->scratch_gen++;
     }
     d->last.bin_capacity = std::min<uint64_t>(d->sets[0].bins_cap, d->sets[1].bins ? d->sets[1].bins_cap : ~0ull);
+    if (d->census_words) {  // distinct primitives that won a pixel in the last census draw
+        std::vector<uint32_t> bits(d->census_words);
+        ZR_HIP(hipMemcpy(bits.data(), d->win_bits, bits.size() * 4, hipMemcpyDeviceToHost));
+        uint64_t n = 0;
+        for (uint32_t w : bits) n += (uint64_t)__builtin_popcount(w);
+        d->last.winners = n;
+        d->census_words = 0;
+    }
     return ZR_SUCCESS;
 }
 
@@ -819,6 +831,13 @@ zr_result exec_draw(zr_device* d, ExecState& s, const Cmd& c, bool indexed) {
                                      : tile_threads_for(P.ntiles, (uint32_t)std::max(d->cu_count, 1), prims, partitioned);
     P.rec_table = (d->rec_table < 0 ? use_record_table(prims, P.tiles_x, P.tiles_y) : d->rec_table != 0) ? 1u : 0u;
     P.debug = d->debug;
+    if (d->census && !d->capturing) {  // winner census: a bitmap over the draw's primitives, zeroed per draw
+        const uint64_t words = ((uint64_t)P.draw_prims + 31u) / 32u + 1u;
+        if ((rc = grow(d, d->win_bits, d->win_bits_cap, words, 4))) return rc;
+        ZR_HIP(hipMemsetAsync(d->win_bits, 0, words * 4, d->stream));
+        P.win_bits = d->win_bits;
+        d->census_words = words;
+    }
     if (d->debug & kDebugStamps) {
         if (!d->dbg_ts) ZR_HIP(hipMalloc((void**)&d->dbg_ts, (8192 + kMaxTilesPerPass) * 8 * sizeof(unsigned long long)));
         P.dbg_ts = d->dbg_ts;
@@ -1077,6 +1096,7 @@ ZR_API void zr_device_destroy(zr_device* d) {
     collect_timings(d);
     for (hipEvent_t e : d->event_pool) (void)hipEventDestroy(e);
     if (d->dbg_ts) (void)hipFree(d->dbg_ts);
+    if (d->win_bits) (void)hipFree(d->win_bits);
     for (ScratchSet& S : d->sets) {
         for (void* p : {(void*)S.records, (void*)S.records_big, (void*)S.mesh_edges, (void*)S.bboxes, (void*)S.tile_counts,
                         (void*)S.draw_info, (void*)S.counters, (void*)S.bins, (void*)S.xsend, (void*)S.xrecv,
@@ -1113,6 +1133,7 @@ ZR_API zr_result zr_device_wait_idle(zr_device* d) {
 ZR_API zr_result zr_device_set_profiling(zr_device* d, int32_t enable) {
     if (!d) return fail(ZR_ERROR_VALIDATION_FAILED, "device is NULL");
     d->profiling = enable != 0;
+    d->census = enable >= 2 ? 1 : 0;
     return ZR_SUCCESS;
 }
 

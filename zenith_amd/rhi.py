@@ -51,8 +51,11 @@ class RenderDevice:
     def wait_idle(self):
         check(lib().zr_device_wait_idle(self.handle), "zr_device_wait_idle")
 
-    def set_profiling(self, enable: bool):
-        check(lib().zr_device_set_profiling(self.handle, 1 if enable else 0), "zr_device_set_profiling")
+    def set_profiling(self, enable, census: bool = False):
+        """Per-kernel event timing; ``census`` also counts each draw's winning
+        primitives (last_draw_stats()["winners"]; extra atomics: untimed frames only)."""
+        level = (2 if census else 1) if enable else 0
+        check(lib().zr_device_set_profiling(self.handle, level), "zr_device_set_profiling")
 
     def kernel_times(self, reset: bool = False) -> dict:
         arr = (zr.zr_kernel_time * 32)()
