@@ -744,3 +744,31 @@ def test_winner_census(monkeypatch, nt):
         assert dev.last_draw_stats()["winners"] == expected
     finally:
         dev.close()
+
+
+@pytest.mark.parametrize("sched", [0, 1])
+def test_tile_schedule(monkeypatch, sched):
+    """k_tile's heaviest-first tile schedule (built by k_setup_bin's last workgroup
+    past phase 2; ZR_TILE_SCHED forces it on or off): exact on every program, a
+    tile-row shard, the spill path, partitioned records-mode setup and the mesh
+    program, at both workgroup sizes; a list order never changes the image."""
+    monkeypatch.setenv("ZR_TILE_SCHED", str(sched))
+    for nt in (256, 512):
+        monkeypatch.setenv("ZR_TILE_NT", str(nt))
+        dev = rhi.RenderDevice(0)
+        try:
+            for prog in (scenes.PROGRAM_TRIANGLE, scenes.PROGRAM_FLAT_COLOR, scenes.PROGRAM_BLINN_PHONG):
+                assert_parity(dev, scenes.soup_scene(90 + prog, 5000, 330, 250, 7.0, prog))
+            assert_parity(dev, scenes.soup_scene(93, 4000, 330, 250, 7.0, scenes.PROGRAM_BLINN_PHONG), shard=(1, 3))
+            assert_parity(dev, scenes.mesh_soup_scene(94, 3000, 320, 240))
+            assert_parity(dev, scenes.cerberus_scene(640, 480))
+        finally:
+            dev.close()
+    monkeypatch.setenv("ZR_BIN_CAPACITY", "1024")
+    dev = rhi.RenderDevice(0)
+    try:
+        assert_parity(dev, scenes.soup_scene(95, 4000, 320, 240, 12.0, scenes.PROGRAM_FLAT_COLOR))
+    finally:
+        dev.close()
+    monkeypatch.delenv("ZR_BIN_CAPACITY")
+    assert_partitioned_parity(scenes.soup_scene(96, 6000, 320, 240, 8.0, scenes.PROGRAM_BLINN_PHONG), 3)

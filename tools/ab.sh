@@ -12,6 +12,7 @@ for r in $(seq $R); do
     for v in $V; do
       # a variant is a build name, optionally with environment settings: name:VAR=1,VAR2=2
       lib=zenith_amd/variants/${v%%:*}/libzenith_raster.so
+      [ "${v%%:*}" = prod ] && lib=zenith_amd/lib/libzenith_raster.so  # the in-tree build
       envs=""; [ "$v" != "${v#*:}" ] && envs=$(echo "${v#*:}" | tr ',' ' ')
       env $envs ZR_LIB_PATH=$lib timeout -k 10 150 python bench.py --config $c --no-cpu-baseline --cold-copies 0 "$@" \
         > "$O/$(echo $v | tr ":=," "---")_${c}_$r.json" 2>> $O/err.log || { echo "FAIL $v $c $r"; exit 1; }

@@ -140,6 +140,7 @@ enum CounterWord : uint32_t {
     kCtSetup = 0, kCtDropped = 1,
     kCtMaxTile = 2,   // the largest tile list of the draw (pairs, including any past the slab)
     kCtPairs = 4,     // u64 (words 4-5): (tile, primitive) pairs of the draw
+    kCtSchedTicket = 6,  // k_setup_bin workgroups past phase 2 (the last one builds the tile schedule)
     kCtWords = 32,
 };
 // draw_info words (written by k_setup_bin for k_tile)
@@ -227,6 +228,7 @@ struct DrawParams {
     uint32_t bbox_lds;        // 0: bboxes in global memory; else LDS entries per workgroup (own units * unit size)
     uint32_t debug;           // kDebug* bits (timing experiments only)
     unsigned long long* dbg_ts; // [setup_wgs][8] s_memrealtime stamps (kDebugStamps only)
+    uint32_t* tile_order;     // tile schedule (k_setup_bin's last workgroup -> k_tile), or nullptr: xcd_tile order
     uint32_t* win_bits;       // winner census (zr_device_set_profiling level 2): bit p = draw primitive p won a pixel
     uint32_t* status;         // host-mapped
     // push-constant state at the draw (zr_cmd_push_constants): the bytes ride in
@@ -240,8 +242,10 @@ struct DrawParams {
 // primitives spread over more waves).  Measured on C2 shards (1 GPU, rank 0 of
 // G): G=4 tile pass 44 -> 39 us, G=8 40 -> 33 us; 16 waves per tile was slower
 // than 4 (61 / 43 us), so it is not built.
-// k_setup_bin LDS words besides the two tile arrays: misc (32) + list prefix (64).
-constexpr uint32_t kSetupMiscWords = 96;
+// k_setup_bin LDS words besides the two tile arrays: misc (32) + list prefix (64)
+// + the tile schedule's per-XCD bucket counts (8 x 64, the last workgroup only).
+constexpr uint32_t kSchedBuckets = 64;
+constexpr uint32_t kSetupMiscWords = 96 + 8 * kSchedBuckets;
 // A draw of fewer than 32 primitives per tile (cerberus at 1080p: 16) also gets 8
 // waves: its few heavy tiles (large triangles) end the pass alone on their CUs
 // (cerberus tile pass 124 -> 113 us; C1, 49 per tile, is 14% slower at 8 waves).
@@ -273,6 +277,19 @@ inline uint32_t tile_threads_for(uint32_t ntiles, uint32_t cus, uint64_t prims, 
 // per tile: 174.6 -> 181.8 us).
 inline bool use_record_table(uint64_t prims, uint32_t tiles_x, uint32_t tiles_y) {
     return prims >= 256ull * tiles_x * tiles_y;
+}
+
+// Whether k_setup_bin builds a heaviest-first tile schedule for k_tile
+// (build_tile_schedule): when the pass has more tiles than resident workgroup
+// slots (4 per CU at 512 threads, 8 at 256), so that dispatch order decides which
+// tiles end the pass, and the draw is sparse (< 32 primitives per tile), where a
+// few heavy tiles (a real mesh's dense parts) otherwise end the pass alone.  On
+// uniform soups the order gains nothing and the schedule costs setup its ticket
+// (round 4, ZR_TILE_SCHED A/B, 2 runs: cerberus frame 53.8 -> 51.0 us; C2 108.4
+// -> 113.7, C3 238.9 -> 245.0, C1 and C4 equal within 0.5 %).
+inline bool use_tile_schedule(uint32_t ntiles, uint32_t cus, uint32_t tile_threads, uint64_t prims) {
+    const uint64_t slots = (uint64_t)cus * (tile_threads >= 512u ? 4u : 8u);
+    return ntiles > slots && prims < 32ull * ntiles;
 }
 
 // Launchers (zr_kernels.hip).  All enqueue on `stream`; no host synchronisation.

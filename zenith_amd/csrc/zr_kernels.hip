@@ -824,6 +824,73 @@ __global__ __launch_bounds__(kRouteThreads) void k_route(DrawParams P) {
     }
 }
 
+// XCD-aware tile order.  Blocks are dealt round-robin over the 8 XCDs, so blocks b
+// and b + 8 share an XCD and its L2 (MI355X_MICROARCH.md; affinity only, nothing
+// depends on it).  Runs of ZR_XCD_TILES consecutive (row-major) tiles go to one
+// XCD, the runs round-robin over the XCDs: a primitive straddling two tiles of a
+// run has its record and vertices read through one L2, and a dense screen region
+// still spreads over every XCD.  A bijection: blocks past the last whole round of
+// runs keep their own tile.
+__device__ __forceinline__ uint32_t xcd_tile(uint32_t b, uint32_t n) {
+    constexpr uint32_t K = ZR_XCD_TILES;
+    if (K <= 1u || b >= n / (8u * K) * (8u * K)) return b;
+    const uint32_t x = b & 7u, l = b >> 3;
+    return ((l / K) * 8u + x) * K + l % K;
+}
+
+// The inverse of xcd_tile: the block that takes tile t in that order.
+__device__ __forceinline__ uint32_t xcd_block(uint32_t t, uint32_t n) {
+    constexpr uint32_t K = ZR_XCD_TILES;
+    if (K <= 1u || t >= n / (8u * K) * (8u * K)) return t;
+    const uint32_t R = t / K, o = t - R * K;
+    return ((R >> 3) * K + o) * 8u + (R & 7u);
+}
+
+// Tile schedule (longest-processing-time first): built by the last k_setup_bin
+// workgroup past phase 2, when every tile's count is final.  Each tile keeps the
+// XCD xcd_tile gives it (block % 8), but within an XCD the blocks take its tiles
+// heaviest list first, so the hardware, which dispatches blocks in order as slots
+// free up, starts the long tiles first and ends the pass on short ones (the
+// pass has ~2 tiles per wave slot at C2; without it its last ~15 us ran at 0.77
+// occupancy, docs/EXPERIMENTS.md).  Counting sort over kSchedBuckets weight
+// classes per XCD (s_sched: 8 x kSchedBuckets words of LDS).
+__device__ void build_tile_schedule(const DrawParams& P, uint32_t nt, uint32_t* s_sched) {
+    const uint32_t tid = threadIdx.x;
+    for (uint32_t i = tid; i < 8u * kSchedBuckets; i += kSetupThreads) s_sched[i] = 0u;
+    const uint32_t top = __hip_atomic_fetch_max(&P.counters[kCtMaxTile], 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    const uint32_t shift = top >= kSchedBuckets ? 32u - __clz(top / kSchedBuckets) : 0u;  // top >> shift < 64
+    __syncthreads();
+    auto key = [&](uint32_t t, uint32_t& x) {  // XCD and descending-weight bucket of tile t
+        const uint32_t c = __hip_atomic_fetch_add(&P.tile_counts[t], 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        x = xcd_block(t, nt) & 7u;
+        return kSchedBuckets - 1u - min(c >> shift, kSchedBuckets - 1u);
+    };
+    for (uint32_t t = tid; t < nt; t += kSetupThreads) {
+        uint32_t x;
+        const uint32_t k = key(t, x);
+        atomicAdd(&s_sched[x * kSchedBuckets + k], 1u);
+    }
+    __syncthreads();
+    if (tid < 8u * 64u) {  // one wave per XCD: exclusive scan of its 64 buckets
+        static_assert(kSchedBuckets == 64, "one lane per bucket");
+        const uint32_t c = s_sched[tid];
+        uint32_t inc = c;
+#pragma unroll
+        for (int d = 1; d < 64; d <<= 1) {
+            const uint32_t y = __shfl_up(inc, d, 64);
+            if ((int)(tid & 63u) >= d) inc += y;
+        }
+        s_sched[tid] = inc - c;
+    }
+    __syncthreads();
+    for (uint32_t t = tid; t < nt; t += kSetupThreads) {
+        uint32_t x;
+        const uint32_t k = key(t, x);
+        const uint32_t l = atomicAdd(&s_sched[x * kSchedBuckets + k], 1u);  // rank of t within its XCD
+        P.tile_order[l * 8u + x] = t;  // block l * 8 + x runs on XCD x (a bijection on [0, nt))
+    }
+}
+
 // ----------------------------------------------------------- k_setup_bin
 //
 // One launch, one 1024-thread workgroup per CU (fewer for small draws), no grid
@@ -864,6 +931,7 @@ __global__ __launch_bounds__(kSetupThreads) void k_setup_bin(DrawParams P) {
     uint32_t* s_hist = s_lds;                       // histogram -> cursors
     uint32_t* s_misc = s_hist + ((nt + 3u) & ~3u);  // [32]
     uint32_t* s_pre = s_misc + 32;       // records mode: exclusive prefix of the received blocks' counts
+    uint32_t* s_sched = s_misc + 96;     // [8 x kSchedBuckets] the tile schedule (last workgroup)
     // this workgroup's primitives' tile bboxes, indexed like phase 4's flattened
     // (own unit, primitive in unit) space, when they fit (P.bbox_lds)
     BBox* s_bbox = reinterpret_cast<BBox*>(s_misc + kSetupMiscWords);
@@ -1002,6 +1070,20 @@ __global__ __launch_bounds__(kSetupThreads) void k_setup_bin(DrawParams P) {
             if (s_misc[2]) atomicMax(&P.counters[kCtMaxTile], s_misc[2]);
             if (s_misc[3]) atomicAdd(reinterpret_cast<unsigned long long*>(&P.counters[kCtPairs]), (unsigned long long)s_misc[3]);
         }
+        if (P.tile_order) {
+            // The last workgroup to take a ticket sees every tile's final count: the
+            // counts and the max are only ever changed by atomics, which execute at
+            // the memory side, and every one of this workgroup's has completed before
+            // its ticket (returned, or drained by the wait below); the schedule reads
+            // them back with atomics too, so no L2 holds a stale copy in between.
+            asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+            __syncthreads();
+            if (tid == 0)
+                s_misc[5] = __hip_atomic_fetch_add(&P.counters[kCtSchedTicket], 1u, __ATOMIC_RELAXED,
+                                                   __HIP_MEMORY_SCOPE_AGENT);
+            __syncthreads();
+            if (s_misc[5] == G - 1u) build_tile_schedule(P, nt, s_sched);
+        }
     }
     ZR_STAMP(2);
     if (!P.bbox_lds || rec_mode) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // phase 4 reads global bboxes / gids
@@ -1091,20 +1173,6 @@ __device__ __forceinline__ void store_color(const DrawParams& P, int px, int py,
 }
 
 __device__ __forceinline__ int rl(int v, uint32_t lane) { return __builtin_amdgcn_readlane(v, lane); }
-
-// XCD-aware tile order.  Blocks are dealt round-robin over the 8 XCDs, so blocks b
-// and b + 8 share an XCD and its L2 (MI355X_MICROARCH.md; affinity only, nothing
-// depends on it).  Runs of ZR_XCD_TILES consecutive (row-major) tiles go to one
-// XCD, the runs round-robin over the XCDs: a primitive straddling two tiles of a
-// run has its record and vertices read through one L2, and a dense screen region
-// still spreads over every XCD.  A bijection: blocks past the last whole round of
-// runs keep their own tile.
-__device__ __forceinline__ uint32_t xcd_tile(uint32_t b, uint32_t n) {
-    constexpr uint32_t K = ZR_XCD_TILES;
-    if (K <= 1u || b >= n / (8u * K) * (8u * K)) return b;
-    const uint32_t x = b & 7u, l = b >> 3;
-    return ((l / K) * 8u + x) * K + l % K;
-}
 
 // Rasterize one primitive (wave-uniform record) into the tile's LDS keys: lanes
 // sweep the primitive's bbox ∩ tile, packed power-of-two rows per pass.
@@ -1921,7 +1989,7 @@ __global__ __launch_bounds__(NT, kTileWgs * kTileThreads / 256) void k_tile(Draw
     uint32_t* s_dbg = s_misc + 3;    // [2] kDebugStamps: lane-walk steps of the chunks, wave-path sweeps
     uint32_t* s_nwin = s_misc + 5;   // resolve: distinct winners of the tile
     const uint32_t b = (tile_debug(P) & kDebugReverseTiles) ? P.ntiles - 1u - blockIdx.x : blockIdx.x;
-    const uint32_t t = xcd_tile(b, P.ntiles);
+    const uint32_t t = P.tile_order ? P.tile_order[b] : xcd_tile(b, P.ntiles);
     const uint32_t oy = t / P.tiles_x, tx = t - oy * P.tiles_x;
     const uint32_t ty = oy * P.shard_count + P.shard_rank;
     const int x0 = (int)tx * kTile, y0 = (int)ty * kTile;

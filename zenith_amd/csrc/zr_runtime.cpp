@@ -208,6 +208,8 @@ struct ScratchSet {
     uint64_t counters_cap = 0;
     uint32_t* bins = nullptr;
     uint64_t bins_cap = 0;
+    uint32_t* tile_order = nullptr;  // k_tile's block -> tile schedule (k_setup_bin's last workgroup writes it)
+    uint64_t tile_order_cap = 0;
     uint8_t* xsend = nullptr;   // partitioned setup: exchange blocks (bytes)
     uint64_t xsend_cap = 0;
     uint8_t* xrecv = nullptr;
@@ -247,6 +249,7 @@ struct zr_device_t {
     // ZR_SETUP_OVERLAP=0 / 1 forces it off / on.
     int setup_overlap = -1;
     int rec_table = -1;        // ZR_REC_TABLE=0/1 forces k_tile's record table (A/B); -1: use_record_table
+    int tile_sched = -1;       // ZR_TILE_SCHED=0/1 forces the heaviest-first tile schedule (A/B); -1: use_tile_schedule
     int cu_count = 0;
     uint32_t occupancy_checked_tiles = 0;
     bool occupancy_checked_mesh = false;
@@ -830,6 +833,8 @@ zr_result exec_draw(zr_device* d, ExecState& s, const Cmd& c, bool indexed) {
     P.tile_threads = d->tile_threads ? d->tile_threads
                                      : tile_threads_for(P.ntiles, (uint32_t)std::max(d->cu_count, 1), prims, partitioned);
     P.rec_table = (d->rec_table < 0 ? use_record_table(prims, P.tiles_x, P.tiles_y) : d->rec_table != 0) ? 1u : 0u;
+    const bool sched = d->tile_sched < 0 ? use_tile_schedule(P.ntiles, (uint32_t)std::max(d->cu_count, 1), P.tile_threads, prims)
+                                         : d->tile_sched != 0;
     P.debug = d->debug;
     if (d->census && !d->capturing) {  // winner census: a bitmap over the draw's primitives, zeroed per draw
         const uint64_t words = ((uint64_t)P.draw_prims + 31u) / 32u + 1u;
@@ -851,6 +856,10 @@ zr_result exec_draw(zr_device* d, ExecState& s, const Cmd& c, bool indexed) {
     ScratchSet& S = d->sets[overlap ? d->cur_set : 0];
     if (overlap) d->cur_set ^= 1u;
     if ((rc = ensure_scratch(d, S, P))) return rc;
+    if (sched) {
+        if ((rc = grow(d, S.tile_order, S.tile_order_cap, P.ntiles, 4))) return rc;
+        P.tile_order = S.tile_order;
+    }
     d->last_prims = prims;
     d->last.triangles_in = prims;
 
@@ -1063,6 +1072,7 @@ ZR_API zr_result zr_device_create(int32_t hip_device, zr_device** out) {
     if (const char* g = getenv("ZR_GRAPH")) d->use_graphs = strtoul(g, nullptr, 0) != 0;
     if (const char* o = getenv("ZR_SETUP_OVERLAP")) d->setup_overlap = strtoul(o, nullptr, 0) != 0 ? 1 : 0;
     if (const char* rt = getenv("ZR_REC_TABLE")) d->rec_table = strtoul(rt, nullptr, 0) != 0 ? 1 : 0;
+    if (const char* ts = getenv("ZR_TILE_SCHED")) d->tile_sched = strtoul(ts, nullptr, 0) != 0 ? 1 : 0;
     if (const char* nt = getenv("ZR_TILE_NT")) {
         const unsigned long v = strtoul(nt, nullptr, 0);
         d->tile_threads = v >= 512 ? 512u : v ? 256u : 0u;
@@ -1100,7 +1110,7 @@ ZR_API void zr_device_destroy(zr_device* d) {
     for (ScratchSet& S : d->sets) {
         for (void* p : {(void*)S.records, (void*)S.records_big, (void*)S.mesh_edges, (void*)S.bboxes, (void*)S.tile_counts,
                         (void*)S.draw_info, (void*)S.counters, (void*)S.bins, (void*)S.xsend, (void*)S.xrecv,
-                        (void*)S.gids})
+                        (void*)S.gids, (void*)S.tile_order})
             if (p) (void)hipFree(p);
         if (S.setup_done) (void)hipEventDestroy(S.setup_done);
         if (S.tile_done) (void)hipEventDestroy(S.tile_done);
