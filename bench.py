@@ -268,16 +268,16 @@ def emulate(a, scene, cuda):
         tr = timed(enc)
         kt = kernels(enc)
         st = dev.last_draw_stats()
-        pixels = int(shard.owned_rows(H, r, G).numel()) * W
+        pixels = shard.owned_pixels(W, H, r, G)
         ranks.append({"rank": r, "ms": round(tr * 1e3, 4), "kernels_us": kt, "bin_pairs": st["bin_pairs"],
                       "triangles_setup": st["triangles_setup"], "pixels": pixels,
                       "route_fallback_draws": st["route_fallback_draws"]})
         enc.destroy()
     worst = max(ranks, key=lambda x: x["ms"])
-    # the row gather, modelled: the largest peer's rows into rank 0
+    # the tile gather, modelled: the largest peer's pixels into rank 0
     # over one xGMI link at ~153 GB/s, overlapped with the next frame
-    peer_rows = max((int(shard.owned_rows(H, r, G).numel()) for r in range(1, G)), default=0)
-    gather_us = peer_rows * W * 4 / 153e9 * 1e6
+    peer_px = max((shard.owned_pixels(W, H, r, G) for r in range(1, G)), default=0)
+    gather_us = peer_px * 4 / 153e9 * 1e6
     b_in = scenes.config_bytes_per_triangle(a.config)
     n_route = shard.route_range(N, worst["rank"], G)
     rank_bytes = (((n_route[1] - n_route[0]) * b_in + worst["triangles_setup"] * shard.ENTRY_BYTES) if part
@@ -456,7 +456,7 @@ def main():
     sh = (rank, shard_g, exchange, cap) if exchange is not None else ((rank, shard_g) if shard_g > 1 else None)
     # encs[copy][target]: frame f draws geometry copy f % K into target f % nbuf
     encs = [[r.record(c, depth, shard=sh, encoder=rhi.CommandEncoder(dev)) for c in colors] for r in rs]
-    gather = shard.TileRowGather(H, W * 4, rank, world, cuda) if distributed and not runtime_comm else None
+    gather = shard.TileGather(W, H, 4, rank, world, cuda) if distributed and not runtime_comm else None
     # Multi-GPU: torch's current stream is the runtime's main stream, so frames,
     # exchanges and gathers are ordered by streams and events, never a host wait.
     main_stream = torch.cuda.ExternalStream(dev.stream, device=cuda)
@@ -556,7 +556,7 @@ def main():
     dev.set_profiling(False)
     dev.kernel_times(reset=True)
     pairs = stats["bin_pairs"]
-    pixels = int(shard.owned_rows(H, rank, shard_g).numel()) * W
+    pixels = shard.owned_pixels(W, H, rank, shard_g)
     b_in = scenes.config_bytes_per_triangle(a.config)
     n_setup, n_route = N, 0
     index_size = 4 if scene.index_type == scenes.INDEX_U32 else (2 if scene.index_type == scenes.INDEX_U16 else 0)

@@ -384,7 +384,12 @@ ZR_API void zr_cmd_draw(zr_cmd *cmd, uint32_t vertex_count, uint32_t instance_co
 ZR_API void zr_cmd_draw_indexed(zr_cmd *cmd, uint32_t index_count, uint32_t instance_count, uint32_t first_index,
                                 int32_t vertex_offset, uint32_t first_instance);
 /* Multi-GPU extension (no reference counterpart): subsequent
- * render passes touch only screen-tile rows r with r % count == rank. */
+ * render passes touch only the 32x32 screen tiles this rank owns.  Ownership
+ * (DESIGN.md §7): of a target's tiles_y tile rows, the first F = floor(tiles_y /
+ * count) * count go round robin (row ty to rank ty % count); the n tiles of the
+ * remaining rows (row-major) are cut into count runs, rank r owning tiles
+ * [ceil(r n / count), ceil((r + 1) n / count)), so every rank owns the floor or
+ * ceiling of tiles / count. */
 ZR_API void zr_cmd_set_tile_shard(zr_cmd *cmd, uint32_t rank, uint32_t count);
 /* Partitioned tile-row shards: as zr_cmd_set_tile_shard, but each
  * draw's primitive setup is split across the ranks too.  Rank r sets up only its
@@ -428,19 +433,24 @@ ZR_API zr_result zr_device_init_rccl(zr_device *dev, const void *exchange_id, co
 ZR_API zr_exchange_fn zr_rccl_exchange_fn(void);
 ZR_API zr_result zr_device_gather_tile_rows(zr_device *dev, zr_texture *tex, int32_t root);
 /* The point-to-point transfers the two collectives enqueue on this rank (host
- * only, no device): zr_device_gather_tile_rows of a `height`-row image with
- * `row_bytes` per row, and the built-in exchange's grouped send/recv pairing.
- * Each op moves `bytes` at byte `offset` of the image (gather: the same offset on
- * both sides) or of the send / receive buffer (exchange) to or from `peer`.
- * Returns the number of ops (at most `capacity` written; out may be NULL), or -1
- * for bad ranks. */
+ * only, no device): zr_device_gather_tile_rows of a width x height image of
+ * `bytes_per_pixel`, and the built-in exchange's grouped send/recv pairing.  Each
+ * op moves `rows` spans of `bytes` (`pitch` apart; rows == 1: one contiguous
+ * span) at byte `offset` of the image (gather: the same offset on both sides; a
+ * rectangle travels packed through a staging buffer) or of the send / receive
+ * buffer (exchange) to or from `peer`.  Returns the number of ops (at most
+ * `capacity` written; out may be NULL), or -1 for bad ranks or extents.
+ * Ownership (zr_cmd_set_tile_shard): the round-robin tile rows are whole-row
+ * spans; a leftover row yields one op per owner of a run of its tiles. */
 typedef struct zr_transfer_op {
     int32_t peer;
     int32_t send; /* 1 = send to peer, 0 = receive from peer */
     uint64_t offset, bytes;
+    uint32_t rows, reserved;
+    uint64_t pitch;
 } zr_transfer_op;
-ZR_API int32_t zr_gather_plan(uint32_t height, uint64_t row_bytes, int32_t nranks, int32_t rank, int32_t root,
-                              zr_transfer_op *out, int32_t capacity);
+ZR_API int32_t zr_gather_plan(uint32_t width, uint32_t height, uint32_t bytes_per_pixel, int32_t nranks, int32_t rank,
+                              int32_t root, zr_transfer_op *out, int32_t capacity);
 ZR_API int32_t zr_exchange_plan(int32_t nranks, int32_t rank, uint64_t bytes_per_rank, zr_transfer_op *out,
                                 int32_t capacity);
 

@@ -134,9 +134,33 @@ static void store_color(const zro_target *t, uint32_t x, uint32_t y, const float
 
 /* ------------------------------------------------------------------ clear */
 
-static int row_owned(uint32_t y, uint32_t tile, uint32_t rank, uint32_t count) {
-    if (count <= 1) return 1;
-    return ((y / tile) % count) == rank;
+/* Shard ownership (this repo's multi-GPU split; no reference
+ * counterpart): the pixel columns [*x0, *x1) of tile row ty (tile x tile tiles)
+ * that rank `rank` of `count` owns on a width x height target.  The first F =
+ * floor(rows / count) * count tile rows go round robin (row ty to rank ty %
+ * count); the tiles of the rows after them, row-major, are cut into count
+ * consecutive runs, run r = [ceil(r n / count), ceil((r + 1) n / count)) of their
+ * n tiles.  An empty range when the rank owns none of the row. */
+static void owned_cols(uint32_t ty, uint32_t width, uint32_t height, uint32_t tile, uint32_t rank, uint32_t count,
+                       int32_t *x0, int32_t *x1) {
+    *x0 = 0;
+    *x1 = (int32_t)width;
+    if (count <= 1) return;
+    const uint64_t tiles_x = (width + tile - 1) / tile, rows = (height + tile - 1) / tile;
+    const uint64_t full = rows / count * count;
+    if (ty < full) {
+        if (ty % count != rank) *x1 = 0;
+        return;
+    }
+    const uint64_t n = (rows - full) * tiles_x;
+    const uint64_t lo = (rank * n + count - 1) / count, hi = ((rank + 1) * n + count - 1) / count;
+    const int64_t i0 = (int64_t)((ty - full) * tiles_x);
+    int64_t c0 = (int64_t)lo - i0, c1 = (int64_t)hi - i0; /* tiles [c0, c1) of this row */
+    if (c0 < 0) c0 = 0;
+    if (c1 > (int64_t)tiles_x) c1 = (int64_t)tiles_x;
+    if (c0 >= c1) { *x1 = 0; return; }
+    *x0 = (int32_t)(c0 * tile);
+    *x1 = (int32_t)(c1 * tile < (int64_t)width ? c1 * tile : (int64_t)width);
 }
 
 void zro_clear(const zro_target *t, const int32_t ra[4], const float cc[4], int clear_colour,
@@ -146,8 +170,9 @@ void zro_clear(const zro_target *t, const int32_t ra[4], const float cc[4], int 
     if (x1 > (int32_t)t->width) x1 = (int32_t)t->width;
     if (y1 > (int32_t)t->height) y1 = (int32_t)t->height;
     for (int32_t y = y0; y < y1; ++y) {
-        if (!row_owned((uint32_t)y, tile, rank, count)) continue;
-        for (int32_t x = x0; x < x1; ++x) {
+        int32_t ox0, ox1;
+        owned_cols((uint32_t)y / tile, t->width, t->height, tile, rank, count, &ox0, &ox1);
+        for (int32_t x = x0 > ox0 ? x0 : ox0; x < x1 && x < ox1; ++x) {
             if (clear_colour && t->color) store_color(t, (uint32_t)x, (uint32_t)y, cc, 0xF);
             if (clear_depth && t->depth) t->depth[(size_t)y * t->width + x] = cd;
         }
@@ -499,10 +524,12 @@ static void shade(const zro_draw_state *s, const zro_vertex_input *vi, const tri
     blinn_phong(n, kd, out);
 }
 
-/* Rasterize one set-up triangle over rows [ry0, ry1] (inclusive), in order. */
+/* Rasterize one set-up triangle over rows [ry0, ry1] (inclusive) and columns
+ * [cx0, cx1) (the band's owned pixels), in order. */
 static void raster_rows(const zro_target *t, const zro_draw_state *s, const zro_vertex_input *vi,
-                        const tri_setup *o, int32_t ry0, int32_t ry1, zro_stats *st) {
+                        const tri_setup *o, int32_t ry0, int32_t ry1, int32_t cx0, int32_t cx1, zro_stats *st) {
     int32_t y0 = o->py0 > ry0 ? o->py0 : ry0, y1 = o->py1 < ry1 ? o->py1 : ry1;
+    const int32_t x0 = o->px0 > cx0 ? o->px0 : cx0, x1 = o->px1 < cx1 - 1 ? o->px1 : cx1 - 1;
     const int32_t dx0 = o->X[2] - o->X[1], dy0 = o->Y[2] - o->Y[1];
     const int32_t dx1 = o->X[0] - o->X[2], dy1 = o->Y[0] - o->Y[2];
     const int32_t dx2 = o->X[1] - o->X[0], dy2 = o->Y[1] - o->Y[0];
@@ -515,9 +542,8 @@ static void raster_rows(const zro_target *t, const zro_draw_state *s, const zro_
     const float dhi = s->viewport[4] < s->viewport[5] ? s->viewport[5] : s->viewport[4];
     const int test = s->depth_test && t->depth;
     for (int32_t py = y0; py <= y1; ++py) {
-        if (!row_owned((uint32_t)py, s->tile_size, s->shard_rank, s->shard_count)) continue;
         const int64_t Sy = (int64_t)py * 256 + 128;
-        for (int32_t px = o->px0; px <= o->px1; ++px) {
+        for (int32_t px = x0; px <= x1; ++px) {
             const int64_t Sx = (int64_t)px * 256 + 128;
             const int64_t w0 = (int64_t)dx0 * (Sy - o->Y[1]) - (int64_t)dy0 * (Sx - o->X[1]);
             const int64_t w1 = (int64_t)dx1 * (Sy - o->Y[2]) - (int64_t)dy1 * (Sx - o->X[2]);
@@ -578,11 +604,13 @@ int zro_draw(const zro_target *t, const zro_draw_state *s, const zro_vertex_inpu
             zro_stats ls;
             memset(&ls, 0, sizeof ls);
             const int32_t ry0 = b * band, ry1 = b * band + band - 1;
-            if (!row_owned((uint32_t)ry0, s->tile_size, s->shard_rank, s->shard_count)) continue;
+            int32_t cx0, cx1;
+            owned_cols((uint32_t)b, t->width, t->height, s->tile_size, s->shard_rank, s->shard_count, &cx0, &cx1);
+            if (cx0 >= cx1) continue;
             for (int64_t i = 0; i < 3 * n; ++i) { /* in API order; a primitive's fan triangles do not overlap */
                 const tri_setup *o = &buf[i];
-                if (!o->valid || o->py1 < ry0 || o->py0 > ry1) continue;
-                raster_rows(t, s, vi, o, ry0, ry1, &ls);
+                if (!o->valid || o->py1 < ry0 || o->py0 > ry1 || o->px1 < cx0 || o->px0 >= cx1) continue;
+                raster_rows(t, s, vi, o, ry0, ry1, cx0, cx1, &ls);
             }
             fc += ls.fragments_covered;
             fp += ls.fragments_passed;

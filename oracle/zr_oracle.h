@@ -70,8 +70,8 @@ typedef struct zro_draw_state {
     uint32_t depth_test, depth_write;
     int32_t depth_op;          /* VkCompareOp                                        */
     uint32_t color_write_mask; /* VkColorComponentFlags                              */
-    uint32_t tile_size;        /* screen-tile edge (rows are sharded in tile rows)    */
-    uint32_t shard_rank, shard_count; /* tile row r is drawn iff r % count == rank  */
+    uint32_t tile_size;        /* screen-tile edge (shards own whole tiles)           */
+    uint32_t shard_rank, shard_count; /* only this rank's tiles are drawn (zr_oracle.c owned_cols) */
     float view_proj[16];       /* mesh program: View.view_proj, column-major (glam)   */
 } zro_draw_state;
 

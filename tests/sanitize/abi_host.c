@@ -158,10 +158,10 @@ int main(void) {
     zr_transfer_op ops[80];
     for (int32_t g = 1; g <= 8; ++g)
         for (int32_t r = 0; r < g; ++r) {
-            const int32_t n = zr_gather_plan(1080, 7680, g, r, 0, ops, 80);
-            EXPECT(n >= 0 && n <= 80 && zr_gather_plan(1080, 7680, g, r, 0, NULL, 0) == n);
+            const int32_t n = zr_gather_plan(1920, 1080, 4, g, r, 0, ops, 80);
+            EXPECT(n >= 0 && n <= 80 && zr_gather_plan(1920, 1080, 4, g, r, 0, NULL, 0) == n);
             EXPECT(zr_exchange_plan(g, r, 16 + 48 * 100, ops, 80) == 2 * g);
-            EXPECT(zr_gather_plan(1080, 7680, g, r, 0, ops, 1) == n); /* capacity 1: count only past it */
+            EXPECT(zr_gather_plan(1920, 1080, 4, g, r, 0, ops, 1) == n); /* capacity 1: count only past it */
         }
     EXPECT(zr_exchange_plan(33, 0, 64, ops, 80) == -1);
 

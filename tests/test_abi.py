@@ -166,42 +166,63 @@ def _plan(fn, *args):
     assert n >= 0
     ops = (zr.zr_transfer_op * max(n, 1))()
     assert fn(*args, ops, n) == n
-    return [(o.peer, o.send, o.offset, o.bytes) for o in ops[:n]]
+    return [(o.peer, o.send, o.offset, o.bytes, o.rows, o.pitch) for o in ops[:n]]
 
 
-@pytest.mark.parametrize("height", [1080, 2160, 120, 40, 33, 1])
+@pytest.mark.parametrize("w,h", [(1920, 1080), (3840, 2160), (320, 120), (100, 40), (33, 33), (70, 1)])
 @pytest.mark.parametrize("world", [2, 3, 4, 5, 8])
 @pytest.mark.parametrize("root", [0, 1])
-def test_gather_plan_covers_every_row_once(height, world, root):
-    """zr_device_gather_tile_rows' plan (zr_gather_plan) against shard.owned_rows:
-    the root receives every row it does not own exactly once, from that row's
-    owner, into the row's own place; each peer sends exactly its own rows to the
-    root; the root's rows never move; a partial last tile row moves only its rows."""
+def test_gather_plan_covers_every_pixel_once(w, h, world, root):
+    """zr_device_gather_tile_rows' plan (zr_gather_plan) against shard.owned_mask:
+    the root receives every pixel it does not own exactly once, from that pixel's
+    owner, into its own place; each peer sends exactly its own pixels; the root's
+    pixels never move; round-robin tile rows travel as whole-row spans, a
+    leftover row's tile runs as rectangles (rows spans, pitch = the image row)."""
     from zenith_amd import shard
     root = root % world
-    row_bytes = 7680
+    bpp = 4
+    row_bytes = w * bpp
     lib = zr.lib()
-    want = {r: set(shard.owned_rows(height, r, world).tolist()) for r in range(world)}
-    recv = _plan(lib.zr_gather_plan, height, row_bytes, world, root, root)
-    got_rows = {}
-    for peer, send, off, nbytes in recv:
+
+    def ops_of(r):
+        n = lib.zr_gather_plan(w, h, bpp, world, r, root, None, 0)
+        assert n >= 0
+        arr = (zr.zr_transfer_op * max(n, 1))()
+        assert lib.zr_gather_plan(w, h, bpp, world, r, root, arr, n) == n
+        return [(o.peer, o.send, o.offset, o.bytes, o.rows, o.pitch) for o in arr[:n]]
+
+    def pixels(off, nbytes, rows, pitch):
+        assert off % bpp == 0 and nbytes % bpp == 0 and nbytes > 0 and rows >= 1
+        starts = off + np.arange(rows, dtype=np.int64) * pitch
+        if rows > 1:  # each rectangle row stays inside one image row
+            assert ((starts // row_bytes) == ((starts + nbytes - 1) // row_bytes)).all()
+        return ((starts // bpp)[:, None] + np.arange(nbytes // bpp)[None, :]).reshape(-1)
+
+    owner = np.full(h * w, -1)
+    for r in range(world):
+        owner[shard.owned_mask(w, h, r, world).reshape(-1)] = r
+    got = np.zeros(h * w, dtype=np.int64)
+    src = np.full(h * w, -1)
+    recv = ops_of(root)
+    for peer, send, off, nb, rows, pitch in recv:
         assert send == 0 and peer != root
-        assert off % row_bytes == 0 and nbytes % row_bytes == 0 and nbytes > 0
-        for y in range(off // row_bytes, (off + nbytes) // row_bytes):
-            assert y not in got_rows, f"row {y} received twice"
-            got_rows[y] = peer
-    assert set(got_rows) == set(range(height)) - want[root]
-    assert all(y in want[p] for y, p in got_rows.items())
+        assert rows == 1 or pitch == row_bytes
+        px = pixels(off, nb, rows, pitch)
+        got[px] += 1
+        src[px] = peer
+    assert (got[owner != root] == 1).all() and (got[owner == root] == 0).all(), "a pixel missed or received twice"
+    assert np.array_equal(src[owner != root], owner[owner != root])
     sent = []
     for r in range(world):
-        ops = _plan(lib.zr_gather_plan, height, row_bytes, world, r, root)
         if r == root:
             continue
-        assert all(send == 1 and peer == root for peer, send, _, _ in ops)
-        rows = {y for _, _, off, nb in ops for y in range(off // row_bytes, (off + nb) // row_bytes)}
-        assert rows == want[r]
-        sent += [(r, off, nb) for _, _, off, nb in ops]
-    assert sorted(sent) == sorted((p, off, nb) for p, _, off, nb in recv)  # every send has its receive
+        ops = ops_of(r)
+        assert all(send == 1 and peer == root for peer, send, *_ in ops)
+        px = np.sort(np.concatenate([pixels(off, nb, rows, pitch) for _, _, off, nb, rows, pitch in ops])) \
+            if ops else np.zeros(0, np.int64)
+        assert np.array_equal(px, np.flatnonzero(owner == r))
+        sent += [(r, off, nb, rows, pitch) for _, _, off, nb, rows, pitch in ops]
+    assert sorted(sent) == sorted((p, off, nb, rows, pitch) for p, _, off, nb, rows, pitch in recv)
 
 
 @pytest.mark.parametrize("world", [1, 2, 3, 8, 32])
@@ -213,10 +234,11 @@ def test_exchange_plan_pairs_every_peer(world):
     bpr = 16 + 48 * 1000
     for r in range(world):
         ops = _plan(lib.zr_exchange_plan, world, r, bpr)
-        assert sorted((p, s) for p, s, _, _ in ops) == sorted((p, s) for p in range(world) for s in (0, 1))
-        assert all(off == p * bpr and nb == bpr for p, _, off, nb in ops)
+        assert sorted((p, s) for p, s, *_ in ops) == sorted((p, s) for p in range(world) for s in (0, 1))
+        assert all(off == p * bpr and nb == bpr for p, _, off, nb, *_ in ops)
     assert lib.zr_exchange_plan(33, 0, bpr, None, 0) == -1
-    assert lib.zr_gather_plan(1080, 7680, 2, 2, 0, None, 0) == -1
+    assert lib.zr_gather_plan(1920, 1080, 4, 2, 2, 0, None, 0) == -1
+    assert lib.zr_gather_plan(0, 1080, 4, 2, 0, 0, None, 0) == -1
 
 
 # ------------------------------------------------- push constants (host only)

@@ -1,7 +1,8 @@
 """Multi-rank tile-row sharding + gather over gloo, world_size 2/3.
 
-Each rank renders only the tile rows it owns (row % G == rank) and
-TileRowGather assembles the frame on rank 0; the result must equal a
+Each rank renders only the tiles it owns (shard.tile_owner: round-robin tile
+rows, the leftover rows cut into one run of tiles per rank) and TileGather
+assembles the frame on rank 0; the result must equal a
 single-rank render of the whole frame.  The CPU test renders the shards with
 the oracle (this container has no GPU); the gpu-marked test renders them with
 the HIP path, every rank on cuda:0, and gathers host tensors over gloo.
@@ -40,7 +41,7 @@ def _worker(rank, world, port, use_gpu, out_path):
         from oracle import oracle
         color, _ = oracle.render(s, shard=(rank, world))
     img = torch.from_numpy(np.ascontiguousarray(color).reshape(s.height, -1))
-    g = shard.TileRowGather(s.height, img.shape[1], rank, world, torch.device("cpu"))
+    g = shard.TileGather(s.width, s.height, 4, rank, world, torch.device("cpu"))
     g.gather(img)
     if rank == 0:
         np.save(out_path, img.numpy())
@@ -68,11 +69,23 @@ def test_gloo_shard_gather_oracle(world, tmp_path):
     assert np.array_equal(got, _full_frame())
 
 
-def test_owned_rows_partition():
+@pytest.mark.parametrize("w,h", [(1920, 1080), (3840, 2160), (320, 256), (160, 120), (33, 1)])
+def test_owned_tiles_partition(w, h):
+    """Every pixel belongs to exactly one rank, and the tile counts differ by at
+    most one between ranks (C2 at 8 ranks: 255 tiles each; round-robin rows alone
+    gave 5 or 4 rows of 60)."""
     from zenith_amd import shard
-    for world in (1, 2, 3, 8):
-        rows = torch.cat([shard.owned_rows(1080, r, world) for r in range(world)])
-        assert sorted(rows.tolist()) == list(range(1080))
+    tx, ty = -(-w // 32), -(-h // 32)
+    for world in (1, 2, 3, 5, 8, 32):
+        masks = [shard.owned_mask(w, h, r, world) for r in range(world)]
+        assert np.array_equal(sum(m.astype(np.int64) for m in masks), np.ones((h, w), np.int64))
+        own = shard.tile_owner(tx, ty, world)
+        counts = np.bincount(own.reshape(-1), minlength=world)
+        assert counts.max() - counts.min() <= 1
+        full = (ty // world) * world
+        assert np.array_equal(own[:full], np.broadcast_to((np.arange(full) % world)[:, None], (full, tx)))
+    assert list(np.bincount(shard.tile_owner(60, 34, 8).reshape(-1))) == [255] * 8
+    assert list(np.bincount(shard.tile_owner(120, 68, 8).reshape(-1))) == [1020] * 8
 
 
 @pytest.mark.gpu
@@ -92,7 +105,9 @@ def _spans(n, seed=5):
 
 
 def _expected(lo, hi, rank, world):
-    return [p for p in range(len(lo)) if lo[p] >= 0 and any(t % world == rank for t in range(lo[p], hi[p] + 1))]
+    from zenith_amd import shard
+    own = shard.tile_owner(1, int(max(hi)) + 1, world)  # route_blocks' default target: one tile column
+    return [p for p in range(len(lo)) if lo[p] >= 0 and rank in own[lo[p]:hi[p] + 1, 0]]
 
 
 def _a2a_worker(rank, world, port, n, out_path):

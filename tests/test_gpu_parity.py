@@ -16,18 +16,18 @@ pytestmark = pytest.mark.gpu
 FLOAT_ULP_TOL = 0  # north_star allows 1 ULP on shaded float colour; we hold 0
 
 
-def owned_rows(h, tile, shard):
-    if shard is None:
-        return np.ones(h, dtype=bool)
-    r, n = shard
-    return ((np.arange(h) // tile) % n) == r
+def owned(scene, shard_):
+    """[H, W] mask of the pixels a shard owns (shard.owned_mask; all without one)."""
+    if shard_ is None:
+        return np.ones((scene.height, scene.width), dtype=bool)
+    return shard.owned_mask(scene.width, scene.height, shard_[0], shard_[1])
 
 
 def assert_parity(device, scene, shard=None, **kw):
     gc, gd = renderer.render_scene(device, scene, shard=shard, **kw)
     oc, od = oracle.render(scene, shard=shard or (0, 1), **kw)
-    rows = owned_rows(scene.height, 32, shard)
-    gc, oc = gc[rows], oc[rows]
+    rows = owned(scene, shard)
+    gc, oc = gc[rows], oc.reshape(scene.height, scene.width, -1)[rows]
     if scene.color_format == zr.FORMAT_R32G32B32A32_SFLOAT:
         g = gc.view(np.float32).reshape(-1)
         o = oc.view(np.float32).reshape(-1)
@@ -36,7 +36,7 @@ def assert_parity(device, scene, shard=None, **kw):
     else:
         diff = np.argwhere(np.any(gc != oc, axis=-1))
         assert diff.size == 0, f"{len(diff)} pixels differ, first {diff[:5].tolist()}: " \
-                               f"gpu {gc[tuple(diff[0])]} oracle {oc[tuple(diff[0])]}"
+                               f"gpu {gc[diff[0][0]]} oracle {oc[diff[0][0]]}"
     if scene.depth:
         gdb, odb = gd[rows].view(np.uint32), od[rows].view(np.uint32)
         bad = np.argwhere(gdb != odb)
@@ -299,16 +299,20 @@ def test_full_config_parity(device, cfg):
 
 
 def test_c3_4k_shards_union(device):
-    """C3 geometry (1M tris, 3840x2160): the union of 8 tile-row shards rendered
-    separately equals the oracle frame (the multi-GPU partition, on one GPU)."""
+    """C3 geometry (1M tris, 3840x2160): the union of 8 shards rendered separately
+    equals the oracle frame, colour and depth bits (the multi-GPU partition, on
+    one GPU; 1020 tiles per rank: 8 round-robin rows of 120 + a run of 60)."""
     s = scenes.config_scene("c3")
     oc, od = oracle.render(s, nthreads=16)
     acc = np.zeros_like(oc)
+    accd = np.full_like(od, np.nan)
     for r in range(8):
-        gc, _ = renderer.render_scene(device, s, shard=(r, 8))
-        rows = owned_rows(s.height, 32, (r, 8))
+        gc, gd = renderer.render_scene(device, s, shard=(r, 8))
+        rows = owned(s, (r, 8))
         acc[rows] = gc[rows]
+        accd[rows] = gd[rows]
     assert np.array_equal(acc, oc)
+    assert np.array_equal(accd.view(np.uint32), od.view(np.uint32))
 
 
 def test_c4_micro_triangles(device):
@@ -410,7 +414,7 @@ def assert_partitioned_parity(scene, world, capacity=0, frames=1, nthreads=16, *
     oc, od = oracle.render(scene, nthreads=nthreads, **kw)
     stats = []
     for r, (gc, gd, st) in enumerate(render_partitioned(scene, world, capacity, frames, **kw)):
-        rows = owned_rows(scene.height, 32, (r, world))
+        rows = owned(scene, (r, world))
         bad = np.argwhere(np.any(gc[rows] != oc[rows], axis=-1))
         assert bad.size == 0, f"rank {r}/{world}: {len(bad)} pixels differ, first {bad[:5].tolist()}"
         if scene.depth:
@@ -442,8 +446,13 @@ def test_partitioned_paths():
 
 
 def test_partitioned_ranks_without_rows():
-    """G=8 on a 160x120 target has 4 tile rows: ranks 4-7 own none, yet they still
-    route their ranges and join every exchange (nobody is left waiting)."""
+    """G=8 on a 96x64 target has 6 tiles: ranks 3 and 7 own none, yet they still
+    route their ranges and join every exchange
+    (nobody is left waiting); a 160x120 target (20 tiles, all leftover rows) gives
+    every rank a run of 2 or 3 tiles."""
+    s = scenes.soup_scene(77, 3000, 96, 64, 8.0, scenes.PROGRAM_BLINN_PHONG)
+    assert sum(shard.owned_pixels(96, 64, r, 8) == 0 for r in range(8)) == 2
+    assert_partitioned_parity(s, 8)
     assert_partitioned_parity(scenes.soup_scene(77, 4000, 160, 120, 8.0, scenes.PROGRAM_BLINN_PHONG), 8)
 
 

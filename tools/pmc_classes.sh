@@ -18,6 +18,7 @@ DBG=zenith_amd/variants/dbg/libzenith_raster.so
 [ -f $DBG ] || { echo "missing $DBG (tools/build_variant.sh dbg -DZR_TILE_DEBUG=1)"; exit 2; }
 run() {  # name lib debug counter
   local n=$1 lib=$2 dbg=$3 ctr=$4
+  shift 4
   ZR_LIB_PATH=$lib ZR_DEBUG=$dbg timeout -s KILL 90 rocprofv3 --pmc $ctr -d $O/$n -o run --output-format csv -- \
     python3 bench.py --steps 5 --warmup 2 --no-cpu-baseline --cold-copies 0 "$@" > $O/$n.log 2>&1
   local rc=$?

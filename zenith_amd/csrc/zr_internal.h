@@ -86,6 +86,54 @@ constexpr uint32_t kMaxTilesPerPass = 16384;  // LDS histogram of the setup pass
 constexpr uint32_t kMaxPushBytes = 128;       // ZR_MAX_PUSH_CONSTANTS_SIZE (Vulkan's guaranteed minimum)
 constexpr uint32_t kMaxPushWords = kMaxPushBytes / 4;
 
+// Tile ownership of a G-way screen shard.  The first F =
+// floor(tiles_y / G) * G tile rows go round robin, row ty to rank ty % G
+// (interleaved for load balance); the tiles of the last tiles_y - F rows (n of
+// them, row-major) are cut into G runs, rank r owning [ceil(r n / G), ceil((r + 1)
+// n / G)) -- so every rank owns floor or ceil of all tiles / G (C2 at 1080p over 8
+// ranks: 255 each instead of 5 or 4 rows of 60), and the tile of leftover index i
+// belongs to rank floor(i G / n).  A rank's owned tiles are indexed round-robin
+// rows first (own row o, column tx: o * tiles_x + tx), then its leftover run.
+struct ShardGeom {
+    uint32_t tiles_x, tiles_y, G, rank;
+    uint32_t full_rows, own_rows, left_lo, left_hi;
+};
+__host__ __device__ inline ShardGeom shard_geom(uint32_t tiles_x, uint32_t tiles_y, uint32_t G, uint32_t rank) {
+    ShardGeom s;
+    s.tiles_x = tiles_x;
+    s.tiles_y = tiles_y;
+    s.G = G;
+    s.rank = rank;
+    s.own_rows = tiles_y / G;
+    s.full_rows = s.own_rows * G;
+    const uint64_t n = (uint64_t)(tiles_y - s.full_rows) * tiles_x;
+    s.left_lo = (uint32_t)(((uint64_t)rank * n + G - 1) / G);
+    s.left_hi = (uint32_t)(((uint64_t)(rank + 1) * n + G - 1) / G);
+    return s;
+}
+__host__ __device__ inline uint32_t shard_tiles(const ShardGeom& s) {
+    return s.own_rows * s.tiles_x + (s.left_hi - s.left_lo);
+}
+// Owner of tile (tx, ty).
+__host__ __device__ inline uint32_t shard_owner(const ShardGeom& s, uint32_t tx, uint32_t ty) {
+    if (ty < s.full_rows) return ty % s.G;
+    const uint64_t n = (uint64_t)(s.tiles_y - s.full_rows) * s.tiles_x;
+    return (uint32_t)(((uint64_t)(ty - s.full_rows) * s.tiles_x + tx) * s.G / n);
+}
+// Owned tile index t (< shard_tiles) -> tile coordinates.
+__host__ __device__ inline void shard_tile_xy(const ShardGeom& s, uint32_t t, uint32_t& tx, uint32_t& ty) {
+    const uint32_t fullc = s.own_rows * s.tiles_x;
+    if (t < fullc) {
+        const uint32_t o = t / s.tiles_x;
+        tx = t - o * s.tiles_x;
+        ty = o * s.G + s.rank;
+    } else {
+        const uint32_t i = s.left_lo + (t - fullc);
+        ty = s.full_rows + i / s.tiles_x;
+        tx = i % s.tiles_x;
+    }
+}
+
 // Partitioned setup for tile-row shards.  Rank r sets up the
 // primitives of its range [r * span, (r + 1) * span), kRouteChunk per workgroup
 // of k_route, and ships each set-up primitive -- its compact record, pixel bbox
@@ -197,7 +245,11 @@ struct DrawParams {
     const float* time_ptr;    // Time.time uniform (device) or nullptr
     const float* view_proj;   // mesh program: View.view_proj, 16 floats column-major (device)
     // tiling / sharding
-    uint32_t tiles_x, tiles_y, shard_rank, shard_count, owned_rows, ntiles;
+    uint32_t tiles_x, tiles_y, shard_rank, shard_count, ntiles;
+    // tile ownership of the shard (ShardGeom): round-robin rows [0, full_rows),
+    // own_rows of them this rank's; of the leftover rows' tiles (row-major index i
+    // from full_rows * tiles_x on) this rank owns [left_lo, left_hi)
+    uint32_t full_rows, own_rows, left_lo, left_hi;
     uint32_t tile_threads;    // k_tile workgroup size: 256 or 512 (tile_threads_for)
     uint32_t rec_table;       // k_tile (512 threads): keep the record table for the resolve (use_record_table)
     // partitioned setup (records mode).  In records mode `prims` is
@@ -290,6 +342,19 @@ inline bool use_record_table(uint64_t prims, uint32_t tiles_x, uint32_t tiles_y)
 inline bool use_tile_schedule(uint32_t ntiles, uint32_t cus, uint32_t tile_threads, uint64_t prims) {
     const uint64_t slots = (uint64_t)cus * (tile_threads >= 512u ? 4u : 8u);
     return ntiles > slots && prims < 32ull * ntiles;
+}
+
+__host__ __device__ inline ShardGeom shard_geom(const DrawParams& P) {
+    ShardGeom s;
+    s.tiles_x = P.tiles_x;
+    s.tiles_y = P.tiles_y;
+    s.G = P.shard_count;
+    s.rank = P.shard_rank;
+    s.full_rows = P.full_rows;
+    s.own_rows = P.own_rows;
+    s.left_lo = P.left_lo;
+    s.left_hi = P.left_hi;
+    return s;
 }
 
 // Launchers (zr_kernels.hip).  All enqueue on `stream`; no host synchronisation.

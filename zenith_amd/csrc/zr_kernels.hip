@@ -539,17 +539,37 @@ __device__ __forceinline__ int first_owned_row(uint32_t G, uint32_t rank, int ty
     return (int)(orow * G + rank);
 }
 
+// Calls fn(owned tile index, tx, ty) for every tile of [tx0, tx1] x [ty0, ty1]
+// this shard owns (ShardGeom): its round-robin rows, then the leftover rows'
+// tiles inside its run.  G == 1: every tile, index ty * tiles_x + tx.
+template <typename Fn>
+__device__ __forceinline__ void for_owned_tiles(uint32_t G, uint32_t rank, uint32_t tiles_x, uint32_t full_rows,
+                                                uint32_t own_rows, uint32_t left_lo, uint32_t left_hi, int tx0, int ty0,
+                                                int tx1, int ty1, Fn&& fn) {
+    uint32_t orow;
+    const int tyf = min(ty1, (int)full_rows - 1);
+    for (int ty = first_owned_row(G, rank, ty0, orow); ty <= tyf; ty += (int)G, ++orow) {
+        const uint32_t row = orow * tiles_x;
+        for (int tx = tx0; tx <= tx1; ++tx) fn(row + (uint32_t)tx, tx, ty);
+    }
+    for (int ty = max(ty0, (int)full_rows); ty <= ty1; ++ty) {  // leftover rows (G > 1 only)
+        const int i0 = (ty - (int)full_rows) * (int)tiles_x;
+        const int c0 = max(tx0, (int)left_lo - i0), c1 = min(tx1, (int)left_hi - 1 - i0);
+        const uint32_t base = own_rows * tiles_x + (uint32_t)(i0 - (int)left_lo);
+        for (int tx = c0; tx <= c1; ++tx) fn(base + (uint32_t)tx, tx, ty);
+    }
+}
+
 __device__ __forceinline__ uint32_t count_owned_box(const DrawParams& P, int px0, int py0, int px1, int py1,
                                                     uint32_t* s_hist) {
     const int tx0 = px0 >> kTileShift, tx1 = px1 >> kTileShift;
     const int ty0 = py0 >> kTileShift, ty1 = py1 >> kTileShift;
-    const uint32_t G = P.shard_count, tiles_x = P.tiles_x;
-    uint32_t owned = 0, orow;
-    for (int ty = first_owned_row(G, P.shard_rank, ty0, orow); ty <= ty1; ty += (int)G, ++orow) {
-        const uint32_t row = orow * tiles_x;
-        for (int tx = tx0; tx <= tx1; ++tx) atomicAdd(&s_hist[row + tx], 1u);
-        owned += (uint32_t)(tx1 - tx0 + 1);
-    }
+    uint32_t owned = 0;
+    for_owned_tiles(P.shard_count, P.shard_rank, P.tiles_x, P.full_rows, P.own_rows, P.left_lo, P.left_hi, tx0, ty0,
+                    tx1, ty1, [&](uint32_t t, int, int) {
+                        atomicAdd(&s_hist[t], 1u);
+                        ++owned;
+                    });
     return owned;
 }
 
@@ -768,10 +788,22 @@ __device__ __forceinline__ BBox receive_entry(const DrawParams& P, const uint32_
 __device__ __forceinline__ uint32_t dest_mask(const DrawParams& P, const PrimGeom& g) {
     const uint32_t G = P.shard_count;
     const int ty0 = g.py0 >> kTileShift, ty1 = g.py1 >> kTileShift;
-    if ((uint32_t)(ty1 - ty0) + 1u >= G) return G >= 32u ? 0xFFFFFFFFu : (1u << G) - 1u;
+    const int tx0 = g.px0 >> kTileShift, tx1 = g.px1 >> kTileShift;
+    const uint32_t all = G >= 32u ? 0xFFFFFFFFu : (1u << G) - 1u;
+    const int tyf = min(ty1, (int)P.full_rows - 1);  // round-robin rows: owner ty % G
     uint32_t m = 0;
-    for (int ty = ty0; ty <= ty1; ++ty) m |= 1u << ((uint32_t)ty % G);
-    return m;
+    if (tyf >= ty0) m = (uint32_t)(tyf - ty0) + 1u >= G ? all : 0u;
+    if (!m)
+        for (int ty = ty0; ty <= tyf; ++ty) m |= 1u << ((uint32_t)ty % G);
+    if (ty1 >= (int)P.full_rows) {  // leftover rows: the owners of the bbox's columns, a contiguous rank range per row
+        const uint64_t n = (uint64_t)(P.tiles_y - P.full_rows) * P.tiles_x;
+        for (int ty = max(ty0, (int)P.full_rows); ty <= ty1; ++ty) {
+            const uint64_t i0 = (uint64_t)(ty - (int)P.full_rows) * P.tiles_x;
+            const uint32_t ra = (uint32_t)((i0 + (uint64_t)tx0) * G / n), rb = (uint32_t)((i0 + (uint64_t)tx1) * G / n);
+            m |= (rb >= 31u ? 0xFFFFFFFFu : (2u << rb) - 1u) & ~((1u << ra) - 1u);
+        }
+    }
+    return m & all;
 }
 
 __global__ __launch_bounds__(kRouteThreads) void k_route(DrawParams P) {
@@ -1099,27 +1131,24 @@ __global__ __launch_bounds__(kSetupThreads) void k_setup_bin(DrawParams P) {
         // per iteration)
         uint32_t* const bins = P.bins;
         const uint32_t slab = P.slab, sG = P.shard_count, srank = P.shard_rank, tiles_x = P.tiles_x;
+        const uint32_t full_rows = P.full_rows, own_rows = P.own_rows, left_lo = P.left_lo, left_hi = P.left_hi;
         auto scatter = [&](uint32_t rec, const BBox bb) {
             if (bb.bb0 == kEmptyBox) return;
             const int tx0 = (int)(bb.bb0 & 0xFFFFu) >> kTileShift, tx1 = (int)(bb.bb1 & 0xFFFFu) >> kTileShift;
             const int ty0 = (int)(bb.bb0 >> 16) >> kTileShift, ty1 = (int)(bb.bb1 >> 16) >> kTileShift;
-            uint32_t orow;
-            for (int ty = first_owned_row(sG, srank, ty0, orow); ty <= ty1; ty += (int)sG, ++orow) {
-                const uint32_t r = orow * tiles_x;
+            for_owned_tiles(sG, srank, tiles_x, full_rows, own_rows, left_lo, left_hi, tx0, ty0, tx1, ty1,
+                            [&](uint32_t t, int tx, int ty) {
                 const int cy0 = max((int)(bb.bb0 >> 16), ty << kTileShift);
                 const int cy1 = min((int)(bb.bb1 >> 16), (ty << kTileShift) + kTile - 1);
-                for (int tx = tx0; tx <= tx1; ++tx) {
-                    const int cx0 = max((int)(bb.bb0 & 0xFFFFu), tx << kTileShift);
-                    const int cx1 = min((int)(bb.bb1 & 0xFFFFu), (tx << kTileShift) + kTile - 1);
-                    // cost class: the lane walk's pair steps over bbox ∩ tile, ceil(w / 2)
-                    // per row (sorting by steps instead of area: C3 tile pass -1 %, C2 -0.8 %)
-                    const uint32_t steps = (uint32_t)(((cx1 - cx0 + 2) >> 1) * (cy1 - cy0 + 1));
-                    const uint32_t bucket = min((steps - 1u) >> 1, kSortBuckets - 1u);
-                    const uint32_t t = r + (uint32_t)tx;
-                    const uint32_t pos = atomicAdd(&s_hist[t], 1u);
-                    if (pos - t * slab < slab) bins[pos] = rec | (bucket << kBinPrimBits);
-                }
-            }
+                const int cx0 = max((int)(bb.bb0 & 0xFFFFu), tx << kTileShift);
+                const int cx1 = min((int)(bb.bb1 & 0xFFFFu), (tx << kTileShift) + kTile - 1);
+                // cost class: the lane walk's pair steps over bbox ∩ tile, ceil(w / 2)
+                // per row (sorting by steps instead of area: C3 tile pass -1 %, C2 -0.8 %)
+                const uint32_t steps = (uint32_t)(((cx1 - cx0 + 2) >> 1) * (cy1 - cy0 + 1));
+                const uint32_t bucket = min((steps - 1u) >> 1, kSortBuckets - 1u);
+                const uint32_t pos = atomicAdd(&s_hist[t], 1u);
+                if (pos - t * slab < slab) bins[pos] = rec | (bucket << kBinPrimBits);
+            });
         };
         uint32_t nown = 0;
         while (own_unit(w, G, nown) < units) ++nown;
@@ -1990,8 +2019,8 @@ __global__ __launch_bounds__(NT, kTileWgs * kTileThreads / 256) void k_tile(Draw
     uint32_t* s_nwin = s_misc + 5;   // resolve: distinct winners of the tile
     const uint32_t b = (tile_debug(P) & kDebugReverseTiles) ? P.ntiles - 1u - blockIdx.x : blockIdx.x;
     const uint32_t t = P.tile_order ? P.tile_order[b] : xcd_tile(b, P.ntiles);
-    const uint32_t oy = t / P.tiles_x, tx = t - oy * P.tiles_x;
-    const uint32_t ty = oy * P.shard_count + P.shard_rank;
+    uint32_t tx, ty;
+    shard_tile_xy(shard_geom(P), t, tx, ty);
     const int x0 = (int)tx * kTile, y0 = (int)ty * kTile;
     const bool stamp = (tile_debug(P) & kDebugStamps) && threadIdx.x == 0 && t < kMaxTilesPerPass;
     unsigned long long* ts = P.dbg_ts + 8192 * 8 + (size_t)t * 8;
@@ -2288,13 +2317,17 @@ __global__ __launch_bounds__(NT, kTileWgs * kTileThreads / 256) void k_tile(Draw
     if (stamp) {
         ts[4] = __builtin_amdgcn_s_memrealtime();
         ts[7] = ((unsigned long long)s_dbg[1] << 32) | s_dbg[0];
+        if (NT >= 512) {  // (resolve_tile's own stamps use these two at 256 threads)
+            ts[5] = 0ull;
+            ts[6] = count;  // the tile's list length (tools/tile_stamps.py)
+        }
     }
 }
 
 __global__ __launch_bounds__(kTileThreads) void k_clear(DrawParams P) {
     const uint32_t t = blockIdx.x;
-    const uint32_t oy = t / P.tiles_x, tx = t - oy * P.tiles_x;
-    const uint32_t ty = oy * P.shard_count + P.shard_rank;
+    uint32_t tx, ty;
+    shard_tile_xy(shard_geom(P), t, tx, ty);
     const int x0 = (int)tx * kTile, y0 = (int)ty * kTile;
     const float c[4] = {0.f, 0.f, 0.f, 0.f};
     for (int i = threadIdx.x; i < kTilePixels; i += kTileThreads) {

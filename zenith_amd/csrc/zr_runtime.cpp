@@ -275,6 +275,8 @@ struct zr_device_t {
     int comm_rank = 0, comm_size = 1;
     hipStream_t gather_stream = nullptr;
     hipEvent_t frame_done = nullptr;
+    uint8_t* gather_stage = nullptr;  // packed leftover-row rectangles of the row gather
+    uint64_t gather_stage_cap = 0;
     zr_draw_stats last{};
     uint64_t last_prims = 0;
     // profiling (zr_device_set_profiling): 1 = per-kernel events, 2 = also the winner census
@@ -581,8 +583,12 @@ zr_result fill_target(const ExecState& s, DrawParams& P) {
     P.tiles_y = (P.fb_h + kTile - 1) / kTile;
     P.shard_rank = s.shard_rank;
     P.shard_count = s.shard_count;
-    P.owned_rows = P.tiles_y > s.shard_rank ? (P.tiles_y - s.shard_rank + s.shard_count - 1) / s.shard_count : 0;
-    P.ntiles = P.owned_rows * P.tiles_x;
+    const ShardGeom sg = shard_geom(P.tiles_x, P.tiles_y, s.shard_count, s.shard_rank);
+    P.full_rows = sg.full_rows;
+    P.own_rows = sg.own_rows;
+    P.left_lo = sg.left_lo;
+    P.left_hi = sg.left_hi;
+    P.ntiles = shard_tiles(sg);
     // clears (fused into the first draw of the pass, else k_clear at end_rendering)
     P.clear_color_enable = (ct && s.color_clear_pending) ? 1u : 0u;
     if (ct) {
@@ -852,7 +858,9 @@ zr_result exec_draw(zr_device* d, ExecState& s, const Cmd& c, bool indexed) {
     // Overlapped and partitioned draws alternate between the two scratch sets.
     // Partitioned draws always do: the route, exchange and setup of draw i+1 run
     // on setup_stream while draw i's tile pass runs on the main stream.
-    const bool overlap = partitioned || overlap_setup;
+    // (ZR_SETUP_OVERLAP=0 serialises partitioned draws too: a diagnostic that times
+    // each of their kernels alone)
+    const bool overlap = (partitioned && d->setup_overlap != 0) || overlap_setup;
     ScratchSet& S = d->sets[overlap ? d->cur_set : 0];
     if (overlap) d->cur_set ^= 1u;
     if ((rc = ensure_scratch(d, S, P))) return rc;
@@ -1119,6 +1127,7 @@ ZR_API void zr_device_destroy(zr_device* d) {
     rccl_comm_destroy(d->comm_x);
     rccl_comm_destroy(d->comm_g);
     if (d->gather_stream) (void)hipStreamDestroy(d->gather_stream);
+    if (d->gather_stage) (void)hipFree(d->gather_stage);
     if (d->frame_done) (void)hipEventDestroy(d->frame_done);
     (void)hipStreamDestroy(d->setup_stream);
     (void)hipStreamDestroy(d->own_stream);
@@ -1869,25 +1878,51 @@ zr_result rccl_exchange(void* user, void* stream, const void* send, void* recv, 
 }  // namespace
 
 // Host-side plans of the two collectives (no device needed; tests/test_abi.py).
-// Gather: every tile row is a contiguous span of the linear image, sent from its
-// owner (ty % nranks) straight into place on the root -- one send/recv per tile
-// row, no packing; the root's own rows do not move.  `offset` is the span's byte
-// offset in the image (the same on both sides), the last row may be partial.
-ZR_API int32_t zr_gather_plan(uint32_t height, uint64_t row_bytes, int32_t nranks, int32_t rank, int32_t root,
-                              zr_transfer_op* out, int32_t capacity) {
-    if (nranks < 1 || rank < 0 || rank >= nranks || root < 0 || root >= nranks) return -1;
-    const uint32_t tiles_y = (height + kTile - 1) / kTile;
+// Gather (ShardGeom ownership): a round-robin tile row is a contiguous span of the
+// linear image, sent from its owner straight into place on the root; a leftover
+// row holds one run of tiles per owner, a rectangle (rows spans `pitch` apart)
+// unless it is the whole row -- the runtime packs it into a staging buffer to send
+// and unpacks it on the root.  One op per (tile row, owner), none for the root's
+// own tiles.  `offset` is the byte offset in the image (the same on both sides);
+// the last tile row may be partial.
+ZR_API int32_t zr_gather_plan(uint32_t width, uint32_t height, uint32_t bytes_per_pixel, int32_t nranks, int32_t rank,
+                              int32_t root, zr_transfer_op* out, int32_t capacity) {
+    if (nranks < 1 || nranks > (int32_t)kMaxShards || rank < 0 || rank >= nranks || root < 0 || root >= nranks ||
+        width == 0 || height == 0 || bytes_per_pixel == 0)
+        return -1;
+    const uint32_t tiles_x = (width + kTile - 1) / kTile, tiles_y = (height + kTile - 1) / kTile;
+    const uint64_t row_bytes = (uint64_t)width * bytes_per_pixel;
     int32_t n = 0;
-    for (uint32_t ty = 0; ty < tiles_y; ++ty) {
-        const int32_t owner = (int32_t)(ty % (uint32_t)nranks);
-        if (owner == root || (rank != root && rank != owner)) continue;
+    auto emit = [&](int32_t owner, uint32_t ty, uint32_t c0, uint32_t c1) {  // tiles [c0, c1] of row ty
+        if (owner == root || (rank != root && rank != owner)) return;
+        const uint32_t rows = std::min<uint32_t>(kTile, height - ty * kTile);
+        const uint32_t x0 = c0 * kTile, x1 = std::min<uint32_t>(width, (c1 + 1) * kTile);
         if (out && n < capacity) {
-            out[n].peer = rank == root ? owner : root;
-            out[n].send = rank == root ? 0 : 1;
-            out[n].offset = (uint64_t)ty * kTile * row_bytes;
-            out[n].bytes = (uint64_t)std::min<uint32_t>(kTile, height - ty * kTile) * row_bytes;
+            zr_transfer_op& op = out[n];
+            memset(&op, 0, sizeof op);
+            op.peer = rank == root ? owner : root;
+            op.send = rank == root ? 0 : 1;
+            op.offset = (uint64_t)ty * kTile * row_bytes + (uint64_t)x0 * bytes_per_pixel;
+            if (x0 == 0 && x1 == width) {  // whole rows: one contiguous span
+                op.bytes = (uint64_t)rows * row_bytes;
+                op.rows = 1;
+            } else {
+                op.bytes = (uint64_t)(x1 - x0) * bytes_per_pixel;
+                op.rows = rows;
+                op.pitch = row_bytes;
+            }
         }
         ++n;
+    };
+    for (int32_t r = 0; r < nranks; ++r) {
+        const ShardGeom sg = shard_geom(tiles_x, tiles_y, (uint32_t)nranks, (uint32_t)r);
+        for (uint32_t ty = (uint32_t)r; ty < sg.full_rows; ty += (uint32_t)nranks) emit(r, ty, 0, tiles_x - 1);
+        for (uint32_t i = sg.left_lo; i < sg.left_hi;) {  // its leftover run, cut at row ends
+            const uint32_t ty = sg.full_rows + i / tiles_x, c0 = i % tiles_x;
+            const uint32_t c1 = std::min(tiles_x - 1, c0 + (sg.left_hi - i) - 1);
+            emit(r, ty, c0, c1);
+            i += c1 - c0 + 1;
+        }
     }
     return n;
 }
@@ -1902,10 +1937,12 @@ ZR_API int32_t zr_exchange_plan(int32_t nranks, int32_t rank, uint64_t bytes_per
     for (int32_t p = 0; p < nranks; ++p)
         for (int32_t send = 1; send >= 0; --send) {
             if (out && n < capacity) {
+                memset(&out[n], 0, sizeof out[n]);
                 out[n].peer = p;
                 out[n].send = send;
                 out[n].offset = (uint64_t)p * bytes_per_rank;
                 out[n].bytes = bytes_per_rank;
+                out[n].rows = 1;
             }
             ++n;
         }
@@ -1958,18 +1995,52 @@ ZR_API zr_result zr_device_gather_tile_rows(zr_device* d, zr_texture* t, int32_t
     // after everything enqueued so far on the device stream (the frame)
     ZR_HIP(hipEventRecord(d->frame_done, d->stream));
     ZR_HIP(hipStreamWaitEvent(d->gather_stream, d->frame_done, 0));
-    const uint64_t row_bytes = (uint64_t)t->width * t->bpp;
-    const int32_t n = zr_gather_plan(t->height, row_bytes, d->comm_size, d->comm_rank, root, nullptr, 0);
+    const int32_t n = zr_gather_plan(t->width, t->height, t->bpp, d->comm_size, d->comm_rank, root, nullptr, 0);
     std::vector<zr_transfer_op> plan((size_t)std::max(n, 0));
-    zr_gather_plan(t->height, row_bytes, d->comm_size, d->comm_rank, root, plan.data(), n);
+    zr_gather_plan(t->width, t->height, t->bpp, d->comm_size, d->comm_rank, root, plan.data(), n);
+    // rectangles (leftover rows' tile runs) travel packed through a staging buffer
+    uint64_t stage_bytes = 0;
+    for (const zr_transfer_op& op : plan)
+        if (op.rows > 1) stage_bytes += op.bytes * op.rows;
+    if (stage_bytes > d->gather_stage_cap) {
+        ZR_HIP(hipStreamSynchronize(d->gather_stream));
+        if (d->gather_stage) ZR_HIP(hipFree(d->gather_stage));
+        d->gather_stage = nullptr;
+        ZR_HIP(hipMalloc((void**)&d->gather_stage, stage_bytes));
+        d->gather_stage_cap = stage_bytes;
+    }
+    const hipStream_t gs = d->gather_stream;
+    uint64_t so = 0;
+    for (const zr_transfer_op& op : plan) {  // senders pack first
+        if (op.rows <= 1) continue;
+        if (op.send)
+            ZR_HIP(hipMemcpy2DAsync(d->gather_stage + so, op.bytes, (const uint8_t*)t->ptr + op.offset, op.pitch, op.bytes,
+                                    op.rows, hipMemcpyDeviceToDevice, gs));
+        so += op.bytes * op.rows;
+    }
     std::string err;
     bool ok = rccl_group_start(err);
+    so = 0;
     for (const zr_transfer_op& op : plan) {
         uint8_t* p = (uint8_t*)t->ptr + op.offset;
-        ok = ok && (op.send ? rccl_send(p, op.bytes, op.peer, d->comm_g, d->gather_stream, err)
-                            : rccl_recv(p, op.bytes, op.peer, d->comm_g, d->gather_stream, err));
+        uint64_t bytes = op.bytes;
+        if (op.rows > 1) {
+            p = d->gather_stage + so;
+            bytes = op.bytes * op.rows;
+            so += bytes;
+        }
+        ok = ok && (op.send ? rccl_send(p, bytes, op.peer, d->comm_g, gs, err)
+                            : rccl_recv(p, bytes, op.peer, d->comm_g, gs, err));
     }
     if (!rccl_group_end(err) || !ok) return fail(ZR_ERROR_DEVICE_LOST, err);
+    so = 0;
+    for (const zr_transfer_op& op : plan) {  // the root unpacks after the group
+        if (op.rows <= 1) continue;
+        if (!op.send)
+            ZR_HIP(hipMemcpy2DAsync((uint8_t*)t->ptr + op.offset, op.pitch, d->gather_stage + so, op.bytes, op.bytes,
+                                    op.rows, hipMemcpyDeviceToDevice, gs));
+        so += op.bytes * op.rows;
+    }
     ZR_HIP(hipEventRecord(t->gather_done, d->gather_stream));
     t->gather_pending = true;
     return ZR_SUCCESS;

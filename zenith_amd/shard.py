@@ -1,11 +1,15 @@
-"""Screen-tile sharding across ranks and the tile-row gather.
+"""Screen-tile sharding across ranks and the tile gather.
 
-Rank r of G renders the tile rows t with t % G == r (interleaved for load
-balance).  Its rows of the final image are contiguous row spans, so the gather
-is: pack the owned rows into one contiguous buffer, point-to-point send it to
-rank 0 (RCCL over xGMI on the GPU box: each peer uses its own link, no ring),
-and rank 0 scatters the received rows into place.  Works on any torch device,
-so the same code is exercised with gloo on CPU in tests/test_dist.py.
+Ownership (zr_internal.h ShardGeom, restated here): of a target's
+tiles_y rows of 32x32 tiles, the first F = floor(tiles_y / G) * G go round robin
+(row t to rank t % G, interleaved for load balance); the n tiles of the last
+tiles_y - F rows, in row-major order, are cut into G runs, tile i of them
+belonging to rank floor(i * G / n).  Every rank owns the floor or the ceiling of
+the tiles / G.  The gather: each rank packs its owned pixels into one
+contiguous buffer, sends it point-to-point to rank 0 (RCCL over xGMI on the GPU
+box: each peer uses its own link, no ring), and rank 0 scatters them into place.
+Works on any torch device, so the same code is exercised with gloo on CPU in
+tests/test_dist.py.
 """
 from __future__ import annotations
 
@@ -16,36 +20,59 @@ import torch.distributed as dist
 TILE = 32  # must match zr::kTile (zenith_amd/csrc/zr_internal.h)
 
 
-def owned_rows(height: int, rank: int, world: int, tile: int = TILE, device=None) -> torch.Tensor:
-    rows = torch.arange(height, device=device)
-    return rows[((rows // tile) % world) == rank]
+def tile_owner(tiles_x: int, tiles_y: int, world: int) -> np.ndarray:
+    """[tiles_y, tiles_x] owner rank of every tile."""
+    full = (tiles_y // world) * world
+    own = np.empty((tiles_y, tiles_x), dtype=np.int64)
+    own[:full] = (np.arange(full) % world)[:, None]
+    n = (tiles_y - full) * tiles_x
+    if n:
+        own[full:] = (np.arange(n) * world // n).reshape(tiles_y - full, tiles_x)
+    return own
 
 
-class TileRowGather:
-    """Pre-plans the row index lists and receive buffers for one image shape."""
+def owned_mask(width: int, height: int, rank: int, world: int, tile: int = TILE) -> np.ndarray:
+    """[height, width] bool: the pixels of the tiles rank `rank` of `world` owns."""
+    own = tile_owner(-(-width // tile), -(-height // tile), world) == rank
+    return np.repeat(np.repeat(own, tile, axis=0), tile, axis=1)[:height, :width]
 
-    def __init__(self, height: int, row_bytes: int, rank: int, world: int, device, tile: int = TILE, group=None):
+
+def owned_pixels(width: int, height: int, rank: int, world: int, tile: int = TILE) -> int:
+    return int(owned_mask(width, height, rank, world, tile).sum())
+
+
+class TileGather:
+    """Pre-plans the owned-pixel index lists and receive buffers for one image
+    shape (torch.distributed point-to-point; the runtime's own RCCL gather is
+    zr_device_gather_tile_rows)."""
+
+    def __init__(self, width: int, height: int, bytes_per_pixel: int, rank: int, world: int, device,
+                 tile: int = TILE, group=None):
         self.rank, self.world, self.group = rank, world, group
-        self.rows = [owned_rows(height, r, world, tile, device) for r in range(world)]
-        self.send_buf = torch.empty((len(self.rows[rank]), row_bytes), dtype=torch.uint8, device=device)
+        self.shape = (height * width, bytes_per_pixel)
+        flat = [torch.from_numpy(np.flatnonzero(owned_mask(width, height, r, world, tile))).to(device)
+                for r in range(world)]
+        self.pix = flat
+        self.send_buf = torch.empty((len(flat[rank]), bytes_per_pixel), dtype=torch.uint8, device=device)
         self.recv_bufs = None
         if rank == 0:
-            self.recv_bufs = [torch.empty((len(self.rows[r]), row_bytes), dtype=torch.uint8, device=device)
+            self.recv_bufs = [torch.empty((len(flat[r]), bytes_per_pixel), dtype=torch.uint8, device=device)
                               for r in range(world)]
 
     def gather(self, image: torch.Tensor) -> None:
-        """image: [H, row_bytes] uint8, fully valid on rank 0 afterwards."""
+        """image: [H, W * bytes_per_pixel] uint8, fully valid on rank 0 afterwards."""
         if self.world == 1:
             return
+        img = image.view(self.shape)
         peer = (lambda r: dist.get_global_rank(self.group, r)) if self.group is not None else (lambda r: r)
         if self.rank == 0:
             ops = [dist.P2POp(dist.irecv, self.recv_bufs[r], peer(r), group=self.group) for r in range(1, self.world)]
             for req in dist.batch_isend_irecv(ops):
                 req.wait()
             for r in range(1, self.world):
-                image.index_copy_(0, self.rows[r], self.recv_bufs[r])
+                img.index_copy_(0, self.pix[r], self.recv_bufs[r])
         else:
-            torch.index_select(image, 0, self.rows[self.rank], out=self.send_buf)
+            torch.index_select(img, 0, self.pix[self.rank], out=self.send_buf)
             for req in dist.batch_isend_irecv([dist.P2POp(dist.isend, self.send_buf, peer(0), group=self.group)]):
                 req.wait()
 
@@ -94,13 +121,24 @@ def route_range(n_prims: int, rank: int, world: int):
     return lo, min(n_prims, lo + span)
 
 
-def route_blocks(row_lo, row_hi, rank: int, world: int, cap: int = 0) -> torch.Tensor:
+def route_dests(row_lo: int, row_hi: int, world: int, tiles_x: int, tiles_y: int):
+    """Ranks owning a tile of rows [row_lo, row_hi] (every column): k_route's
+    dest_mask for a bbox spanning the target's width."""
+    own = tile_owner(tiles_x, tiles_y, world)
+    return sorted(set(own[row_lo:row_hi + 1].reshape(-1).tolist()))
+
+
+def route_blocks(row_lo, row_hi, rank: int, world: int, cap: int = 0, tiles_x: int = 1, tiles_y: int = 0) -> torch.Tensor:
     """Host model of k_route for rank `rank`: row_lo/row_hi are each primitive's
-    first/last tile row (row_lo < 0: no sample); the entries' bbox words carry
-    them (bb0 = row_lo, bb1 = row_hi) in place of a pixel bbox.  Returns the send
-    buffer, [world][block_bytes] uint8, entries in primitive order (one of the
-    orders the device may produce)."""
+    first/last tile row (row_lo < 0: no sample) of a tiles_x x tiles_y target
+    (default: one column, rows up to the largest row_hi), the primitive spanning
+    every column; the entries' bbox words carry the rows (bb0 = row_lo, bb1 =
+    row_hi) in place of a pixel bbox.  Returns the send buffer,
+    [world][block_bytes] uint8, entries in primitive order (one of the orders the
+    device may produce)."""
     n = len(row_lo)
+    tiles_y = tiles_y or int(max(row_hi)) + 1
+    own = tile_owner(tiles_x, tiles_y, world)
     _, span, cap, bb = route_geometry(n, world, cap)
     hdr = np.zeros(world, dtype=_HEADER)
     ent = np.zeros((world, cap), dtype=_ENTRY)
@@ -109,7 +147,7 @@ def route_blocks(row_lo, row_hi, rank: int, world: int, cap: int = 0) -> torch.T
         a, b = int(row_lo[p]), int(row_hi[p])
         if a < 0:
             continue
-        dests = range(world) if b - a + 1 >= world else sorted({t % world for t in range(a, b + 1)})
+        dests = sorted(set(own[a:b + 1].reshape(-1).tolist()))
         for d in dests:
             k = int(hdr[d]["total"])
             if k < cap:

@@ -77,7 +77,8 @@ class zr_kernel_time(C.Structure):
 
 
 class zr_transfer_op(C.Structure):
-    _fields_ = [("peer", C.c_int32), ("send", C.c_int32), ("offset", C.c_uint64), ("bytes", C.c_uint64)]
+    _fields_ = [("peer", C.c_int32), ("send", C.c_int32), ("offset", C.c_uint64), ("bytes", C.c_uint64),
+                ("rows", C.c_uint32), ("reserved", C.c_uint32), ("pitch", C.c_uint64)]
 
 
 class zr_draw_stats(C.Structure):
@@ -235,7 +236,7 @@ _SIGS = {
     "zr_cmd_clear_color_image": (None, [_P, _P, C.POINTER(C.c_float * 4)]),
     "zr_cmd_set_tile_shard_exchange": (None, [_P, C.c_uint32, C.c_uint32, _P, _P]),
     "zr_cmd_set_route_capacity": (None, [_P, C.c_uint32]),
-    "zr_gather_plan": (C.c_int32, [C.c_uint32, C.c_uint64, C.c_int32, C.c_int32, C.c_int32,
+    "zr_gather_plan": (C.c_int32, [C.c_uint32, C.c_uint32, C.c_uint32, C.c_int32, C.c_int32, C.c_int32,
                                    C.POINTER(zr_transfer_op), C.c_int32]),
     "zr_exchange_plan": (C.c_int32, [C.c_int32, C.c_int32, C.c_uint64, C.POINTER(zr_transfer_op), C.c_int32]),
     "zr_device_set_stream": (_R, [_P, _P]),
