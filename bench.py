@@ -175,20 +175,22 @@ class CaptureExchange(shard.Exchange):
             shard.device_bytes(recv, nbytes * self.world, self.device).zero_()
 
 
-class ReplayExchange(shard.Exchange):
+class ReplayExchange:
     """--emulate-shard, partitioned setup: delivers the blocks every source rank
     really routed to this rank (assembled from their captured sends), so the
     rank's binning and tile pass see its real received set.  The delivery is a
-    device copy of those bytes on the runtime's setup stream (the real all-to-all
-    over xGMI is the driver's 8-GPU run to measure)."""
+    device copy of those bytes on the runtime's route stream, enqueued by the
+    runtime itself (zr_replay_exchange_fn: no Python callback per frame, which
+    would make the emulated frame host-bound); the real all-to-all over xGMI is
+    the driver's 8-GPU run to measure."""
 
     def __init__(self, device, recv_blocks: torch.Tensor):
-        super().__init__()
-        self.device, self.src = device, recv_blocks.reshape(-1)
+        self.device, self.src = device, recv_blocks.reshape(-1).contiguous()
 
-    def exchange(self, stream, send, recv, nbytes):
-        with torch.cuda.stream(torch.cuda.ExternalStream(stream, device=self.device)):
-            shard.device_bytes(recv, self.src.numel(), self.device).copy_(self.src)
+    def native(self):
+        import ctypes
+        desc = zr.zr_replay_exchange(self.src.data_ptr(), self.src.numel())
+        return zr.lib().zr_replay_exchange_fn(), ctypes.addressof(desc), (desc, self.src)
 
 
 def route_totals(sent: torch.Tensor):

@@ -431,6 +431,17 @@ ZR_API zr_result zr_rccl_get_unique_id(void *out);
 ZR_API zr_result zr_device_init_rccl(zr_device *dev, const void *exchange_id, const void *gather_id, int32_t nranks,
                                      int32_t rank);
 ZR_API zr_exchange_fn zr_rccl_exchange_fn(void);
+/* A zr_exchange_fn that delivers a recorded receive buffer instead of running a
+ * collective: `user` points to a zr_replay_exchange whose `src` (device memory,
+ * count x bytes_per_rank) is copied into the receive buffer on the runtime's
+ * stream.  For emulating one rank of a partitioned shard on one GPU with the
+ * blocks the other ranks really routed to it (bench.py --emulate-shard): the
+ * copy stands in for the all-to-all's transfer, without a host callback. */
+typedef struct zr_replay_exchange {
+    const void *src;
+    uint64_t bytes;
+} zr_replay_exchange;
+ZR_API zr_exchange_fn zr_replay_exchange_fn(void);
 ZR_API zr_result zr_device_gather_tile_rows(zr_device *dev, zr_texture *tex, int32_t root);
 /* The point-to-point transfers the two collectives enqueue on this rank (host
  * only, no device): zr_device_gather_tile_rows of a width x height image of

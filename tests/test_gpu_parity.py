@@ -27,6 +27,7 @@ def assert_parity(device, scene, shard=None, **kw):
     gc, gd = renderer.render_scene(device, scene, shard=shard, **kw)
     oc, od = oracle.render(scene, shard=shard or (0, 1), **kw)
     rows = owned(scene, shard)
+    full_c, full_d = gc, gd
     gc, oc = gc[rows], oc.reshape(scene.height, scene.width, -1)[rows]
     if scene.color_format == zr.FORMAT_R32G32B32A32_SFLOAT:
         g = gc.view(np.float32).reshape(-1)
@@ -41,7 +42,7 @@ def assert_parity(device, scene, shard=None, **kw):
         gdb, odb = gd[rows].view(np.uint32), od[rows].view(np.uint32)
         bad = np.argwhere(gdb != odb)
         assert bad.size == 0, f"{len(bad)} depth values differ, first {bad[:5].tolist()}"
-    return gc, gd
+    return full_c, full_d
 
 
 def test_triangle_reference_scene(device):

@@ -3,6 +3,8 @@
 #pragma once
 #include <stdint.h>
 
+#include <algorithm>
+
 namespace zr {
 
 constexpr int kTile = 32;          // screen-tile edge in pixels (one workgroup per tile)
@@ -161,6 +163,10 @@ __host__ __device__ inline uint64_t route_block_bytes(uint32_t cap) { return siz
 constexpr uint32_t kRouteChunk = 512;
 constexpr int kRouteThreads = 512;   // 1 primitive per thread (a latency chain: index -> positions)
 constexpr uint32_t kMaxShards = 32;  // destination masks are u32
+// Scratch sets the runtime cycles through for overlapped draws: a partitioned
+// draw's route + exchange, binning and tile pass are three pipeline stages on
+// three streams, each stage of draw i + 2, i + 1 and i in a set of its own.
+constexpr uint32_t kScratchSets = 3;
 
 // Timing-experiment switches (ZR_DEBUG env var); never set in production runs.
 enum : uint32_t { kDebugSkipRaster = 1u, kDebugSkipShade = 2u, kDebugLoadOnly = 16u,
@@ -313,11 +319,25 @@ constexpr uint32_t kSetupMiscWords = 96 + 8 * kSchedBuckets;
 // 61.9 us per frame; replicated shards, whose single setup kernel needs whole
 // CUs, are 13-20 % slower that way, and C2's shard of 8, at one tile per CU,
 // equal).
+// Round 4 (three-stage partitioned pipeline, balanced tile ownership): a
+// partitioned shard whose tiles fit one round of 512-thread workgroups (4 per CU)
+// takes 8 waves per tile -- C3 rank of 8 (1020 tiles), with the records-mode grid
+// below: 4.47x vs 4.12x at 4 waves -- and 4 waves only past one round.
 inline uint32_t tile_threads_for(uint32_t ntiles, uint32_t cus, uint64_t prims, bool partitioned) {
     const uint32_t c = cus ? cus : 1u;
     const uint32_t per_cu = ntiles / c;
-    if (partitioned) return 2ull * ntiles >= 7ull * c ? (uint32_t)kTileThreads : 512u;
+    if (partitioned) return ntiles > 4ull * c ? (uint32_t)kTileThreads : 512u;
     return (per_cu >= 6u && prims >= 32ull * ntiles && prims < 80ull * ntiles) ? (uint32_t)kTileThreads : 512u;
+}
+
+// k_setup_bin workgroups of a partitioned (records-mode) draw that expects about
+// `entries` received records: one per 2048 entries (16 waves x 2 records per
+// lane), at least 16, at most one per CU.  One per CU (the unpartitioned choice)
+// left most of a workgroup's waves idle and multiplied the per-tile counter
+// atomics (round 4, emulated rank of 8: C2 frame 43.6 -> 38.4 us, C3 equal).
+inline uint32_t records_setup_wgs(uint64_t entries, uint32_t cus) {
+    const uint64_t w = (entries + 2047u) / 2048u;
+    return (uint32_t)std::max<uint64_t>(1u, std::min<uint64_t>(cus ? cus : 1u, std::max<uint64_t>(16u, w)));
 }
 
 // Whether k_tile's 512-thread resolve reads its winners' records from the tile's

@@ -218,6 +218,7 @@ struct ScratchSet {
     uint64_t gids_cap = 0;
     uint64_t xsend_layout = 0;  // (shard count, route capacity) the send headers were last zeroed for
     hipEvent_t setup_done = nullptr;  // k_setup_bin of the last draw that used this set
+    hipEvent_t route_done = nullptr;  // partitioned draws: k_route + exchange of the last draw that used this set
     hipEvent_t tile_done = nullptr;   // k_tile of the last draw that used this set
     bool tile_done_valid = false;
     // a draw on the main stream alone used this set after tile_done was recorded:
@@ -237,9 +238,14 @@ struct zr_device_t {
     // Scratch (grow-only) in two sets: consecutive draws alternate, so the setup of
     // draw i+1 (on setup_stream) only waits for the tile pass of draw i-1, the last
     // reader of its set, and runs while the tile pass of draw i finishes.
-    ScratchSet sets[2];
+    ScratchSet sets[kScratchSets];
     uint32_t cur_set = 0;
     hipStream_t setup_stream = nullptr;
+    // partitioned draws: k_route + the exchange on a stream of their own, so draw
+    // i+2's route and exchange, draw i+1's records-mode binning (setup_stream) and
+    // draw i's tile pass (main stream) run together: a three-stage pipeline over
+    // three scratch sets
+    hipStream_t route_stream = nullptr;
     // k_setup_bin on the setup stream (two scratch sets), so draw i+1's setup
     // fills CUs draw i's tile pass frees.  Measured with round 1's two-launch
     // split setup (1 GPU): C1 (100k tris) 1180 -> 1274 Mtri/s, C2 7925 -> 8007,
@@ -250,6 +256,7 @@ struct zr_device_t {
     int setup_overlap = -1;
     int rec_table = -1;        // ZR_REC_TABLE=0/1 forces k_tile's record table (A/B); -1: use_record_table
     int tile_sched = -1;       // ZR_TILE_SCHED=0/1 forces the heaviest-first tile schedule (A/B); -1: use_tile_schedule
+    uint32_t rec_wgs = 0;      // ZR_REC_WGS: k_setup_bin workgroups of partitioned (records-mode) draws; 0: one per CU
     int cu_count = 0;
     uint32_t occupancy_checked_tiles = 0;
     bool occupancy_checked_mesh = false;
@@ -342,6 +349,7 @@ void timed_launch(zr_device* d, const char* name, hipStream_t stream, F&& fn) {
 
 // Both streams idle (scratch may be freed, host-visible status is final).
 zr_result sync_streams(zr_device* d) {
+    ZR_HIP(hipStreamSynchronize(d->route_stream));
     ZR_HIP(hipStreamSynchronize(d->setup_stream));
     ZR_HIP(hipStreamSynchronize(d->stream));
     if (d->gather_stream) ZR_HIP(hipStreamSynchronize(d->gather_stream));
@@ -492,7 +500,9 @@ zr_result device_sync(zr_device* d) {
         }
         d->scratch_gen++;
     }
-    d->last.bin_capacity = std::min<uint64_t>(d->sets[0].bins_cap, d->sets[1].bins ? d->sets[1].bins_cap : ~0ull);
+    d->last.bin_capacity = d->sets[0].bins_cap;
+    for (const ScratchSet& S : d->sets)
+        if (S.bins) d->last.bin_capacity = std::min<uint64_t>(d->last.bin_capacity, S.bins_cap);
     if (d->census_words) {  // distinct primitives that won a pixel in the last census draw
         std::vector<uint32_t> bits(d->census_words);
         ZR_HIP(hipMemcpy(bits.data(), d->win_bits, bits.size() * 4, hipMemcpyDeviceToHost));
@@ -628,6 +638,7 @@ zr_result ensure_scratch(zr_device* d, ScratchSet& S, DrawParams& P) {
     if (!S.setup_done) {
         ZR_HIP(hipEventCreateWithFlags(&S.setup_done, kStreamEventFlags));
         ZR_HIP(hipEventCreateWithFlags(&S.tile_done, kStreamEventFlags));
+        ZR_HIP(hipEventCreateWithFlags(&S.route_done, kStreamEventFlags));
     }
     P.records = S.records;
     P.records_big = S.records_big;
@@ -819,6 +830,10 @@ zr_result exec_draw(zr_device* d, ExecState& s, const Cmd& c, bool indexed) {
         const uint64_t cus = (uint64_t)std::max(d->cu_count, 1);
         const uint64_t per_wg = (uint64_t)kSetupThreads * P.setup_batch;
         P.setup_wgs = (uint32_t)std::max<uint64_t>(1, std::min<uint64_t>(cus, (positions + per_wg - 1) / per_wg));
+        if (partitioned)  // records mode: sized to the expected received entries (ZR_REC_WGS: A/B)
+            P.setup_wgs = std::min<uint32_t>(P.setup_wgs, d->rec_wgs ? d->rec_wgs
+                                                                     : records_setup_wgs((uint64_t)s.shard_count * P.route_cap,
+                                                                                         (uint32_t)cus));
         uint32_t shift = 6;
         while ((1u << shift) < 64u * P.setup_batch) ++shift;
         while (((positions + (1ull << shift) - 1) >> shift) > 64ull * P.setup_wgs) ++shift;
@@ -862,7 +877,7 @@ zr_result exec_draw(zr_device* d, ExecState& s, const Cmd& c, bool indexed) {
     // each of their kernels alone)
     const bool overlap = (partitioned && d->setup_overlap != 0) || overlap_setup;
     ScratchSet& S = d->sets[overlap ? d->cur_set : 0];
-    if (overlap) d->cur_set ^= 1u;
+    if (overlap) d->cur_set = (d->cur_set + 1u) % kScratchSets;
     if ((rc = ensure_scratch(d, S, P))) return rc;
     if (sched) {
         if ((rc = grow(d, S.tile_order, S.tile_order_cap, P.ntiles, 4))) return rc;
@@ -872,21 +887,28 @@ zr_result exec_draw(zr_device* d, ExecState& s, const Cmd& c, bool indexed) {
     d->last.triangles_in = prims;
 
     const hipStream_t ss = overlap ? d->setup_stream : d->stream;
-    // the first pass on ss may start once the previous reader of this scratch set
-    // (the k_tile two draws back) is done
+    // partitioned: route + exchange on their own stream (serialised: the device stream)
+    const hipStream_t rs = overlap ? d->route_stream : d->stream;
+    // the first pass into this scratch set may start once its previous reader (the
+    // k_tile kScratchSets draws back) is done
     if (overlap && S.main_reader_pending) {
         // everything enqueued on the main stream so far includes that last reader
         ZR_HIP(hipEventRecord(S.tile_done, d->stream));
         S.tile_done_valid = true;
         S.main_reader_pending = false;
     }
-    if (overlap && S.tile_done_valid) ZR_HIP(hipStreamWaitEvent(ss, S.tile_done, 0));
+    if (overlap && S.tile_done_valid) ZR_HIP(hipStreamWaitEvent(partitioned ? rs : ss, S.tile_done, 0));
     // debug early exits skip the self-reset at the end of k_setup_bin; the memsets
     // go on the stream that runs this draw's k_setup_bin, so they precede it
-    if (d->debug) {
-        ZR_HIP(hipMemsetAsync(P.counters, 0, kCtWords * 4, ss));
-        ZR_HIP(hipMemsetAsync(P.tile_counts, 0, (size_t)P.ntiles * 4, ss));
-    }
+    // (partitioned: after the route, which waited for the set's last reader)
+    auto debug_resets = [&]() -> zr_result {
+        if (d->debug) {
+            ZR_HIP(hipMemsetAsync(P.counters, 0, kCtWords * 4, ss));
+            ZR_HIP(hipMemsetAsync(P.tile_counts, 0, (size_t)P.ntiles * 4, ss));
+        }
+        return ZR_SUCCESS;
+    };
+    if (!partitioned && (rc = debug_resets())) return rc;
     if (partitioned) {
         const uint64_t bytes = (uint64_t)s.shard_count * route_block_bytes(P.route_cap);
         if ((rc = grow(d, S.xsend, S.xsend_cap, bytes, 1))) return rc;
@@ -898,7 +920,7 @@ zr_result exec_draw(zr_device* d, ExecState& s, const Cmd& c, bool indexed) {
         const uint64_t block = route_block_bytes(P.route_cap);
         const uint64_t layout = ((uint64_t)s.shard_count << 32) | P.route_cap;
         auto zero_headers = [&]() -> zr_result {
-            ZR_HIP(hipMemset2DAsync(S.xsend, block, 0, sizeof(RouteHeader), s.shard_count, ss));
+            ZR_HIP(hipMemset2DAsync(S.xsend, block, 0, sizeof(RouteHeader), s.shard_count, rs));
             return ZR_SUCCESS;
         };
         if (S.xsend_layout != layout) {
@@ -907,11 +929,11 @@ zr_result exec_draw(zr_device* d, ExecState& s, const Cmd& c, bool indexed) {
         }
         P.route_out = S.xsend;
         P.gids = S.gids;
-        timed_launch(d, "route", ss, [&] { launch_route(P, ss); });
+        timed_launch(d, "route", rs, [&] { launch_route(P, rs); });
         ZR_HIP(hipGetLastError());
         zr_result xr = ZR_SUCCESS;
-        timed_launch(d, "exchange", ss, [&] {
-            xr = s.exchange(s.exchange_user, (void*)ss, S.xsend, S.xrecv, route_block_bytes(P.route_cap));
+        timed_launch(d, "exchange", rs, [&] {
+            xr = s.exchange(s.exchange_user, (void*)rs, S.xsend, S.xrecv, route_block_bytes(P.route_cap));
         });
         if (xr != ZR_SUCCESS) {
             // the route's totals stay in the send headers (no records-mode setup will
@@ -925,12 +947,17 @@ zr_result exec_draw(zr_device* d, ExecState& s, const Cmd& c, bool indexed) {
             // joined back into the device stream like every other setup-stream pass, so
             // a fence (or a caller stream waiting on the device stream) covers the
             // route's reads of the caller's vertex and index buffers
-            ZR_HIP(hipEventRecord(S.setup_done, ss));
-            ZR_HIP(hipStreamWaitEvent(d->stream, S.setup_done, 0));
+            ZR_HIP(hipEventRecord(S.route_done, rs));
+            ZR_HIP(hipStreamWaitEvent(d->stream, S.route_done, 0));
             s.color_clear_pending = false;
             s.depth_clear_pending = false;
             return ZR_SUCCESS;
         }
+        if (rs != ss) {  // the binning stage waits for this draw's exchange
+            ZR_HIP(hipEventRecord(S.route_done, rs));
+            ZR_HIP(hipStreamWaitEvent(ss, S.route_done, 0));
+        }
+        if ((rc = debug_resets())) return rc;
         // Records-mode setup (binning the received records) runs on the setup
         // stream behind the exchange, so draw i+1's route, exchange and binning
         // overlap draw i's tile pass (the main stream only runs tile passes;
@@ -1081,6 +1108,7 @@ ZR_API zr_result zr_device_create(int32_t hip_device, zr_device** out) {
     if (const char* o = getenv("ZR_SETUP_OVERLAP")) d->setup_overlap = strtoul(o, nullptr, 0) != 0 ? 1 : 0;
     if (const char* rt = getenv("ZR_REC_TABLE")) d->rec_table = strtoul(rt, nullptr, 0) != 0 ? 1 : 0;
     if (const char* ts = getenv("ZR_TILE_SCHED")) d->tile_sched = strtoul(ts, nullptr, 0) != 0 ? 1 : 0;
+    if (const char* rw = getenv("ZR_REC_WGS")) d->rec_wgs = (uint32_t)strtoul(rw, nullptr, 0);
     if (const char* nt = getenv("ZR_TILE_NT")) {
         const unsigned long v = strtoul(nt, nullptr, 0);
         d->tile_threads = v >= 512 ? 512u : v ? 256u : 0u;
@@ -1089,6 +1117,7 @@ ZR_API zr_result zr_device_create(int32_t hip_device, zr_device** out) {
     ZR_HIP(hipStreamCreateWithFlags(&d->stream, hipStreamNonBlocking));
     d->own_stream = d->stream;
     ZR_HIP(hipStreamCreateWithFlags(&d->setup_stream, hipStreamNonBlocking));
+    ZR_HIP(hipStreamCreateWithFlags(&d->route_stream, hipStreamNonBlocking));
     for (uint32_t b : {1u, 2u, 4u})  // histograms + bbox array may exceed the 64 KB default
         ZR_HIP(hipFuncSetAttribute(setup_bin_kernel(b, false), hipFuncAttributeMaxDynamicSharedMemorySize,
                                    (int)kSetupLdsBudget));
@@ -1109,6 +1138,7 @@ ZR_API zr_result zr_device_create(int32_t hip_device, zr_device** out) {
 ZR_API void zr_device_destroy(zr_device* d) {
     if (!d) return;
     (void)hipSetDevice(d->hip_device);
+    (void)hipStreamSynchronize(d->route_stream);
     (void)hipStreamSynchronize(d->setup_stream);
     (void)hipStreamSynchronize(d->stream);
     collect_timings(d);
@@ -1121,6 +1151,7 @@ ZR_API void zr_device_destroy(zr_device* d) {
                         (void*)S.gids, (void*)S.tile_order})
             if (p) (void)hipFree(p);
         if (S.setup_done) (void)hipEventDestroy(S.setup_done);
+        if (S.route_done) (void)hipEventDestroy(S.route_done);
         if (S.tile_done) (void)hipEventDestroy(S.tile_done);
     }
     (void)hipHostFree(d->status_host);
@@ -1130,6 +1161,7 @@ ZR_API void zr_device_destroy(zr_device* d) {
     if (d->gather_stage) (void)hipFree(d->gather_stage);
     if (d->frame_done) (void)hipEventDestroy(d->frame_done);
     (void)hipStreamDestroy(d->setup_stream);
+    (void)hipStreamDestroy(d->route_stream);
     (void)hipStreamDestroy(d->own_stream);
     delete d;
 }
@@ -1984,6 +2016,17 @@ ZR_API zr_result zr_device_init_rccl(zr_device* d, const void* exchange_id, cons
 }
 
 ZR_API zr_exchange_fn zr_rccl_exchange_fn(void) { return &rccl_exchange; }
+
+static zr_result replay_exchange(void* user, void* stream, const void* send, void* recv, uint64_t bytes_per_rank) {
+    (void)send;
+    (void)bytes_per_rank;
+    const zr_replay_exchange* r = (const zr_replay_exchange*)user;
+    if (!r || !r->src) return fail(ZR_ERROR_VALIDATION_FAILED, "zr_replay_exchange_fn: no recorded buffer");
+    ZR_HIP(hipMemcpyAsync(recv, r->src, r->bytes, hipMemcpyDeviceToDevice, (hipStream_t)stream));
+    return ZR_SUCCESS;
+}
+
+ZR_API zr_exchange_fn zr_replay_exchange_fn(void) { return &replay_exchange; }
 
 ZR_API zr_result zr_device_gather_tile_rows(zr_device* d, zr_texture* t, int32_t root) {
     if (!d || !t) return fail(ZR_ERROR_VALIDATION_FAILED, "NULL argument");

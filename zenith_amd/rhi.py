@@ -625,6 +625,10 @@ class CommandEncoder:
         elif exchange == "rccl":  # the runtime's own all-to-all (RenderDevice.init_rccl)
             lib().zr_cmd_set_tile_shard_exchange(self.handle, rank, count, lib().zr_rccl_exchange_fn(),
                                                  self.device.handle)
+        elif hasattr(exchange, "native"):  # a runtime-side zr_exchange_fn and its user data
+            fn, user, keep = exchange.native()
+            self._keep.append(keep)
+            lib().zr_cmd_set_tile_shard_exchange(self.handle, rank, count, fn, user)
         else:
             cb = exchange.c_callback()
             self._keep.append(cb)  # the callback must outlive every submission of this list

@@ -177,6 +177,10 @@ class zr_rendering_info(C.Structure):
                 ("depth_attachment", C.POINTER(zr_rendering_attachment))]
 
 
+class zr_replay_exchange(C.Structure):
+    _fields_ = [("src", C.c_void_p), ("bytes", C.c_uint64)]
+
+
 # zr_exchange_fn (include/zenith_raster.h): (user, hip_stream, send, recv, bytes_per_rank) -> zr_result
 EXCHANGE_FN = C.CFUNCTYPE(C.c_int32, C.c_void_p, C.c_void_p, C.c_void_p, C.c_void_p, C.c_uint64)
 RCCL_ID_BYTES = 128
@@ -245,6 +249,7 @@ _SIGS = {
     "zr_rccl_get_unique_id": (_R, [_P]),
     "zr_device_init_rccl": (_R, [_P, _P, _P, C.c_int32, C.c_int32]),
     "zr_rccl_exchange_fn": (_P, []),
+    "zr_replay_exchange_fn": (_P, []),
     "zr_device_gather_tile_rows": (_R, [_P, _P, C.c_int32]),
     "zr_fence_create": (_R, [_P, C.POINTER(_P)]),
     "zr_fence_destroy": (None, [_P]),
