@@ -269,6 +269,8 @@ def lib():
             raise ImportError(f"{LIB_PATH} is missing: run __graft_entry__.build() (make -C zenith_amd)")
         L = C.CDLL(LIB_PATH, mode=C.RTLD_GLOBAL)
         for name, (res, args) in _SIGS.items():
+            if os.environ.get("ZR_LIB_PATH") and not hasattr(L, name):
+                continue  # an older build under A/B (tools/ab.sh): bind what it has
             fn = getattr(L, name)
             fn.restype = res
             fn.argtypes = args
