@@ -35,14 +35,19 @@ def main():
     from zenith_amd import renderer, rhi, scenes
     scene = scenes.config_scene(a.config)
     dev = rhi.RenderDevice(0)
-    renderer.render_scene(dev, scene, shard=tuple(a.shard) if a.shard else None, frames=a.frames)
+    sh = tuple(a.shard) if a.shard else None
+    # a first frame sizes the scratch (a tile list longer than its slab takes the
+    # slow all-records scan until the runtime grows the bins at a sync point)
+    renderer.render_scene(dev, scene, shard=sh, frames=1)
+    renderer.render_scene(dev, scene, shard=sh, frames=a.frames)
     dev.close()
     rows = list(csv.reader(open(ts + ".tiles.csv")))
     # the csv holds one block per sync point, each starting with a header: keep the last
     starts = [i for i, r in enumerate(rows) if r and r[0] == "tile"]
     last = rows[starts[-1] + 1:]
-    t = np.array([[float(x) for x in r[1:6]] for r in last])  # t0 start, t1 init, t2 sorted, t3 raster, t4 resolve
+    t = np.array([[float(x) for x in r[1:7]] for r in last])  # t0 start, t1 init, t2 sorted, t3 raster, t4 resolve, t5 chunks
     cnt = np.array([int(r[8]) for r in last])
+    nbig = np.array([int(r[7]) for r in last])
     dur = t[:, 4] - t[:, 0]
     print(f"{a.config} shard {a.shard}: {len(t)} tiles, pass span {t[:, 4].max() - t[:, 0].min():.1f} us, "
           f"tile {dur.mean():.1f} us avg (p10 {np.percentile(dur, 10):.1f}, p90 {np.percentile(dur, 90):.1f}, "
@@ -52,8 +57,15 @@ def main():
         print(f"  {name:8s} avg {d.mean():6.2f}  p90 {np.percentile(d, 90):6.2f}  max {d.max():6.2f} us")
     print(f"  starts: first {t[:, 0].min():.1f}, last {t[:, 0].max():.1f}; ends: first {t[:, 4].min():.1f}, "
           f"last {t[:, 4].max():.1f} us; list length avg {cnt.mean():.0f} max {cnt.max()}")
-    heavy = np.argsort(-dur)[:5]
-    print("  slowest tiles:", ", ".join(f"#{k} {dur[k]:.1f} us ({cnt[k]} entries)" for k in heavy))
+    heavy = np.argsort(-dur)[:8]
+    steps = np.array([int(r[9]) for r in last])   # ZR_TILE_WORK_STATS builds: longest lane walks of the chunks
+    sweeps = np.array([int(r[10]) for r in last])  # and wave-path sweeps
+    print("  slowest tiles:")
+    for k in heavy:
+        ph = " ".join(f"{n} {t[k, j] - t[k, i]:.1f}" for n, i, j in (("init", 0, 1), ("sort", 1, 2), ("raster", 2, 3),
+                                                                       ("resolve", 3, 4)))
+        print(f"    #{k} {dur[k]:.1f} us, {cnt[k]} entries ({nbig[k]} wave-path), lane steps {steps[k]}, "
+              f"wave sweeps {sweeps[k]}, start {t[k, 0]:.1f}: {ph}, chunks end {t[k, 5] - t[k, 2]:.1f} after sort")
 
 
 if __name__ == "__main__":
