@@ -23,7 +23,10 @@ def main():
     p.add_argument("--shard", nargs=2, type=int, default=None)
     p.add_argument("--frames", type=int, default=3)
     p.add_argument("--out", required=True)
+    p.add_argument("--from-csv", action="store_true", help="report an existing <out>.tiles.csv (no GPU)")
     a = p.parse_args()
+    if a.from_csv:
+        return report(a, os.path.abspath(a.out))
     os.makedirs(os.path.dirname(a.out) or ".", exist_ok=True)
     ts = os.path.abspath(a.out)
     for f in (ts, ts + ".tiles.csv"):
@@ -41,6 +44,10 @@ def main():
     renderer.render_scene(dev, scene, shard=sh, frames=1)
     renderer.render_scene(dev, scene, shard=sh, frames=a.frames)
     dev.close()
+    report(a, ts)
+
+
+def report(a, ts):
     rows = list(csv.reader(open(ts + ".tiles.csv")))
     # the csv holds one block per sync point, each starting with a header: keep the last
     starts = [i for i, r in enumerate(rows) if r and r[0] == "tile"]

@@ -60,7 +60,9 @@ static_assert(sizeof(TriRecord) == 64, "TriRecord must be 64 B");
 // depth terms, and 1/A2 with the orientation swap (kFlagSwapped) in its sign bit
 // (A2 > 0 after orientation, so the bit is free).  Bias flags and the pixel bbox
 // are recomputed from the vertices.  A primitive too large for int16 deltas has
-// dx1 == kCompactLarge and its full TriRecord in records_big.
+// dx1 == kCompactLarge and its full TriRecord in records_big; its dy1 is 1 when it
+// covers at most a quarter of its bbox (a sliver, which k_tile's lane walk takes
+// in any cost bucket), else 0.
 struct alignas(16) TriCompact {
     int32_t X0, Y0;
     int16_t dx1, dy1, dx2, dy2;

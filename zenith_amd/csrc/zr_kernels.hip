@@ -41,6 +41,9 @@ namespace zr {
 #ifndef ZR_XCD_TILES
 #define ZR_XCD_TILES 8       // tiles per XCD run (xcd_tile); 0 or 1: blockIdx order
 #endif
+#ifndef ZR_LARGE_LANES
+#define ZR_LARGE_LANES 1     // 0: every large primitive takes k_tile's wave path; 2: the last cost bucket's too (A/B)
+#endif
 #ifndef ZR_TAB
 #define ZR_TAB 1
 #endif
@@ -579,6 +582,9 @@ __device__ __forceinline__ uint32_t count_owned(const DrawParams& P, const PrimG
 
 // A compact record (as two 16-B words) whose primitive is too large for int16 deltas.
 __device__ __forceinline__ bool compact_is_large(const int4 q0) { return (int16_t)(q0.z & 0xFFFF) == kCompactLarge; }
+// A large primitive covering at most a quarter of its bbox (dy1 == 1 in its
+// compact record; the lane walk takes it even in the last cost bucket, k_tile).
+__device__ __forceinline__ bool compact_is_sliver(const int4 q0) { return (q0.z >> 16) == 1; }
 
 // The compact record and the clipped pixel bbox of a set-up triangle.
 __device__ __forceinline__ TriCompact make_compact(const PrimGeom& g, BBox& box) {
@@ -589,7 +595,9 @@ __device__ __forceinline__ TriCompact make_compact(const PrimGeom& g, BBox& box)
     TriCompact c;
     c.X0 = X[0]; c.Y0 = Y[0];
     c.dx1 = small ? (int16_t)(X[1] - X[0]) : kCompactLarge;
-    c.dy1 = small ? (int16_t)(Y[1] - Y[0]) : (int16_t)0;
+    const long long bbox = (long long)(max(X[0], max(X[1], X[2])) - min(X[0], min(X[1], X[2]))) *
+                           (max(Y[0], max(Y[1], Y[2])) - min(Y[0], min(Y[1], Y[2])));
+    c.dy1 = small ? (int16_t)(Y[1] - Y[0]) : (int16_t)(bbox >= 2 * g.A2 ? 1 : 0);  // large: the sliver flag
     c.dx2 = small ? (int16_t)(X[2] - X[0]) : (int16_t)0;
     c.dy2 = small ? (int16_t)(Y[2] - Y[0]) : (int16_t)0;
     c.z0 = g.z[0];
@@ -1209,6 +1217,24 @@ __device__ __forceinline__ int rl(int v, uint32_t lane) { return __builtin_amdgc
 // the raster and resolve use: vertices, depth terms, |1/A2|, kFlagSmall/Swapped,
 // and with `full` also the top-left bias flags and the clipped pixel bbox, computed
 // exactly as k_setup_bin computed them.  v0..v2 are not part of the compact form.
+// The top-left bias flags and the clipped pixel bbox of a record's vertices,
+// computed exactly as k_setup_bin computed them.
+__device__ __forceinline__ void finish_record(const DrawParams& P, TriRecord& r) {
+    const int X[3] = {r.X0, r.X1, r.X2}, Y[3] = {r.Y0, r.Y1, r.Y2};
+#pragma unroll
+    for (int i = 0; i < 3; ++i) {  // top-left rule (y-down), edge i opposite vertex i
+        const int a = (i + 1) % 3, b = (i + 2) % 3;
+        const int dx = X[b] - X[a], dy = Y[b] - Y[a];
+        if (!((dy < 0) || (dy == 0 && dx > 0))) r.flags |= (kFlagBias0 << i);
+    }
+    const int minX = min(X[0], min(X[1], X[2])), maxX = max(X[0], max(X[1], X[2]));
+    const int minY = min(Y[0], min(Y[1], Y[2])), maxY = max(Y[0], max(Y[1], Y[2]));
+    const int px0 = max((minX - 128 + 255) >> 8, P.clip_x0), px1 = min((maxX - 128) >> 8, P.clip_x1);
+    const int py0 = max((minY - 128 + 255) >> 8, P.clip_y0), py1 = min((maxY - 128) >> 8, P.clip_y1);
+    r.bb0 = (uint32_t)px0 | ((uint32_t)py0 << 16);
+    r.bb1 = (uint32_t)px1 | ((uint32_t)py1 << 16);
+}
+
 __device__ __forceinline__ TriRecord decode_compact(const DrawParams& P, const int4 q0, const int4 q1, bool full) {
     TriRecord r;
     r.X0 = q0.x; r.Y0 = q0.y;
@@ -1216,26 +1242,48 @@ __device__ __forceinline__ TriRecord decode_compact(const DrawParams& P, const i
     r.X2 = q0.x + (int)(int16_t)(q0.w & 0xFFFF); r.Y2 = q0.y + (q0.w >> 16);
     r.z0 = __int_as_float(q1.x); r.dz1 = __int_as_float(q1.y); r.dz2 = __int_as_float(q1.z);
     r.invA2 = fabsf(__int_as_float(q1.w));
-    uint32_t flags = kFlagSmall | ((q1.w < 0) ? kFlagSwapped : 0u);
+    r.flags = kFlagSmall | ((q1.w < 0) ? kFlagSwapped : 0u);
     r.v0 = r.v1 = r.v2 = 0u;
     r.bb0 = r.bb1 = 0u;
-    if (full) {
-        const int X[3] = {r.X0, r.X1, r.X2}, Y[3] = {r.Y0, r.Y1, r.Y2};
-#pragma unroll
-        for (int i = 0; i < 3; ++i) {  // top-left rule (y-down), edge i opposite vertex i
-            const int a = (i + 1) % 3, b = (i + 2) % 3;
-            const int dx = X[b] - X[a], dy = Y[b] - Y[a];
-            if (!((dy < 0) || (dy == 0 && dx > 0))) flags |= (kFlagBias0 << i);
-        }
-        const int minX = min(X[0], min(X[1], X[2])), maxX = max(X[0], max(X[1], X[2]));
-        const int minY = min(Y[0], min(Y[1], Y[2])), maxY = max(Y[0], max(Y[1], Y[2]));
-        const int px0 = max((minX - 128 + 255) >> 8, P.clip_x0), px1 = min((maxX - 128) >> 8, P.clip_x1);
-        const int py0 = max((minY - 128 + 255) >> 8, P.clip_y0), py1 = min((maxY - 128) >> 8, P.clip_y1);
-        r.bb0 = (uint32_t)px0 | ((uint32_t)py0 << 16);
-        r.bb1 = (uint32_t)px1 | ((uint32_t)py1 << 16);
-    }
-    r.flags = flags;
+    if (full) finish_record(P, r);
     return r;
+}
+
+// A compact record for the lane walk; for a large primitive (large: its compact
+// record holds vertex 0, the depth terms and |1/A2|, the same values as its full
+// record) with vertices 1 and 2 from records_big (X1, Y1, X2, Y2: bytes 8-23).
+// Biases and bbox as setup computed them.
+__device__ __forceinline__ TriRecord decode_large(const DrawParams& P, const int4 q0, const int4 q1, bool large,
+                                                  const int2 v1, const int2 v2) {
+    TriRecord r;
+    r.X0 = q0.x; r.Y0 = q0.y;
+    r.X1 = large ? v1.x : q0.x + (int)(int16_t)(q0.z & 0xFFFF); r.Y1 = large ? v1.y : q0.y + (q0.z >> 16);
+    r.X2 = large ? v2.x : q0.x + (int)(int16_t)(q0.w & 0xFFFF); r.Y2 = large ? v2.y : q0.y + (q0.w >> 16);
+    r.z0 = __int_as_float(q1.x); r.dz1 = __int_as_float(q1.y); r.dz2 = __int_as_float(q1.z);
+    r.invA2 = fabsf(__int_as_float(q1.w));
+    r.flags = (q1.w < 0) ? kFlagSwapped : 0u;
+    r.v0 = r.v1 = r.v2 = 0u;
+    finish_record(P, r);
+    return r;
+}
+
+// Whether the lane walk (raster_lane) is exact for a large primitive in this
+// tile: every edge value it tests, over bbox ∩ tile widened by the pair walk's
+// one column on either side, must fit int32.  The edge functions are linear, so
+// their extremes are at the rectangle's corners: |w| <= |w(corner)| + |dy| 256 W
+// + |dx| 256 H, bounded in int64 against 2^31 - 1.
+__device__ __forceinline__ bool lane_walk_fits(const TriRecord& r, int x0, int y0) {
+    const int bx0 = max((int)(r.bb0 & 0xFFFFu), x0) - 1, by0 = max((int)(r.bb0 >> 16), y0);
+    const int bx1 = min((int)(r.bb1 & 0xFFFFu), x0 + kTile - 1) + 1, by1 = min((int)(r.bb1 >> 16), y0 + kTile - 1);
+    const long long Sx = (long long)bx0 * 256 + 128, Sy = (long long)by0 * 256 + 128;
+    const long long Wd = (long long)(bx1 - bx0) * 256, Hd = (long long)max(by1 - by0, 0) * 256;
+    auto edge = [&](int Xa, int Ya, int Xb, int Yb) {
+        const long long dx = (long long)Xb - Xa, dy = (long long)Yb - Ya;
+        const long long w = dx * (Sy - Ya) - dy * (Sx - Xa);
+        return llabs(w) + llabs(dy) * Wd + llabs(dx) * Hd;
+    };
+    const long long m = max(edge(r.X1, r.Y1, r.X2, r.Y2), max(edge(r.X2, r.Y2, r.X0, r.Y0), edge(r.X0, r.Y0, r.X1, r.Y1)));
+    return m < 0x7FFFFFFFll;
 }
 
 // A wave-uniform full record, moved to scalar registers right after the load so
@@ -1280,20 +1328,26 @@ __device__ __forceinline__ void raster_prim(const DrawParams& P, const TriRecord
     const int lx = lane & ((1 << sh) - 1), lyo = lane >> sh;
     const long long bias0 = (r.flags >> 1) & 1, bias1 = (r.flags >> 2) & 1, bias2 = (r.flags >> 3) & 1;
     const DepthPlane dp = depth_plane(r.z0, r.dz1, r.dz2, r.invA2, (int)bias1, (int)bias2);
+    const float dlo = P.dlo, dhi = P.dhi;  // (held: a per-pass kernarg reload waits on the scalar cache)
+    // The lane's biased edge values at its first pixel, then stepped by `rows`
+    // pixel rows per pass in int64 (exact; a pass was two int64 products per edge.
+    // Stepping in double measured slower: cerberus 48.5 -> 51.3 us)
+    const EdgeEval e = eval_edges(r, bx0 + lx, by0 + lyo);
+    long long w0 = e.w0 - bias0, w1 = e.w1 - bias1, w2 = e.w2 - bias2;
+    const long long s0 = (long long)(r.X2 - r.X1) * (256 * rows), s1 = (long long)(r.X0 - r.X2) * (256 * rows);
+    const long long s2 = (long long)(r.X1 - r.X0) * (256 * rows);
     for (int ry = 0; ry < bh; ry += rows) {
         const int ly = ry + lyo;
-        if (lx < bw && ly < bh) {
-            const int px = bx0 + lx, py = by0 + ly;
-            const EdgeEval e = eval_edges(r, px, py);
-            if (e.w0 >= bias0 && e.w1 >= bias1 && e.w2 >= bias2) {
-                const float z = plane_z(dp, (float)(e.w1 - bias1), (float)(e.w2 - bias2));
-                if (z >= P.dlo && z <= P.dhi) {
-                    const int li = (py - y0) * kTile + (px - x0);
-                    if (!INITD || depth_pass(P.depth_op, z, s_initd[li]))
-                        atomicMin(&s_key[li], frag_key<MODE>(z, seq));
-                }
+        if (lx < bw && ly < bh && (w0 | w1 | w2) >= 0) {
+            const float z = plane_z(dp, (float)w1, (float)w2);
+            if (z >= dlo && z <= dhi) {
+                const int li = (by0 + ly - y0) * kTile + (bx0 + lx - x0);
+                if (!INITD || depth_pass(P.depth_op, z, s_initd[li])) atomicMin(&s_key[li], frag_key<MODE>(z, seq));
             }
         }
+        w0 += s0;
+        w1 += s1;
+        w2 += s2;
     }
 }
 
@@ -1333,13 +1387,19 @@ __device__ __forceinline__ void raster_lane(const DrawParams& P, const TriRecord
             }
         }
     }
+    // Edge values and steps in arithmetic mod 2^32 (u32 products and sums): exact
+    // wherever the true value fits int32, which holds at every sample the walk
+    // tests -- a small primitive's |w| <= 2^29, a large one is sent here only when
+    // lane_walk_fits bounds its values over bbox ∩ tile -- whatever the steps'
+    // own magnitudes (a row wrap's jump may exceed int32; the sum it lands on does not).
+    auto wr = [](uint32_t a) { return (int)a; };
     const int Sx = bx0 * 256 + 128, Sy = (by0 + sub) * 256 + 128;
-    const int dx0 = X2 - X1, dy0 = Y2 - Y1, dx1 = X0 - X2, dy1 = Y0 - Y2, dx2 = X1 - X0, dy2 = Y1 - Y0;
-    int r0 = dx0 * (Sy - Y1) - dy0 * (Sx - X1);
-    int r1 = dx1 * (Sy - Y2) - dy1 * (Sx - X2);
-    int r2 = dx2 * (Sy - Y0) - dy2 * (Sx - X0);
-    const int sx0 = -dy0 * 256, sx1 = -dy1 * 256, sx2 = -dy2 * 256;  // +1 pixel in x
-    const int sy0 = dx0 * 256, sy1 = dx1 * 256, sy2 = dx2 * 256;     // +1 pixel in y
+    const uint32_t dx0 = X2 - X1, dy0 = Y2 - Y1, dx1 = X0 - X2, dy1 = Y0 - Y2, dx2 = X1 - X0, dy2 = Y1 - Y0;
+    int r0 = wr(dx0 * (uint32_t)(Sy - Y1) - dy0 * (uint32_t)(Sx - X1));
+    int r1 = wr(dx1 * (uint32_t)(Sy - Y2) - dy1 * (uint32_t)(Sx - X2));
+    int r2 = wr(dx2 * (uint32_t)(Sy - Y0) - dy2 * (uint32_t)(Sx - X0));
+    const int sx0 = wr(0u - dy0 * 256u), sx1 = wr(0u - dy1 * 256u), sx2 = wr(0u - dy2 * 256u);  // +1 pixel in x
+    const int sy0 = wr(dx0 * 256u), sy1 = wr(dx1 * 256u), sy2 = wr(dx2 * 256u);                 // +1 pixel in y
     const int b0 = (int)((flags >> 1) & 1u), b1 = (int)((flags >> 2) & 1u), b2 = (int)((flags >> 3) & 1u);
     // Sweep the bbox in row order, stepping the edge values: +sx per pixel, and at
     // the end of a row the jump back to the next row's first pixel, chosen with
@@ -1351,7 +1411,7 @@ __device__ __forceinline__ void raster_lane(const DrawParams& P, const TriRecord
     // per-fragment -0 -> +0 rule therefore gives the same bits).  The sweep ends when the key address reaches the row after the
     // last one (no separate step counter).
     const int rows = (bh - sub + k - 1) >> ksh;
-    int w0 = r0 - b0, w1 = r1 - b1, w2 = r2 - b2;
+    int w0 = wr((uint32_t)r0 - b0), w1 = wr((uint32_t)r1 - b1), w2 = wr((uint32_t)r2 - b2);
     int ex = 0;
     uint32_t la = (uint32_t)(((by0 + sub - y0) * kTile + (bx0 - x0)) * 8);  // byte offset of the key
     const uint32_t la_end = la + (uint32_t)(rows * k * kTile * 8);
@@ -1374,19 +1434,20 @@ __device__ __forceinline__ void raster_lane(const DrawParams& P, const TriRecord
     // samples).  The second pixel of a row's last pair lies past an odd-width
     // bbox and is skipped (pair index lastB).
     const int hw = (bw + 1) >> 1, lastB = chk ? hw - 1 : hw;
-    const int t0 = 2 * sx0, t1 = 2 * sx1, t2 = 2 * sx2;
-    const int q0 = k * sy0 - 2 * (hw - 1) * sx0, q1 = k * sy1 - 2 * (hw - 1) * sx1, q2 = k * sy2 - 2 * (hw - 1) * sx2;
+    const int t0 = wr(2u * sx0), t1 = wr(2u * sx1), t2 = wr(2u * sx2);
+    const uint32_t kk = (uint32_t)k, hh = 2u * (uint32_t)(hw - 1);
+    const int q0 = wr(kk * sy0 - hh * sx0), q1 = wr(kk * sy1 - hh * sx1), q2 = wr(kk * sy2 - hh * sx2);
     const uint32_t lq = (uint32_t)((k * kTile - 2 * (hw - 1)) * 8);
     auto sweep = [&](auto ztest, auto wchk) {
         do {
             if ((w0 | w1 | w2) >= 0) frag(ztest, w1, w2, la);
-            const int v0 = w0 + sx0, v1 = w1 + sx1, v2 = w2 + sx2;
+            const int v0 = wr((uint32_t)w0 + sx0), v1 = wr((uint32_t)w1 + sx1), v2 = wr((uint32_t)w2 + sx2);
             if ((!decltype(wchk)::value || ex != lastB) && (v0 | v1 | v2) >= 0) frag(ztest, v1, v2, la + 8u);
             const bool wrap = ++ex == hw;
             ex = wrap ? 0 : ex;
-            w0 += wrap ? q0 : t0;
-            w1 += wrap ? q1 : t1;
-            w2 += wrap ? q2 : t2;
+            w0 = wr((uint32_t)w0 + (wrap ? q0 : t0));
+            w1 = wr((uint32_t)w1 + (wrap ? q1 : t1));
+            w2 = wr((uint32_t)w2 + (wrap ? q2 : t2));
             la += wrap ? lq : 16u;
         } while (la != la_end);
     };
@@ -2190,6 +2251,22 @@ __global__ __launch_bounds__(NT, kTileWgs * kTileThreads / 256) void k_tile(Draw
                 const bool valid = j < n && !(tile_debug(P) & kDebugLoadOnly);
                 if (tile_debug(P) & kDebugLoadOnly) asm volatile("" ::"v"(q0.x), "v"(q1.x), "v"(my_prim));
                 const bool large = compact_is_large(q0);
+                // A large primitive below the last cost bucket (bbox ∩ tile under ~253
+                // px) takes the lane walk too when its edge values there fit int32
+                // (lane_walk_fits): a wave-path sweep spends ~100 instructions of setup
+                // per primitive, and sliver-heavy tiles queue hundreds of primitives with
+                // a few dozen covered pixels each (cerberus: tile pass 42.6 -> 26.9 us).
+                // Its other two vertices come from records_big.  The last bucket stays on
+                // the wave path, which covers a large part of the tile in fewer
+                // instructions (all large primitives walked: C3 tile pass +4.7 us).
+                bool walk = valid && !large;
+                int2 v1 = make_int2(0, 0), v2 = v1;
+                if (valid && large && (!gb || compact_is_sliver(q0) || ZR_LARGE_LANES >= 2) && ZR_LARGE_LANES) {
+                    const int2* vp = reinterpret_cast<const int2*>(P.records_big + my_prim) + 1;
+                    v1 = vp[0];
+                    v2 = vp[1];
+                    walk = lane_walk_fits(decode_large(P, q0, q1, true, v1, v2), x0, y0);
+                }
                 if (tab && valid && sub == 0) {
                     if (!large) {
                         rec_table_insert(s_thash, s_trec, my_prim, j, q0, q1, x0, y0);
@@ -2202,10 +2279,9 @@ __global__ __launch_bounds__(NT, kTileWgs * kTileThreads / 256) void k_tile(Draw
                         s_trec[j] = make_int4(0, q0.z, 0, 0);
                     }
                 }
-                if (valid && !large && !(tile_debug(P) & kDebugSkipLanePath)) {
-                    const TriRecord r = decode_compact(P, q0, q1, true);
-                    raster_lane<MODE, INITD>(P, r, entry_seq<PROG>(P, my_prim), x0, y0, s_key, s_initd, sub, (int)ksh);
-                }
+                if (walk && !(tile_debug(P) & kDebugSkipLanePath))
+                    raster_lane<MODE, INITD>(P, decode_large(P, q0, q1, large, v1, v2), entry_seq<PROG>(P, my_prim), x0, y0,
+                                             s_key, s_initd, sub, (int)ksh);
                 if (ZR_TILE_WORK_STATS && (tile_debug(P) & kDebugStamps)) {  // work of the chunk: its longest lane walk
                     int steps = 0;
                     if (valid && !large) {
@@ -2220,7 +2296,7 @@ __global__ __launch_bounds__(NT, kTileWgs * kTileThreads / 256) void k_tile(Draw
                 }
                 // large primitives: queued for the segment's wave pass; the whole
                 // wave sweeps them itself only when the queue is full
-                const bool is_big = valid && large && sub == 0;
+                const bool is_big = valid && large && !walk && sub == 0;
                 unsigned long long big = __ballot(is_big);
                 if (big) {
                     uint32_t base = 0;
@@ -2243,6 +2319,10 @@ __global__ __launch_bounds__(NT, kTileWgs * kTileThreads / 256) void k_tile(Draw
             }
             __syncthreads();
             const uint32_t nbig = min(s_nbig, kBigQueue);
+            if (stamp && NT >= 512 && seg == 0) {  // first segment: chunks done, wave-path queue length
+                ts[5] = __builtin_amdgcn_s_memrealtime();
+                ts[6] = (unsigned long long)s_nbig << 32;
+            }
             for (;;) {  // the segment's queued wave-path primitives, two per claim
                 uint32_t i = 0;
                 if (lane == 0) i = atomicAdd(&s_bclaim, 2u);
@@ -2251,7 +2331,9 @@ __global__ __launch_bounds__(NT, kTileWgs * kTileThreads / 256) void k_tile(Draw
                 const bool two = i + 1u < nbig;
                 const uint32_t e0 = s_big[i], e1 = two ? s_big[i + 1u] : e0;
                 // both full records' loads in flight at once (one exposed latency per
-                // claim), the second held in scalar registers
+                // claim), the second held in scalar registers.  (Staging the segment's
+                // queued records in LDS with one workgroup-wide load: cerberus -0.8 us,
+                // C2 +0.9, C3 +2.6.)
                 const int4* a = reinterpret_cast<const int4*>(P.records_big + e0);
                 const int4* b = reinterpret_cast<const int4*>(P.records_big + e1);
                 const int4 a0 = a[0], a1 = a[1], a2 = a[2], a3 = a[3];
@@ -2318,8 +2400,8 @@ __global__ __launch_bounds__(NT, kTileWgs * kTileThreads / 256) void k_tile(Draw
         ts[4] = __builtin_amdgcn_s_memrealtime();
         ts[7] = ((unsigned long long)s_dbg[1] << 32) | s_dbg[0];
         if (NT >= 512) {  // (resolve_tile's own stamps use these two at 256 threads)
-            ts[5] = 0ull;
-            ts[6] = count;  // the tile's list length (tools/tile_stamps.py)
+            if (!count) ts[5] = ts[2] = ts[1];  // no segment ran
+            ts[6] = (ts[6] & ~0xFFFFFFFFull) | count;  // the tile's list length (tools/tile_stamps.py)
         }
     }
 }

@@ -439,12 +439,14 @@ void dump_stamps(zr_device* d) {
             if (g) {
                 unsigned long long t1 = ~0ull;
                 for (uint32_t w = 0; w < d->dbg_tiles; ++w) t1 = std::min(t1, tt[w * 8]);
-                fprintf(g, "tile,t0,t1,t2,t3,t4,hwid,xcc,count,lane_steps,wave_sweeps\n");
+                fprintf(g, "tile,t0,t1,t2,t3,t4,t5,nbig,count,lane_steps,wave_sweeps\n");
                 for (uint32_t w = 0; w < d->dbg_tiles; ++w) {
                     fprintf(g, "%u", w);
                     for (int i = 0; i <= 4; ++i) fprintf(g, ",%.2f", (double)(tt[w * 8 + i] - t1) * 0.01);
-                    fprintf(g, ",%llu,%llu,%llu,%llu,%llu\n", tt[w * 8 + 5] & 0xFFFFFFFFull, tt[w * 8 + 5] >> 32, tt[w * 8 + 6],
-                            tt[w * 8 + 7] & 0xFFFFFFFFull, tt[w * 8 + 7] >> 32);
+                    // 512-thread tiles: t5 = the first segment's chunks done, nbig = its
+                    // wave-path queue (256: resolve_tile's own stamps, in t5 / the count word)
+                    fprintf(g, ",%.2f,%llu,%llu,%llu,%llu\n", (double)(tt[w * 8 + 5] - t1) * 0.01, tt[w * 8 + 6] >> 32,
+                            tt[w * 8 + 6] & 0xFFFFFFFFull, tt[w * 8 + 7] & 0xFFFFFFFFull, tt[w * 8 + 7] >> 32);
                 }
                 fclose(g);
             }
