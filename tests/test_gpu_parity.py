@@ -102,6 +102,48 @@ def test_large_triangles_wave_path(device):
     assert_parity(device, s)
 
 
+@pytest.mark.parametrize("seed", [0, 1])
+def test_large_slivers_lane_walk(device, seed):
+    """Long thin triangles (20 px to ~20,000 px, most of them past the screen, 0.5-6
+    px wide, every orientation, some fanned around a shared vertex): large
+    primitives that k_tile's lane walk takes tile by tile when their edge values
+    there fit int32 (lane_walk_fits) and the wave path takes elsewhere."""
+    g = np.random.default_rng(40 + seed)
+    W, H, n = 1024, 768, 2400
+    c = g.uniform(-1.2, 1.2, (n, 2))
+    ang = g.uniform(0, 2 * np.pi, n)
+    length = np.exp(g.uniform(np.log(20.0), np.log(20000.0), n)) / (W / 2)   # NDC units
+    width = g.uniform(0.5, 6.0, n) / (H / 2)
+    d = np.stack([np.cos(ang), np.sin(ang)], 1)
+    nrm = np.stack([-d[:, 1], d[:, 0]], 1)
+    p0 = c - d * length[:, None] / 2
+    p1 = c + d * length[:, None] / 2
+    p2 = c + nrm * width[:, None] * g.choice([-1.0, 1.0], (n, 1))
+    fan = g.random(n) < 0.2  # slivers sharing vertex 0 (a cap's spokes)
+    p0[fan] = np.array([0.1, -0.05])
+    z = g.uniform(0.05, 0.95, (n, 3))
+    pos = np.stack([p0, p1, p2], 1)
+    verts = np.concatenate([pos, z[..., None], g.uniform(0, 1, (n, 3, 3))], axis=2).reshape(-1, 6)
+    s = scenes.Scene(f"slivers_{seed}", W, H, scenes.PROGRAM_FLAT_COLOR, verts.astype(np.float32),
+                     np.arange(3 * n, dtype=np.uint32), depth=True)
+    assert_parity(device, s)
+
+
+def test_wave_queue_overflow(device):
+    """More large primitives in one tile segment than k_tile's wave-path queue
+    holds (kBigQueue = 512): 1100 screen-covering triangles, none a sliver, so
+    every tile's batch straddles the queue's end and the waves sweep the rest
+    themselves (a straddling batch once left queue slots unfilled)."""
+    g = np.random.default_rng(77)
+    n = 1100
+    pos = g.uniform(-3.0, 3.0, (n, 3, 2))
+    z = g.uniform(0.0, 1.0, (n, 3, 1))
+    verts = np.concatenate([pos, z, g.uniform(0, 1, (n, 3, 3))], axis=2).reshape(-1, 6)
+    s = scenes.Scene("wave_queue_overflow", 256, 192, scenes.PROGRAM_FLAT_COLOR, verts.astype(np.float32),
+                     np.arange(3 * n, dtype=np.uint32), depth=True)
+    assert_parity(device, s)
+
+
 def test_mixed_sizes(device):
     a = scenes.soup_scene(14, 1500, 300, 200, 6.0, scenes.PROGRAM_FLAT_COLOR)
     b = scenes.soup_scene(15, 60, 300, 200, 120.0, scenes.PROGRAM_FLAT_COLOR)

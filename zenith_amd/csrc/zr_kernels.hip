@@ -2299,14 +2299,18 @@ __global__ __launch_bounds__(NT, kTileWgs * kTileThreads / 256) void k_tile(Draw
                 const bool is_big = valid && large && !walk && sub == 0;
                 unsigned long long big = __ballot(is_big);
                 if (big) {
+                    // The wave's batch takes the queue's free slots from `base` on; the
+                    // part past its end stays with this wave.  (s_nbig counts every
+                    // primitive offered, so the wave pass reads min(s_nbig, kBigQueue)
+                    // slots, and each of them must be filled: a batch straddling the end
+                    // fills the last slots.)
                     uint32_t base = 0;
                     if (lane == 0) base = atomicAdd(&s_nbig, (uint32_t)__popcll(big));
                     base = (uint32_t)__builtin_amdgcn_readfirstlane((int)base);
-                    if (base + (uint32_t)__popcll(big) <= kBigQueue) {
-                        if (is_big)
-                            s_big[base + (uint32_t)__popcll(big & ((1ull << lane) - 1ull))] = my_prim;
-                        big = 0;
-                    }
+                    const uint32_t room = base < kBigQueue ? min((uint32_t)__popcll(big), kBigQueue - base) : 0u;
+                    const uint32_t rank = (uint32_t)__popcll(big & ((1ull << lane) - 1ull));
+                    if (is_big && rank < room) s_big[base + rank] = my_prim;
+                    for (uint32_t q = 0; q < room; ++q) big &= big - 1ull;  // the queued ones (lowest lanes)
                 }
                 while (big) {
                     const uint32_t i = (uint32_t)__builtin_ctzll(big);
