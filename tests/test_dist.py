@@ -170,7 +170,7 @@ def test_route_model_matches_device_constants():
     import re
     from zenith_amd import shard
     src = open(os.path.join(ROOT, "zenith_amd", "csrc", "zr_internal.h")).read()
-    assert int(re.search(r"kRouteChunk\s*=\s*(\d+)", src).group(1)) == shard.ROUTE_CHUNK
+    assert int(re.search(r"#define ZR_ROUTE_CHUNK (\d+)", src).group(1)) == shard.ROUTE_CHUNK
     assert 'sizeof(RouteEntry) == 48' in src and 'sizeof(RouteHeader) == 16' in src
     rt = open(os.path.join(ROOT, "zenith_amd", "csrc", "zr_runtime.cpp")).read()
     assert "std::min<uint64_t>(span, (2 * span + G - 1) / G + 4096)" in rt and "if (G <= 2) return span;" in rt

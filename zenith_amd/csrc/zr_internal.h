@@ -162,8 +162,11 @@ struct alignas(16) RouteHeader {
 };
 static_assert(sizeof(RouteHeader) == 16, "RouteHeader must be 16 B");
 __host__ __device__ inline uint64_t route_block_bytes(uint32_t cap) { return sizeof(RouteHeader) + (uint64_t)cap * sizeof(RouteEntry); }
-constexpr uint32_t kRouteChunk = 512;
-constexpr int kRouteThreads = 512;   // 1 primitive per thread (a latency chain: index -> positions)
+#ifndef ZR_ROUTE_CHUNK
+#define ZR_ROUTE_CHUNK 512
+#endif
+constexpr uint32_t kRouteChunk = ZR_ROUTE_CHUNK;
+constexpr int kRouteThreads = ZR_ROUTE_CHUNK;   // 1 primitive per thread (a latency chain: index -> positions)
 constexpr uint32_t kMaxShards = 32;  // destination masks are u32
 // Scratch sets the runtime cycles through for overlapped draws: a partitioned
 // draw's route + exchange, binning and tile pass are three pipeline stages on

@@ -41,6 +41,9 @@ namespace zr {
 #ifndef ZR_XCD_TILES
 #define ZR_XCD_TILES 8       // tiles per XCD run (xcd_tile); 0 or 1: blockIdx order
 #endif
+#ifndef ZR_LANE_STEP
+#define ZR_LANE_STEP 4       // pixels of a row per lane-walk step (2 or 4; 4: C3 tile pass -6.6 us, C1 -3)
+#endif
 #ifndef ZR_LARGE_LANES
 #define ZR_LARGE_LANES 1     // 0: every large primitive takes k_tile's wave path; 2: the last cost bucket's too (A/B)
 #endif
@@ -53,7 +56,9 @@ namespace zr {
 #endif
 
 // k_tile tuning constants (DESIGN.md §4 has the measurements behind each).
-constexpr uint32_t kTileWgs = 8;     // 256-thread k_tile workgroups per CU the register budget is sized for
+constexpr uint32_t kTileWgs = 8;
+constexpr int kLaneStep = ZR_LANE_STEP;
+static_assert(kLaneStep == 2 || kLaneStep == 4, "lane walk: 2 or 4 pixels per step");     // 256-thread k_tile workgroups per CU the register budget is sized for
 constexpr uint32_t kResolveBatch = 2;  // pixels per thread whose gathers are in flight together in the resolve
 constexpr uint32_t kBigLanes = 8;    // lanes per entry at least, for the last cost bucket (127+ pair steps, ~253+ px)
 constexpr uint32_t kMidLanes = 4;    // lanes per entry at least, for buckets kMidBucket..62
@@ -1268,13 +1273,14 @@ __device__ __forceinline__ TriRecord decode_large(const DrawParams& P, const int
 }
 
 // Whether the lane walk (raster_lane) is exact for a large primitive in this
-// tile: every edge value it tests, over bbox ∩ tile widened by the pair walk's
-// one column on either side, must fit int32.  The edge functions are linear, so
+// tile: every edge value it tests, over bbox ∩ tile widened by the walk's
+// kLaneStep - 1 columns on either side, must fit int32.  The edge functions are linear, so
 // their extremes are at the rectangle's corners: |w| <= |w(corner)| + |dy| 256 W
 // + |dx| 256 H, bounded in int64 against 2^31 - 1.
 __device__ __forceinline__ bool lane_walk_fits(const TriRecord& r, int x0, int y0) {
-    const int bx0 = max((int)(r.bb0 & 0xFFFFu), x0) - 1, by0 = max((int)(r.bb0 >> 16), y0);
-    const int bx1 = min((int)(r.bb1 & 0xFFFFu), x0 + kTile - 1) + 1, by1 = min((int)(r.bb1 >> 16), y0 + kTile - 1);
+    const int bx0 = max((int)(r.bb0 & 0xFFFFu), x0) - (kLaneStep - 1), by0 = max((int)(r.bb0 >> 16), y0);
+    const int bx1 = min((int)(r.bb1 & 0xFFFFu), x0 + kTile - 1) + (kLaneStep - 1);
+    const int by1 = min((int)(r.bb1 >> 16), y0 + kTile - 1);
     const long long Sx = (long long)bx0 * 256 + 128, Sy = (long long)by0 * 256 + 128;
     const long long Wd = (long long)(bx1 - bx0) * 256, Hd = (long long)max(by1 - by0, 0) * 256;
     auto edge = [&](int Xa, int Ya, int Xb, int Yb) {
@@ -1369,21 +1375,26 @@ __device__ __forceinline__ void raster_lane(const DrawParams& P, const TriRecord
     int bw = bx1 - bx0 + 1;
     const int bh = by1 - by0 + 1;
     if (bw <= 0 || bh <= sub) return;
-    // An odd-width row leaves one sample of its last pair past the bbox.  When the
-    // bbox's right side is the primitive's own x extent (not cut by the tile or the
-    // scissor) that sample lies right of every vertex, so it is never covered; else,
-    // when the left side is its own extent, the pairs start one column further left
-    // (that sample is left of every vertex).  Only when both sides are cut does the
-    // step test for it (chk).
+    // S pixels of a row per step (kLaneStep).  A row whose width is not a multiple
+    // of S leaves samples of its last step past the bbox.  When the bbox's right
+    // side is the primitive's own x extent (not cut by the tile or the scissor)
+    // they lie right of every vertex, so they are never covered; else, when the
+    // left side is its own extent, the steps start that many columns further left
+    // (left of every vertex).  Only when both sides are cut does the step test
+    // for them (chk: pixels j >= rem of the row's last step).
+    constexpr int S = kLaneStep;
     bool chk = false;
-    if (bw & 1) {
+    int rem = S;
+    if (bw & (S - 1)) {
         const int minX = min(X0, min(X1, X2)), maxX = max(X0, max(X1, X2));
         if (bx1 != (maxX - 128) >> 8) {
             if (bx0 == (minX - 128 + 255) >> 8) {
-                --bx0;
-                ++bw;
+                const int e = S - (bw & (S - 1));
+                bx0 -= e;
+                bw += e;
             } else {
                 chk = true;
+                rem = bw & (S - 1);
             }
         }
     }
@@ -1429,26 +1440,34 @@ __device__ __forceinline__ void raster_lane(const DrawParams& P, const TriRecord
             (!INITD || depth_pass(P.depth_op, z, s_initd[a >> 3])))
             atomicMin(reinterpret_cast<unsigned long long*>(reinterpret_cast<char*>(s_key) + a), frag_key<MODE>(z, seq));
     };
-    // Two pixels of a row per step (VALU and loop-control SALU are what the lane
-    // walk spends: one step's wrap selects and branch bookkeeping now serve two
-    // samples).  The second pixel of a row's last pair lies past an odd-width
-    // bbox and is skipped (pair index lastB).
-    const int hw = (bw + 1) >> 1, lastB = chk ? hw - 1 : hw;
-    const int t0 = wr(2u * sx0), t1 = wr(2u * sx1), t2 = wr(2u * sx2);
-    const uint32_t kk = (uint32_t)k, hh = 2u * (uint32_t)(hw - 1);
+    // S pixels of a row per step (VALU and loop-control SALU are what the lane
+    // walk spends: one step's wrap selects and branch bookkeeping serve S
+    // samples).  Pixels j >= rem of a row's last step (index lastB) lie past a
+    // bbox cut on both sides and are skipped.
+    const int hw = (bw + S - 1) / S, lastB = chk ? hw - 1 : hw;
+    const int t0 = wr((uint32_t)S * sx0), t1 = wr((uint32_t)S * sx1), t2 = wr((uint32_t)S * sx2);
+    const uint32_t kk = (uint32_t)k, hh = (uint32_t)S * (uint32_t)(hw - 1);
     const int q0 = wr(kk * sy0 - hh * sx0), q1 = wr(kk * sy1 - hh * sx1), q2 = wr(kk * sy2 - hh * sx2);
-    const uint32_t lq = (uint32_t)((k * kTile - 2 * (hw - 1)) * 8);
+    const uint32_t lq = (uint32_t)((k * kTile - S * (hw - 1)) * 8);
     auto sweep = [&](auto ztest, auto wchk) {
         do {
-            if ((w0 | w1 | w2) >= 0) frag(ztest, w1, w2, la);
-            const int v0 = wr((uint32_t)w0 + sx0), v1 = wr((uint32_t)w1 + sx1), v2 = wr((uint32_t)w2 + sx2);
-            if ((!decltype(wchk)::value || ex != lastB) && (v0 | v1 | v2) >= 0) frag(ztest, v1, v2, la + 8u);
+            int a0 = w0, a1 = w1, a2 = w2;
+#pragma unroll
+            for (int j = 0; j < S; ++j) {
+                if (j) {
+                    a0 = wr((uint32_t)a0 + sx0);
+                    a1 = wr((uint32_t)a1 + sx1);
+                    a2 = wr((uint32_t)a2 + sx2);
+                }
+                if ((j == 0 || !decltype(wchk)::value || ex != lastB || j < rem) && (a0 | a1 | a2) >= 0)
+                    frag(ztest, a1, a2, la + 8u * (uint32_t)j);
+            }
             const bool wrap = ++ex == hw;
             ex = wrap ? 0 : ex;
             w0 = wr((uint32_t)w0 + (wrap ? q0 : t0));
             w1 = wr((uint32_t)w1 + (wrap ? q1 : t1));
             w2 = wr((uint32_t)w2 + (wrap ? q2 : t2));
-            la += wrap ? lq : 16u;
+            la += wrap ? lq : 8u * (uint32_t)S;
         } while (la != la_end);
     };
     const bool wchk = __ballot(chk) != 0ull;
