@@ -17,6 +17,10 @@ constexpr uint32_t kSortBuckets = 64;   // cost classes: the lane walk's pair st
 constexpr int kSetupThreads = 1024;  // setup / bin workgroups (one LDS histogram each)
 constexpr uint32_t kSetupLdsBudget = 160u * 1024u;     // one k_setup_bin workgroup per CU owns the LDS
 constexpr uint32_t kSetupBboxLdsBytes = 96u * 1024u;  // cap on the per-workgroup bbox array in LDS
+#ifndef ZR_BIN_STAGE_DEFAULT
+#define ZR_BIN_STAGE_DEFAULT 1
+#endif
+constexpr bool kBinStageDefault = ZR_BIN_STAGE_DEFAULT;  // k_setup_bin phase 4 staged in LDS (ZR_BIN_STAGE)
 
 enum Program : int32_t { kProgTriangle = 0, kProgFlat = 1, kProgBlinn = 2, kProgMesh = 3, kProgCount = 4 };
 
@@ -289,6 +293,7 @@ struct DrawParams {
     uint32_t units;           // claim units of the draw: ceil(prims / unit size)
     uint32_t setup_batch;     // primitives per lane in flight (template instance of k_setup_bin)
     uint32_t bbox_lds;        // 0: bboxes in global memory; else LDS entries per workgroup (own units * unit size)
+    uint32_t bin_stage;       // k_setup_bin phase 4: LDS staging capacity in pairs (0: scatter straight to the bins)
     uint32_t debug;           // kDebug* bits (timing experiments only)
     unsigned long long* dbg_ts; // [setup_wgs][8] s_memrealtime stamps (kDebugStamps only)
     uint32_t* tile_order;     // tile schedule (k_setup_bin's last workgroup -> k_tile), or nullptr: xcd_tile order
@@ -384,7 +389,7 @@ __host__ __device__ inline ShardGeom shard_geom(const DrawParams& P) {
 
 // Launchers (zr_kernels.hip).  All enqueue on `stream`; no host synchronisation.
 void launch_setup_bin(const DrawParams& p, void* stream);  // setup + bin, one launch
-size_t setup_bin_lds_bytes(uint32_t ntiles, uint32_t bbox_entries);
+size_t setup_bin_lds_bytes(uint32_t ntiles, uint32_t bbox_entries, uint32_t stage_pairs = 0);
 const void* setup_bin_kernel(uint32_t batch, bool mesh);
 void launch_tile(const DrawParams& p, void* stream);
 void launch_clear(const DrawParams& p, void* stream);

@@ -58,7 +58,7 @@ namespace zr {
 // k_tile tuning constants (DESIGN.md §4 has the measurements behind each).
 constexpr uint32_t kTileWgs = 8;
 constexpr int kLaneStep = ZR_LANE_STEP;
-static_assert(kLaneStep == 2 || kLaneStep == 4, "lane walk: 2 or 4 pixels per step");     // 256-thread k_tile workgroups per CU the register budget is sized for
+static_assert(kLaneStep == 2 || kLaneStep == 4 || kLaneStep == 8, "lane walk: 2, 4 or 8 pixels per step");     // 256-thread k_tile workgroups per CU the register budget is sized for
 constexpr uint32_t kResolveBatch = 2;  // pixels per thread whose gathers are in flight together in the resolve
 constexpr uint32_t kBigLanes = 8;    // lanes per entry at least, for the last cost bucket (127+ pair steps, ~253+ px)
 constexpr uint32_t kMidLanes = 4;    // lanes per entry at least, for buckets kMidBucket..62
@@ -980,6 +980,10 @@ __global__ __launch_bounds__(kSetupThreads) void k_setup_bin(DrawParams P) {
     // this workgroup's primitives' tile bboxes, indexed like phase 4's flattened
     // (own unit, primitive in unit) space, when they fit (P.bbox_lds)
     BBox* s_bbox = reinterpret_cast<BBox*>(s_misc + kSetupMiscWords);
+    // phase 4's staging (P.bin_stage): per-tile local cursors, then (bin position,
+    // entry) pairs grouped by tile
+    uint32_t* s_lcur = reinterpret_cast<uint32_t*>(s_bbox + P.bbox_lds);
+    uint2* s_stage = reinterpret_cast<uint2*>(s_lcur + ((nt + 3u) & ~3u));
     ZR_STAMP(0);
     for (uint32_t t = tid; t < nt; t += kSetupThreads) s_hist[t] = 0;
     if (tid < 32) s_misc[tid] = 0;
@@ -1096,6 +1100,7 @@ __global__ __launch_bounds__(kSetupThreads) void k_setup_bin(DrawParams P) {
             const uint32_t c = s_hist[t];
             const uint32_t o = c ? __hip_atomic_fetch_add(&P.tile_counts[t], c, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) : 0u;
             s_hist[t] = t * P.slab + o;
+            if (P.bin_stage) s_lcur[t] = c;
             top = max(top, o + c);
             sum += c;
         }
@@ -1165,7 +1170,72 @@ __global__ __launch_bounds__(kSetupThreads) void k_setup_bin(DrawParams P) {
         };
         uint32_t nown = 0;
         while (own_unit(w, G, nown) < units) ++nown;
-        for (uint32_t j = tid; j < (nown << P.unit_shift); j += kSetupThreads) {
+        // Staged (the workgroup's pairs fit P.bin_stage): the pairs go to LDS grouped
+        // by tile -- local offsets from an exclusive scan of this workgroup's
+        // per-tile counts -- with their bin positions, and are then stored in that
+        // order, so the lanes of a store instruction write a tile's run side by
+        // side (one request per run and line instead of one per pair).
+        const uint32_t npairs = s_misc[3];
+        const bool staged = P.bin_stage && npairs <= P.bin_stage;
+        if (staged) {
+            const uint32_t per = (nt + kSetupThreads - 1u) / kSetupThreads;
+            const uint32_t t0 = min(tid * per, nt), t1 = min(t0 + per, nt);
+            uint32_t sum = 0;
+            for (uint32_t t = t0; t < t1; ++t) sum += s_lcur[t];
+            uint32_t inc = sum;  // exclusive scan of the threads' sums: waves, then the 16 wave totals
+#pragma unroll
+            for (int d = 1; d < 64; d <<= 1) {
+                const uint32_t y = __shfl_up(inc, d, 64);
+                if ((int)(tid & 63u) >= d) inc += y;
+            }
+            if ((tid & 63u) == 63u) s_misc[16 + (tid >> 6)] = inc;
+            __syncthreads();
+            uint32_t base = 0;
+            for (uint32_t q = 0; q < (tid >> 6); ++q) base += s_misc[16 + q];
+            uint32_t run = base + inc - sum;
+            for (uint32_t t = t0; t < t1; ++t) {
+                const uint32_t c = s_lcur[t];
+                s_lcur[t] = run;   // the tile's local cursor
+                s_hist[t] -= run;  // bin position - local slot
+                run += c;
+            }
+            __syncthreads();
+        }
+        auto scatter_staged = [&](uint32_t rec, const BBox bb) {
+            if (bb.bb0 == kEmptyBox) return;
+            const int tx0 = (int)(bb.bb0 & 0xFFFFu) >> kTileShift, tx1 = (int)(bb.bb1 & 0xFFFFu) >> kTileShift;
+            const int ty0 = (int)(bb.bb0 >> 16) >> kTileShift, ty1 = (int)(bb.bb1 >> 16) >> kTileShift;
+            for_owned_tiles(sG, srank, tiles_x, full_rows, own_rows, left_lo, left_hi, tx0, ty0, tx1, ty1,
+                            [&](uint32_t t, int tx, int ty) {
+                const int cy0 = max((int)(bb.bb0 >> 16), ty << kTileShift);
+                const int cy1 = min((int)(bb.bb1 >> 16), (ty << kTileShift) + kTile - 1);
+                const int cx0 = max((int)(bb.bb0 & 0xFFFFu), tx << kTileShift);
+                const int cx1 = min((int)(bb.bb1 & 0xFFFFu), (tx << kTileShift) + kTile - 1);
+                const uint32_t steps = (uint32_t)(((cx1 - cx0 + 2) >> 1) * (cy1 - cy0 + 1));
+                const uint32_t bucket = min((steps - 1u) >> 1, kSortBuckets - 1u);
+                const uint32_t l = atomicAdd(&s_lcur[t], 1u);
+                const uint32_t pos = s_hist[t] + l;
+                s_stage[l] = make_uint2(pos - t * slab < slab ? pos : 0xFFFFFFFFu, rec | (bucket << kBinPrimBits));
+            });
+        };
+        for (uint32_t j = tid; staged && j < (nown << P.unit_shift); j += kSetupThreads) {
+            const uint32_t prim = (own_unit(w, G, j >> P.unit_shift) << P.unit_shift) + (j & (usz - 1u));
+            if (prim >= n_pos) continue;
+            const BBox bb = P.bbox_lds ? s_bbox[j] : P.bboxes[prim];
+            scatter_staged(rec_mode && bb.bb0 != kEmptyBox ? P.gids[prim] : prim, bb);
+            if (MESH) {
+                scatter_staged(mesh_record(P, prim, 1), P.bboxes[mesh_record(P, prim, 1)]);
+                scatter_staged(mesh_record(P, prim, 2), P.bboxes[mesh_record(P, prim, 2)]);
+            }
+        }
+        if (staged) {
+            __syncthreads();
+            for (uint32_t i = tid; i < npairs; i += kSetupThreads) {
+                const uint2 v = s_stage[i];
+                if (v.x != 0xFFFFFFFFu) bins[v.x] = v.y;
+            }
+        }
+        for (uint32_t j = tid; !staged && j < (nown << P.unit_shift); j += kSetupThreads) {
             const uint32_t prim = (own_unit(w, G, j >> P.unit_shift) << P.unit_shift) + (j & (usz - 1u));
             if (prim >= n_pos) continue;
             const BBox bb = P.bbox_lds ? s_bbox[j] : P.bboxes[prim];
@@ -2447,8 +2517,10 @@ __global__ __launch_bounds__(kTileThreads) void k_clear(DrawParams P) {
 
 static inline uint32_t blocks_for(uint32_t n, uint32_t per) { return (n + per - 1) / per; }
 
-size_t setup_bin_lds_bytes(uint32_t ntiles, uint32_t bbox_entries) {
-    return (((size_t)ntiles + 3u) / 4u * 4u + kSetupMiscWords) * sizeof(uint32_t) + (size_t)bbox_entries * sizeof(BBox);
+size_t setup_bin_lds_bytes(uint32_t ntiles, uint32_t bbox_entries, uint32_t stage_pairs) {
+    const size_t nt4 = ((size_t)ntiles + 3u) / 4u * 4u;
+    return (nt4 + kSetupMiscWords) * sizeof(uint32_t) + (size_t)bbox_entries * sizeof(BBox) +
+           (stage_pairs ? nt4 * sizeof(uint32_t) + (size_t)stage_pairs * 8u : 0u);
 }
 
 const void* setup_bin_kernel(uint32_t batch, bool mesh) {
@@ -2461,7 +2533,7 @@ const void* setup_bin_kernel(uint32_t batch, bool mesh) {
 }
 
 void launch_setup_bin(const DrawParams& p, void* stream) {
-    const size_t lds = setup_bin_lds_bytes(p.ntiles, p.bbox_lds);
+    const size_t lds = setup_bin_lds_bytes(p.ntiles, p.bbox_lds, p.bin_stage);
     const hipStream_t s = (hipStream_t)stream;
     if (p.program == kProgMesh) {  // batch 1: the clip path is heavy
         hipLaunchKernelGGL((k_setup_bin<1, true>), dim3(p.setup_wgs), dim3(kSetupThreads), lds, s, p);

@@ -257,6 +257,7 @@ struct zr_device_t {
     int rec_table = -1;        // ZR_REC_TABLE=0/1 forces k_tile's record table (A/B); -1: use_record_table
     int tile_sched = -1;       // ZR_TILE_SCHED=0/1 forces the heaviest-first tile schedule (A/B); -1: use_tile_schedule
     uint32_t rec_wgs = 0;      // ZR_REC_WGS: k_setup_bin workgroups of partitioned (records-mode) draws; 0: one per CU
+    int bin_stage = -1;        // ZR_BIN_STAGE: k_setup_bin phase 4 staged through LDS (1), direct (0), default (-1)
     int cu_count = 0;
     uint32_t occupancy_checked_tiles = 0;
     bool occupancy_checked_mesh = false;
@@ -826,6 +827,7 @@ zr_result exec_draw(zr_device* d, ExecState& s, const Cmd& c, bool indexed) {
         d->occupancy_checked_tiles = P.ntiles;
         d->occupancy_checked_mesh = mesh;
     }
+    uint64_t stage_entries = 0;
     {
         // one workgroup per CU (fewer for small draws); a wave processes units of
         // 64 * batch * 2^k primitives, at most ~64 units per workgroup on average
@@ -848,11 +850,25 @@ zr_result exec_draw(zr_device* d, ExecState& s, const Cmd& c, bool indexed) {
         const uint64_t budget = std::min<uint64_t>(kSetupBboxLdsBytes, hist < kSetupLdsBudget ? kSetupLdsBudget - hist : 0);
         // (mesh: fans 1 and 2 keep their bboxes in global memory, so all of them do)
         P.bbox_lds = (!mesh && entries * sizeof(BBox) <= budget) ? (uint32_t)entries : 0u;
+        stage_entries = entries;
     }
     // k_setup_bin on the setup stream with two scratch sets (zr_device_t::setup_overlap);
     // not while debugging or with graph replay, whose captures bake in set 0
     const bool overlap_setup = (d->setup_overlap > 0 || (d->setup_overlap < 0 && (prims <= (1u << 18) || P.shard_count > 1))) &&
                        !d->use_graphs && !d->debug;
+    // k_setup_bin phase 4 staged in LDS (pairs grouped by tile, stored run by run):
+    // room for twice the workgroup's primitives, in the CU's LDS that setup owns
+    // alone -- not beside a tile pass (overlapped setup), whose workgroups would
+    // lose the LDS (C1 frame +1.9 us).  A workgroup whose pairs do not fit
+    // scatters straight to the bins.
+    {
+        const uint64_t used = setup_bin_lds_bytes(P.ntiles, P.bbox_lds);
+        const uint64_t cur = ((uint64_t)P.ntiles + 3u) / 4u * 4u * 4u;
+        const uint64_t room = used + cur < kSetupLdsBudget ? (kSetupLdsBudget - used - cur) / 8u : 0u;
+        const uint64_t cap = std::min<uint64_t>(room, 2u * std::max<uint64_t>(stage_entries, 1024u));
+        const bool on = d->bin_stage > 0 || (d->bin_stage < 0 && kBinStageDefault && !overlap_setup);
+        P.bin_stage = on && cap >= 1024u ? (uint32_t)cap : 0u;
+    }
     P.tile_threads = d->tile_threads ? d->tile_threads
                                      : tile_threads_for(P.ntiles, (uint32_t)std::max(d->cu_count, 1), prims, partitioned);
     P.rec_table = (d->rec_table < 0 ? use_record_table(prims, P.tiles_x, P.tiles_y) : d->rec_table != 0) ? 1u : 0u;
@@ -1111,6 +1127,7 @@ ZR_API zr_result zr_device_create(int32_t hip_device, zr_device** out) {
     if (const char* rt = getenv("ZR_REC_TABLE")) d->rec_table = strtoul(rt, nullptr, 0) != 0 ? 1 : 0;
     if (const char* ts = getenv("ZR_TILE_SCHED")) d->tile_sched = strtoul(ts, nullptr, 0) != 0 ? 1 : 0;
     if (const char* rw = getenv("ZR_REC_WGS")) d->rec_wgs = (uint32_t)strtoul(rw, nullptr, 0);
+    if (const char* bs = getenv("ZR_BIN_STAGE")) d->bin_stage = atoi(bs);
     if (const char* nt = getenv("ZR_TILE_NT")) {
         const unsigned long v = strtoul(nt, nullptr, 0);
         d->tile_threads = v >= 512 ? 512u : v ? 256u : 0u;
