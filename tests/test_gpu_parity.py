@@ -201,6 +201,31 @@ def test_slab_overflow_one_tile():
         dev.close()
 
 
+@pytest.mark.parametrize("stage", ["0", "1"])
+def test_setup_bin_stage(monkeypatch, stage):
+    """k_setup_bin's phase 4 staged in LDS (ZR_BIN_STAGE=1, forced even beside an
+    overlapped tile pass) and direct (0), bit-exact on: a soup, a tile shard, the
+    camera program's fans, pairs past full slabs (ZR_BIN_CAPACITY), and a draw
+    whose workgroups have more pairs than the staging holds (large triangles:
+    those workgroups scatter directly)."""
+    monkeypatch.setenv("ZR_BIN_STAGE", stage)
+    dev = rhi.RenderDevice(0)
+    try:
+        assert_parity(dev, scenes.config_scene("c1", n=30000, width=640, height=360))
+        assert_parity(dev, scenes.soup_scene(18, 4000, 512, 384, 12.0, scenes.PROGRAM_BLINN_PHONG), shard=(1, 3))
+        assert_parity(dev, scenes.cerberus_scene(640, 480))
+        assert_parity(dev, scenes.soup_scene(17, 300, 512, 384, 150.0, scenes.PROGRAM_FLAT_COLOR))
+    finally:
+        dev.close()
+    monkeypatch.setenv("ZR_BIN_CAPACITY", "1024")
+    dev = rhi.RenderDevice(0)
+    try:
+        assert_parity(dev, scenes.soup_scene(16, 3000, 640, 480, 40.0, scenes.PROGRAM_FLAT_COLOR))
+        assert dev.last_draw_stats()["overflowed_draws"] == 1
+    finally:
+        dev.close()
+
+
 @pytest.mark.parametrize("table", [0, 1])
 def test_record_table(monkeypatch, table):
     """k_tile's 512-thread resolve with its LDS record table forced on or off
