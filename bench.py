@@ -65,7 +65,7 @@ def parse():
                    help="run the multi-GPU code path (RCCL process group, exchange, gather) even at 1 GPU")
     p.add_argument("--worker-timeout", type=float, default=0.0,
                    help="launcher-less N>1 run: stop the workers after this many seconds (0: no limit)")
-    p.add_argument("--pmc", default=os.path.join(ROOT, "profiles", "r04_v2_pmc_c2.json"),
+    p.add_argument("--pmc", default=os.path.join(ROOT, "profiles", "r04_v3_pmc_c2.json"),
                    help="rocprofv3 PMC summary for roofline.traffic (tools/pmc_summary.py)")
     return p.parse_args()
 
