@@ -60,9 +60,18 @@ constexpr uint32_t kTileWgs = 8;
 constexpr int kLaneStep = ZR_LANE_STEP;
 static_assert(kLaneStep == 2 || kLaneStep == 4 || kLaneStep == 8, "lane walk: 2, 4 or 8 pixels per step");     // 256-thread k_tile workgroups per CU the register budget is sized for
 constexpr uint32_t kResolveBatch = 2;  // pixels per thread whose gathers are in flight together in the resolve
-constexpr uint32_t kBigLanes = 8;    // lanes per entry at least, for the last cost bucket (127+ pair steps, ~253+ px)
-constexpr uint32_t kMidLanes = 4;    // lanes per entry at least, for buckets kMidBucket..62
-constexpr uint32_t kMidBucket = 24;  // first bucket of the middle run: 49+ pair steps (~97+ px of bbox ∩ tile)
+#ifndef ZR_BIG_LANES
+#define ZR_BIG_LANES 8
+#endif
+#ifndef ZR_MID_LANES
+#define ZR_MID_LANES 4
+#endif
+#ifndef ZR_MID_BUCKET
+#define ZR_MID_BUCKET 24
+#endif
+constexpr uint32_t kBigLanes = ZR_BIG_LANES;    // lanes per entry at least, for the last cost bucket (127+ pair steps, ~253+ px)
+constexpr uint32_t kMidLanes = ZR_MID_LANES;    // lanes per entry at least, for buckets kMidBucket..62
+constexpr uint32_t kMidBucket = ZR_MID_BUCKET;  // first bucket of the middle run: 49+ pair steps (~97+ px of bbox ∩ tile)
 
 __constant__ float c_srgbT[255] = ZR_SRGB_THRESHOLDS_INIT;
 
