@@ -65,6 +65,9 @@ def parse():
                    help="run the multi-GPU code path (RCCL process group, exchange, gather) even at 1 GPU")
     p.add_argument("--worker-timeout", type=float, default=0.0,
                    help="launcher-less N>1 run: stop the workers after this many seconds (0: no limit)")
+    p.add_argument("--no-census", action="store_true",
+                   help="skip the untimed winner-census frame (its instrumented k_tile would enter a rocprofv3 "
+                        "kernel trace beside the timed launches; roofline.design then counts no winners)")
     p.add_argument("--pmc", default=os.path.join(ROOT, "profiles", "r04_v3_pmc_c2.json"),
                    help="rocprofv3 PMC summary for roofline.traffic (tools/pmc_summary.py)")
     return p.parse_args()
@@ -550,12 +553,14 @@ def main():
     stats = dev.last_draw_stats()
     # winner census: one more (untimed) frame whose resolve marks each primitive
     # that wins a pixel, for the tile pass's per-winner gather bytes
-    dev.set_profiling(True, census=True)
-    frame[0] = 0
-    step(1)
-    dev.wait_idle()
-    winners = dev.last_draw_stats()["winners"]
-    dev.set_profiling(False)
+    winners = None
+    if not a.no_census:
+        dev.set_profiling(True, census=True)
+        frame[0] = 0
+        step(1)
+        dev.wait_idle()
+        winners = dev.last_draw_stats()["winners"]
+        dev.set_profiling(False)
     dev.kernel_times(reset=True)
     pairs = stats["bin_pairs"]
     pixels = shard.owned_pixels(W, H, rank, shard_g)
@@ -591,7 +596,7 @@ def main():
     achieved_survey = round(survey_bytes / (tile_us * 1e-6) / 1e9, 1) if tile_us > 0 else None
     # the design's own request classes (bins, records, winners' gathers, stores)
     per_winner = winner_bytes(scene.program, index_size)
-    design = design_tile_bytes(pairs, winners, per_winner, pixels)
+    design = design_tile_bytes(pairs, winners or 0, per_winner, pixels)
     design_total = sum(design.values())
     achieved_design = round(design_total / (tile_us * 1e-6) / 1e9, 1) if tile_us > 0 else None
 

@@ -241,6 +241,22 @@ def test_exchange_plan_pairs_every_peer(world):
     assert lib.zr_gather_plan(0, 1080, 4, 2, 0, 0, None, 0) == -1
 
 
+@pytest.mark.parametrize("nbytes,bpr", [(0, 64), (100, 64), (64 * 33, 64), (64, 0), (96, 64)])
+def test_replay_exchange_refuses_foreign_layouts(nbytes, bpr):
+    """zr_replay_exchange_fn copies the recorded blocks into the draw's receive
+    buffer (shard count x bytes_per_rank): a recording that is not whole blocks of
+    the draw's layout, or more than kMaxShards of them, is refused before any
+    copy (exec_draw also checks the count against the draw's shard count)."""
+    fn = zr.EXCHANGE_FN(zr.lib().zr_replay_exchange_fn())
+    src = (C.c_uint8 * 16)()
+    desc = zr.zr_replay_exchange(C.cast(src, C.c_void_p), nbytes)
+    rc = fn(C.addressof(desc), None, None, None, bpr)
+    assert rc == zr.ERROR_VALIDATION_FAILED
+    assert b"whole exchange blocks" in zr.lib().zr_last_error_message()
+    empty = zr.zr_replay_exchange(None, 64)
+    assert fn(C.addressof(empty), None, None, None, 64) == zr.ERROR_VALIDATION_FAILED
+
+
 # ------------------------------------------------- push constants (host only)
 # CommandEncoder::push_constants (command.rs:180-185), ShaderReflection::
 # push_constant_size (shader.rs:214, :224-228, :408-413) and the pipeline

@@ -603,6 +603,40 @@ def test_partitioned_route_overflow(capacity):
     assert all(st["route_max_entries"] > capacity for st in stats)
 
 
+def test_replay_exchange_layout_checked(device):
+    """zr_replay_exchange_fn (bench.py --emulate-shard) copies recorded receive
+    blocks into the draw's receive buffer: a recording of another layout (here one
+    block for a 2-way shard) is refused at submit with VALIDATION_FAILED instead of
+    being copied past the buffer's end; the draw's own layout is accepted."""
+    import ctypes
+    import torch
+    s = scenes.soup_scene(82, 2000, 160, 120, 8.0, scenes.PROGRAM_FLAT_COLOR)
+    cap, world = 100, 2
+    block = 16 + 48 * cap  # route_block_bytes(cap): RouteHeader + cap RouteEntry
+
+    class Replay:
+        def __init__(self, nbytes):
+            self.src = torch.zeros(nbytes, dtype=torch.uint8, device="cuda")
+
+        def native(self):
+            desc = zr.zr_replay_exchange(self.src.data_ptr(), self.src.numel())
+            return zr.lib().zr_replay_exchange_fn(), ctypes.addressof(desc), (desc, self.src)
+
+    color = rhi.Texture(device, rhi.TextureDesc.new_color("rt", s.width, s.height, s.color_format))
+    depth = rhi.Texture(device, rhi.TextureDesc.new_depth("ds", s.width, s.height))
+    r = renderer.SceneRenderer(device, s)
+    bad = r.record(color, depth, shard=(0, world, Replay(block), cap), encoder=rhi.CommandEncoder(device))
+    with pytest.raises(zr.ZrError) as e:
+        device.submit(bad)
+    assert e.value.code == zr.ERROR_VALIDATION_FAILED
+    device.wait_idle()
+    good = r.record(color, depth, shard=(0, world, Replay(world * block), cap), encoder=rhi.CommandEncoder(device))
+    device.submit(good)
+    device.wait_idle()
+    for x in (bad, good, color, depth):
+        x.destroy()
+
+
 def test_partitioned_overflow_spill(monkeypatch):
     monkeypatch.setenv("ZR_BIN_CAPACITY", "256")
     assert_partitioned_parity(scenes.soup_scene(74, 3000, 320, 240, 30.0, scenes.PROGRAM_FLAT_COLOR), 2)

@@ -20,9 +20,9 @@ for c in c2 c3; do timeout -k 10 200 python bench.py --config $c --emulate-shard
 timeout -k 10 200 python bench.py --config c3 --emulate-shard 8 --no-cpu-baseline > $O/bench_c3_shard8.json 2>> $O/bench.err || exit 3
 [ "$2" = quick ] && { echo done; exit 0; }
 fi
-timeout -k 10 200 rocprofv3 --kernel-trace --stats -d $O/kt -o run --output-format csv -- python3 bench.py --steps 50 --warmup 5 --no-cpu-baseline > $O/kt.log 2>&1 || exit 4
-timeout -k 10 200 rocprofv3 --pmc FETCH_SIZE -d $O/pf -o run --output-format csv -- python3 bench.py --steps 5 --warmup 2 --no-cpu-baseline > $O/pf.log 2>&1 || exit 5
-timeout -k 10 200 rocprofv3 --pmc WRITE_SIZE -d $O/pw -o run --output-format csv -- python3 bench.py --steps 5 --warmup 2 --no-cpu-baseline > $O/pw.log 2>&1 || exit 6
+timeout -k 10 200 rocprofv3 --kernel-trace --stats -d $O/kt -o run --output-format csv -- python3 bench.py --steps 50 --warmup 5 --no-cpu-baseline --no-census > $O/kt.log 2>&1 || exit 4
+timeout -k 10 200 rocprofv3 --pmc FETCH_SIZE -d $O/pf -o run --output-format csv -- python3 bench.py --steps 5 --warmup 2 --no-cpu-baseline --no-census > $O/pf.log 2>&1 || exit 5
+timeout -k 10 200 rocprofv3 --pmc WRITE_SIZE -d $O/pw -o run --output-format csv -- python3 bench.py --steps 5 --warmup 2 --no-cpu-baseline --no-census > $O/pw.log 2>&1 || exit 6
 timeout -k 10 120 rocprofv3 --pmc FETCH_SIZE -d $O/cf -o run --output-format csv -- tools/build/pmc_calib > $O/calib_known.txt 2>&1 || exit 7
 timeout -k 10 120 rocprofv3 --pmc WRITE_SIZE -d $O/cw -o run --output-format csv -- tools/build/pmc_calib > $O/calib_w.txt 2>&1 || exit 8
 bash tools/pmc_classes.sh $V || exit 9

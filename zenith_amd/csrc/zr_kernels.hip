@@ -56,9 +56,10 @@ namespace zr {
 #endif
 
 // k_tile tuning constants (DESIGN.md §4 has the measurements behind each).
-constexpr uint32_t kTileWgs = 8;
+constexpr uint32_t kTileWgs = 8;  // 256-thread k_tile workgroups per CU the register budget is sized for
 constexpr int kLaneStep = ZR_LANE_STEP;
-static_assert(kLaneStep == 2 || kLaneStep == 4 || kLaneStep == 8, "lane walk: 2, 4 or 8 pixels per step");     // 256-thread k_tile workgroups per CU the register budget is sized for
+// (8 pixels per step was measured slower and has no parity run: not a build option)
+static_assert(kLaneStep == 2 || kLaneStep == 4, "lane walk: 2 or 4 pixels per step");
 constexpr uint32_t kResolveBatch = 2;  // pixels per thread whose gathers are in flight together in the resolve
 #ifndef ZR_BIG_LANES
 #define ZR_BIG_LANES 8
@@ -2502,8 +2503,12 @@ __global__ __launch_bounds__(NT, kTileWgs * kTileThreads / 256) void k_tile(Draw
         ts[4] = __builtin_amdgcn_s_memrealtime();
         ts[7] = ((unsigned long long)s_dbg[1] << 32) | s_dbg[0];
         if (NT >= 512) {  // (resolve_tile's own stamps use these two at 256 threads)
-            if (!count) ts[5] = ts[2] = ts[1];  // no segment ran
-            ts[6] = (ts[6] & ~0xFFFFFFFFull) | count;  // the tile's list length (tools/tile_stamps.py)
+            if (!count) {  // no segment ran: no wave-path queue either (dbg_ts persists across draws)
+                ts[5] = ts[2] = ts[1];
+                ts[6] = 0ull;
+            } else {
+                ts[6] = (ts[6] & ~0xFFFFFFFFull) | count;  // the tile's list length (tools/tile_stamps.py)
+            }
         }
     }
 }

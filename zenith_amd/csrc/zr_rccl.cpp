@@ -109,6 +109,18 @@ bool rccl_recv(void* buf, size_t bytes, int peer, void* comm, hipStream_t s, std
     return check(g_api.recv(buf, bytes, kUint8, peer, comm, s), "ncclRecv", err);
 }
 
+bool rccl_grouped(const P2POp* ops, size_t n, void* comm, hipStream_t s, std::string& err) {
+    if (!rccl_load(err) || !rccl_group_start(err)) return false;
+    bool ok = true;
+    for (size_t i = 0; ok && i < n; ++i)
+        ok = ops[i].send ? rccl_send(ops[i].buf, ops[i].bytes, ops[i].peer, comm, s, err)
+                         : rccl_recv(ops[i].buf, ops[i].bytes, ops[i].peer, comm, s, err);
+    std::string end_err;
+    const bool ended = rccl_group_end(end_err);
+    if (ok && !ended) err = end_err;  // (a failed op's message is the one to report)
+    return ok && ended;
+}
+
 bool rccl_has_all_to_all() { return g_api.all_to_all != nullptr; }
 
 bool rccl_all_to_all(const void* send, void* recv, size_t bytes_per_rank, void* comm, hipStream_t s, std::string& err) {

@@ -25,6 +25,19 @@ bool rccl_group_start(std::string& err);
 bool rccl_group_end(std::string& err);
 bool rccl_send(const void* buf, size_t bytes, int peer, void* comm, hipStream_t s, std::string& err);
 bool rccl_recv(void* buf, size_t bytes, int peer, void* comm, hipStream_t s, std::string& err);
+// One grouped batch of point-to-point calls: ncclGroupStart, every op (a send of
+// `buf` when `send`, else a receive into it) until the first failure, then
+// ncclGroupEnd -- only when the start succeeded, and always then, whatever the
+// sends returned (an unbalanced start or end is an RCCL error of its own and
+// would hide the first one's message).  Both collectives go through it
+// (zr_runtime.cpp); tests/test_rccl_group.py drives it against a fake RCCL.
+struct P2POp {
+    void* buf;
+    size_t bytes;
+    int peer;
+    bool send;
+};
+bool rccl_grouped(const P2POp* ops, size_t n, void* comm, hipStream_t s, std::string& err);
 // RCCL's ncclAllToAll extension (one call instead of a group of 2 * nranks
 // point-to-point calls); absent from plain NCCL-API builds.
 bool rccl_has_all_to_all();

@@ -658,6 +658,7 @@ zr_result ensure_scratch(zr_device* d, ScratchSet& S, DrawParams& P) {
 }
 
 zr_result rccl_exchange(void* user, void* stream, const void* send, void* recv, uint64_t bytes_per_rank);
+zr_result replay_exchange(void* user, void* stream, const void* send, void* recv, uint64_t bytes_per_rank);
 
 zr_result exec_draw(zr_device* d, ExecState& s, const Cmd& c, bool indexed) {
     if (!s.rendering) return fail(ZR_ERROR_VALIDATION_FAILED, "draw outside begin_rendering/end_rendering");
@@ -748,6 +749,14 @@ zr_result exec_draw(zr_device* d, ExecState& s, const Cmd& c, bool indexed) {
         if (positions > kBinPrimMask)
             return fail(ZR_ERROR_FEATURE_NOT_PRESENT, "partitioned draw: more than 2^26-1 block positions");
         P.route_cap = (uint32_t)cap;
+        if (s.exchange == &replay_exchange) {
+            // the recorded blocks are copied into this draw's receive buffer (G blocks)
+            const zr_replay_exchange* r = (const zr_replay_exchange*)s.exchange_user;
+            if (!r || !r->src || r->bytes != G * route_block_bytes(P.route_cap))
+                return fail(ZR_ERROR_VALIDATION_FAILED,
+                            "zr_replay_exchange_fn: recorded bytes differ from this draw's exchange layout "
+                            "(shard count x route_block_bytes(route capacity))");
+        }
         P.route_chunks = (uint32_t)(span / kRouteChunk);
         P.route_lo = (uint32_t)std::min<uint64_t>(prims, (uint64_t)s.shard_rank * span);
         P.route_hi = (uint32_t)std::min<uint64_t>(prims, (uint64_t)P.route_lo + span);
@@ -897,7 +906,10 @@ zr_result exec_draw(zr_device* d, ExecState& s, const Cmd& c, bool indexed) {
     ScratchSet& S = d->sets[overlap ? d->cur_set : 0];
     if (overlap) d->cur_set = (d->cur_set + 1u) % kScratchSets;
     if ((rc = ensure_scratch(d, S, P))) return rc;
-    if (sched) {
+    // (a phase-1-only timing run never reaches the last workgroup's ticket, so it
+    // writes no schedule: k_tile then keeps xcd_tile order instead of reading an
+    // unwritten one)
+    if (sched && !(d->debug & kDebugPhase1Only)) {
         if ((rc = grow(d, S.tile_order, S.tile_order_cap, P.ntiles, 4))) return rc;
         P.tile_order = S.tile_order;
     }
@@ -1916,13 +1928,11 @@ zr_result rccl_exchange(void* user, void* stream, const void* send, void* recv, 
     zr_transfer_op plan[2 * kMaxShards];
     const int32_t n = zr_exchange_plan(d->comm_size, d->comm_rank, bytes_per_rank, plan, 2 * (int32_t)kMaxShards);
     if (n < 0) return fail(ZR_ERROR_VALIDATION_FAILED, "bad exchange plan (rank / rank count)");
-    if (!rccl_group_start(err)) return fail(ZR_ERROR_DEVICE_LOST, err);
-    bool ok = true;
-    for (int32_t i = 0; ok && i < n; ++i)
-        ok = plan[i].send ? rccl_send((const uint8_t*)send + plan[i].offset, plan[i].bytes, plan[i].peer, d->comm_x, s, err)
-                          : rccl_recv((uint8_t*)recv + plan[i].offset, plan[i].bytes, plan[i].peer, d->comm_x, s, err);
-    const bool ended = rccl_group_end(err);  // closes the group whatever the sends returned
-    if (!ended || !ok) return fail(ZR_ERROR_DEVICE_LOST, err);
+    P2POp ops[2 * kMaxShards];
+    for (int32_t i = 0; i < n; ++i)
+        ops[i] = P2POp{plan[i].send ? (void*)((const uint8_t*)send + plan[i].offset) : (void*)((uint8_t*)recv + plan[i].offset),
+                       (size_t)plan[i].bytes, plan[i].peer, plan[i].send != 0};
+    if (!rccl_grouped(ops, (size_t)n, d->comm_x, s, err)) return fail(ZR_ERROR_DEVICE_LOST, err);
     return ZR_SUCCESS;
 }
 
@@ -2036,14 +2046,26 @@ ZR_API zr_result zr_device_init_rccl(zr_device* d, const void* exchange_id, cons
 
 ZR_API zr_exchange_fn zr_rccl_exchange_fn(void) { return &rccl_exchange; }
 
-static zr_result replay_exchange(void* user, void* stream, const void* send, void* recv, uint64_t bytes_per_rank) {
+namespace {
+
+// The recorded receive blocks must be whole blocks of this draw's layout: the
+// receive buffer holds shard_count x bytes_per_rank bytes (exec_draw checks the
+// count against the draw before the route runs; here, without the count, a size
+// that is no whole number of blocks or more than kMaxShards of them is refused --
+// a buffer recorded at another route capacity or shard count would otherwise be
+// copied past the end of the receive buffer).
+zr_result replay_exchange(void* user, void* stream, const void* send, void* recv, uint64_t bytes_per_rank) {
     (void)send;
-    (void)bytes_per_rank;
     const zr_replay_exchange* r = (const zr_replay_exchange*)user;
     if (!r || !r->src) return fail(ZR_ERROR_VALIDATION_FAILED, "zr_replay_exchange_fn: no recorded buffer");
+    if (bytes_per_rank == 0 || r->bytes == 0 || r->bytes % bytes_per_rank != 0 || r->bytes / bytes_per_rank > kMaxShards)
+        return fail(ZR_ERROR_VALIDATION_FAILED,
+                    "zr_replay_exchange_fn: recorded bytes are not whole exchange blocks of this draw's layout");
     ZR_HIP(hipMemcpyAsync(recv, r->src, r->bytes, hipMemcpyDeviceToDevice, (hipStream_t)stream));
     return ZR_SUCCESS;
 }
+
+}  // namespace
 
 ZR_API zr_exchange_fn zr_replay_exchange_fn(void) { return &replay_exchange; }
 
@@ -2081,7 +2103,8 @@ ZR_API zr_result zr_device_gather_tile_rows(zr_device* d, zr_texture* t, int32_t
         so += op.bytes * op.rows;
     }
     std::string err;
-    bool ok = rccl_group_start(err);
+    std::vector<P2POp> ops;
+    ops.reserve(plan.size());
     so = 0;
     for (const zr_transfer_op& op : plan) {
         uint8_t* p = (uint8_t*)t->ptr + op.offset;
@@ -2091,10 +2114,10 @@ ZR_API zr_result zr_device_gather_tile_rows(zr_device* d, zr_texture* t, int32_t
             bytes = op.bytes * op.rows;
             so += bytes;
         }
-        ok = ok && (op.send ? rccl_send(p, bytes, op.peer, d->comm_g, gs, err)
-                            : rccl_recv(p, bytes, op.peer, d->comm_g, gs, err));
+        ops.push_back(P2POp{p, (size_t)bytes, op.peer, op.send != 0});
     }
-    if (!rccl_group_end(err) || !ok) return fail(ZR_ERROR_DEVICE_LOST, err);
+    // one balanced group (rccl_grouped: no ncclGroupEnd after a failed start)
+    if (!rccl_grouped(ops.data(), ops.size(), d->comm_g, gs, err)) return fail(ZR_ERROR_DEVICE_LOST, err);
     so = 0;
     for (const zr_transfer_op& op : plan) {  // the root unpacks after the group
         if (op.rows <= 1) continue;

@@ -398,9 +398,8 @@ class GraphicShaderInputBuilder:
         validation, performed by the C ABI's pipeline validator."""
         inp = GraphicShaderInput(self._vs, self._fs, list(self._bindings), list(self._attrs))
         # ShaderReflection::merge (shader.rs:224-228): the largest stage block
-        if hasattr(lib(), "zr_shader_push_constant_size"):  # (absent only from pre-round-4 A/B builds)
-            inp.push_constant_size = max([lib().zr_shader_push_constant_size(sh.handle)
-                                          for sh in (self._vs, self._fs) if sh is not None] + [0])
+        inp.push_constant_size = max([lib().zr_shader_push_constant_size(sh.handle)
+                                      for sh in (self._vs, self._fs) if sh is not None] + [0])
         dev_free_desc = _pipeline_desc(inp, GraphicPipelineState(), [], None)
         h = C.c_void_p()
         err = zr.zr_pipeline_error()

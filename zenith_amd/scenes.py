@@ -254,20 +254,41 @@ def config_bytes_per_triangle(cfg: str) -> int:
 # zenith-core/src/camera.rs: Camera::view_projection = proj * view (:85-87) with
 # proj = Mat4::perspective_infinite_reverse_rh(fov_y, aspect, near) (:50, :60) and
 # view = Mat4::look_to_rh(position, forward, WORLD_SPACE_UP = +Z) (:121-124), in
-# glam 0.30's column-major layout, restated in float32 as glam computes them.
+# glam 0.30's column-major layout, restated in float32 operation by operation as
+# glam's scalar code computes them (Rust does not contract a * b + c into an FMA):
+# Vec3::dot = (x x' + y y') + z z', Vec3::cross, Vec3::normalize = v * (1 / length),
+# and Mat4 * Mat4 column by column as Mat4::mul_vec4 does,
+# ((A.x * b.x + A.y * b.y) + A.z * b.z) + A.w * b.w, every product and sum rounded
+# to f32 (tests/test_oracle.py::test_view_projection_f32_bits).
 NEAR_PLANE = 0.1          # camera.rs:16
 WORLD_UP = (0.0, 0.0, 1.0)
+_F = np.float32
+
+
+def _dot3(a, b):
+    return (_F(a[0]) * _F(b[0]) + _F(a[1]) * _F(b[1])) + _F(a[2]) * _F(b[2])
+
+
+def _cross3(a, b):
+    a, b = [_F(x) for x in a], [_F(x) for x in b]
+    return (a[1] * b[2] - b[1] * a[2], a[2] * b[0] - b[2] * a[0], a[0] * b[1] - b[0] * a[1])
+
+
+def _normalize3(v):
+    r = _F(1.0) / _F(np.sqrt(_dot3(v, v)))  # Vec3::length_recip: 1 / sqrt(dot), f32
+    return tuple(_F(x) * r for x in v)
 
 
 def perspective_infinite_reverse_rh(fov_y: float, aspect: float, z_near: float) -> np.ndarray:
     """glam Mat4::perspective_infinite_reverse_rh: columns
-    (f/aspect,0,0,0), (0,f,0,0), (0,0,0,-1), (0,0,z_near,0), f = 1/tan(fov_y/2)."""
-    f = np.float32(1.0) / np.float32(math.tan(np.float32(0.5) * np.float32(fov_y)))
+    (f/aspect,0,0,0), (0,f,0,0), (0,0,0,-1), (0,0,z_near,0), f = 1/tan(fov_y/2)
+    (f32::tan: the float64 tangent of the f32 argument, rounded once)."""
+    f = _F(1.0) / _F(math.tan(_F(0.5) * _F(fov_y)))
     m = np.zeros((4, 4), np.float32)  # m[col][row]
-    m[0, 0] = f / np.float32(aspect)
+    m[0, 0] = f / _F(aspect)
     m[1, 1] = f
     m[2, 3] = -1.0
-    m[3, 2] = np.float32(z_near)
+    m[3, 2] = _F(z_near)
     return m
 
 
@@ -275,26 +296,40 @@ def look_to_rh(eye, direction, up) -> np.ndarray:
     """glam Mat4::look_to_rh: f = normalize(dir), s = normalize(f x up), u = s x f;
     columns (s.x,u.x,-f.x,0), (s.y,u.y,-f.y,0), (s.z,u.z,-f.z,0),
     (-dot(eye,s), -dot(eye,u), dot(eye,f), 1)."""
-    e = np.asarray(eye, np.float32)
-    f = np.asarray(direction, np.float32)
-    f = f / np.float32(np.sqrt(np.dot(f, f)))
-    s_ = np.cross(f, np.asarray(up, np.float32)).astype(np.float32)
-    s_ = s_ / np.float32(np.sqrt(np.dot(s_, s_)))
-    u = np.cross(s_, f).astype(np.float32)
+    e = tuple(_F(x) for x in eye)
+    f = _normalize3(direction)
+    s_ = _normalize3(_cross3(f, up))
+    u = _cross3(s_, f)
     m = np.zeros((4, 4), np.float32)
     m[0] = (s_[0], u[0], -f[0], 0.0)
     m[1] = (s_[1], u[1], -f[1], 0.0)
     m[2] = (s_[2], u[2], -f[2], 0.0)
-    m[3] = (-np.dot(e, s_), -np.dot(e, u), np.dot(e, f), 1.0)
+    m[3] = (-_dot3(e, s_), -_dot3(e, u), _dot3(e, f), 1.0)
     return m
 
 
+def mat4_mul(a: np.ndarray, b: np.ndarray) -> np.ndarray:
+    """glam Mat4 * Mat4 (column-major m[col][row]): column c of the product is
+    Mat4::mul_vec4(a, b[c]) = ((a.x * b.x + a.y * b.y) + a.z * b.z) + a.w * b.w,
+    componentwise in f32 (products and sums each rounded)."""
+    a = np.asarray(a, np.float32)
+    b = np.asarray(b, np.float32)
+    out = np.zeros((4, 4), np.float32)
+    for c in range(4):
+        col = a[0] * b[c, 0]
+        col = col + a[1] * b[c, 1]
+        col = col + a[2] * b[c, 2]
+        col = col + a[3] * b[c, 3]
+        out[c] = col
+    return out
+
+
 def view_projection(eye, forward, fov_y=math.pi / 6, aspect=1.77777, z_near=NEAR_PLANE) -> tuple:
-    """proj * view as 16 column-major floats (the View uniform's bytes)."""
+    """Camera::view_projection = proj * view as 16 column-major floats (the View
+    uniform's bytes)."""
     proj = perspective_infinite_reverse_rh(fov_y, aspect, z_near)
     view = look_to_rh(eye, forward, WORLD_UP)
-    vp = (view.astype(np.float64) @ proj.astype(np.float64))  # column-major: (P V)[c] = sum_k V[c][k] P[k]
-    return tuple(float(x) for x in vp.astype(np.float32).reshape(-1))
+    return tuple(float(x) for x in mat4_mul(proj, view).reshape(-1))
 
 
 def mesh_soup_scene(seed: int, n: int, width: int, height: int, extent: float = 6.0,
