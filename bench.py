@@ -54,10 +54,11 @@ def parse():
                    help="diagnostic (1 GPU): every rank of a G-way tile-row shard in turn, beside the unsharded "
                         "frame; reports the max-over-ranks frame time and T1 / that (no gather; partitioned "
                         "setup: each rank receives the records the other ranks really route to it)")
-    p.add_argument("--setup", choices=["partitioned", "replicated"], default="replicated",
+    p.add_argument("--setup", choices=["auto", "partitioned", "replicated"], default="auto",
                    help="tile-row shards: set up every primitive on every rank (binning only its own rows), "
-                        "or route 1/G of the primitives per rank through an RCCL all-to-all (DESIGN.md §7; "
-                        "1-GPU emulation: equal at G=8, slower at G=2/4, before the all-to-all's own cost)")
+                        "or route 1/G of the primitives per rank through an RCCL all-to-all (DESIGN.md §7); "
+                        "auto (default): partitioned for dense draws at 8+ ranks, replicated otherwise "
+                        "(setup_mode: the 1-GPU emulation's slowest rank, round 4)")
     p.add_argument("--comm", choices=["runtime", "torch"], default="runtime",
                    help="multi-GPU collectives: the runtime's own RCCL communicators (exchange + row gather "
                         "enqueued from C++), or torch.distributed's (Python callbacks)")
@@ -74,6 +75,21 @@ def parse():
 
 
 SETUP_IN_BYTES = 12 + 3 * 12    # what k_setup_bin loads per triangle: 3 u32 indices + 3 float3 positions
+
+
+def setup_mode(requested, world, triangles, width, height):
+    """--setup auto: which setup a G-way tile-row shard uses.
+    Partitioned setup ships 1/G of the set-up records per rank through an
+    all-to-all, replicated setup repeats the whole setup on every rank; the
+    1-GPU emulation of the slowest rank (profiles/r04_v3_bench_*shard8*) has
+    partitioned ahead where setup dominates the rank -- dense draws, 256+
+    triangles per 32x32 tile, at 8 ranks (C2: 35.8 vs 47.7 us) -- and replicated
+    ahead elsewhere (C3, 122 per tile: 51.7 vs 54.3 us at 8 ranks; at 2 and 4
+    ranks the route and exchange stages cost more than the setup they split)."""
+    if requested != "auto":
+        return requested
+    tiles = ((width + shard.TILE - 1) // shard.TILE) * ((height + shard.TILE - 1) // shard.TILE)
+    return "partitioned" if world >= 8 and triangles >= 256 * tiles else "replicated"
 
 
 def winner_bytes(program, index_size=4):
@@ -213,6 +229,7 @@ def emulate(a, scene, cuda):
     of the received bytes stands in for it)."""
     G = a.emulate_shard
     W, H, N = scene.width, scene.height, scene.triangles
+    a.setup = setup_mode(a.setup, G, N, W, H)
     dev = rhi.RenderDevice(0)
     color_t = torch.zeros((H, W * 4), dtype=torch.uint8, device=cuda)
     depth_t = torch.zeros((H, W), dtype=torch.float32, device=cuda)
@@ -406,6 +423,8 @@ def main():
 
     scene = scenes.config_scene(a.config)
     W, H, N = scene.width, scene.height, scene.triangles
+    if a.emulate_shard <= 1:
+        a.setup = setup_mode(a.setup, world, N, W, H)
     if a.emulate_shard > 1:
         if distributed:
             raise SystemExit("--emulate-shard is a 1-GPU diagnostic")

@@ -139,6 +139,10 @@ typedef struct zr_draw_stats {
      * with zr_device_set_profiling(dev, 2) (0 otherwise): the resolve's per-winner
      * gathers (vertex ids, attributes) are counted against it (bench.py) */
     uint64_t winners;
+    /* micro primitives (a clipped bbox of one pixel) of the last draw that cover
+     * their sample: setup tests each one and drops those that miss it before
+     * they are binned */
+    uint64_t micro_fragments;
 } zr_draw_stats;
 ZR_API zr_result zr_device_last_draw_stats(zr_device *dev, zr_draw_stats *out);
 /* Last error message recorded on this thread (for logging; never NULL). */

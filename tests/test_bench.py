@@ -99,6 +99,20 @@ def test_bench_emulate_shard(setup):
         assert sum(r["triangles_setup"] for r in d["ranks"]) >= 100_000 * 0.9
 
 
+def test_setup_auto():
+    """--setup auto (the default): partitioned for dense draws (256+ triangles
+    per 32x32 tile) at 8+ ranks -- C2 at 8 -- replicated otherwise (C2 at 2/4, C3
+    and C1 at 8, any single GPU); an explicit choice is kept."""
+    import bench
+    assert bench.setup_mode("auto", 8, 1_000_000, 1920, 1080) == "partitioned"
+    for g in (1, 2, 4):
+        assert bench.setup_mode("auto", g, 1_000_000, 1920, 1080) == "replicated"
+    assert bench.setup_mode("auto", 8, 1_000_000, 3840, 2160) == "replicated"
+    assert bench.setup_mode("auto", 8, 100_000, 1920, 1080) == "replicated"
+    assert bench.setup_mode("replicated", 8, 1_000_000, 1920, 1080) == "replicated"
+    assert bench.setup_mode("partitioned", 2, 100_000, 1920, 1080) == "partitioned"
+
+
 # ------------------------------------------------ launcher-less multi-GPU runs
 def test_worker_commands():
     """bench.py --gpus N without a launcher: N children of the same script with the

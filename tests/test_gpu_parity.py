@@ -384,12 +384,100 @@ def test_c3_4k_shards_union(device):
 
 
 def test_c4_micro_triangles(device):
-    """C4: 10M sub-pixel triangles at 1080p; exact vs the oracle."""
+    """C4: 10M sub-pixel triangles at 1080p; exact vs the oracle.  4.8 primitives
+    per pixel: setup's micro-primitive test is on by default (use_micro_test) and
+    drops the ones that miss their sample."""
     s = scenes.config_scene("c4")
     gc, gd = renderer.render_scene(device, s)
+    assert device.last_draw_stats()["micro_fragments"] > 100_000
     oc, od = oracle.render(s, nthreads=16)
     assert np.array_equal(gc, oc)
     assert np.array_equal(gd.view(np.uint32), od.view(np.uint32))
+
+
+def mixed_micro_scene(seed, n, width, height, program, flat_z=None):
+    """Micro primitives (bbox < 1 px: resolved by k_setup_bin, DrawParams::
+    micro_keys) interleaved in API order with ordinary 6-px ones (binned and
+    walked by k_tile): every third primitive is ordinary.  flat_z: every vertex
+    at that depth, so every fragment of a pixel ties and only API order decides."""
+    normals = program == scenes.PROGRAM_BLINN_PHONG
+    micro = scenes.soup_arrays(seed, n, width, height, 0.45, normals).reshape(n, 3, -1)
+    big = scenes.soup_arrays(seed + 1000, n, width, height, 6.0, normals).reshape(n, 3, -1)
+    pick = (np.arange(n) % 3 == 0)[:, None, None]
+    verts = np.where(pick, big, micro)
+    if flat_z is not None:
+        verts[:, :, 2] = flat_z
+    return scenes.Scene(f"mixed_micro_s{seed}", width, height, program, verts.reshape(3 * n, -1),
+                        np.arange(3 * n, dtype=np.uint32), depth=True)
+
+
+@pytest.fixture(scope="module")
+def micro_device():
+    """A device with setup's micro-primitive test forced on (ZR_MICRO=1, read at
+    device creation; by default only draws of >= 1 primitive per pixel get it)."""
+    import os
+    old = os.environ.get("ZR_MICRO")
+    os.environ["ZR_MICRO"] = "1"
+    dev = rhi.RenderDevice(0)
+    if old is None:
+        del os.environ["ZR_MICRO"]
+    else:
+        os.environ["ZR_MICRO"] = old
+    yield dev
+    dev.close()
+
+
+@pytest.mark.parametrize("op,clear,flat", [(scenes.OP_LESS, 1.0, None), (scenes.OP_LEQUAL, 1.0, 0.5),
+                                           (scenes.OP_LESS, 1.0, 0.5), (scenes.OP_GREATER, 0.0, None),
+                                           (scenes.OP_GEQUAL, 0.0, 0.25)])
+def test_micro_primitives_mixed(micro_device, op, clear, flat):
+    """Micro primitives (tested for their one sample by setup, dropped there when
+    they miss it: DrawParams::micro) beside ordinary ones, API order mixed: depth
+    modes, and with every depth equal the order rules (LESS: first wins, LEQUAL /
+    GEQUAL: last wins).  The draw stats count the covered micro primitives, so the
+    path is known to run."""
+    device = micro_device
+    s = mixed_micro_scene(83, 60_000, 320, 240, scenes.PROGRAM_BLINN_PHONG, flat)
+    s.depth_op, s.depth_clear = op, clear
+    assert_parity(device, s)
+    assert device.last_draw_stats()["micro_fragments"] > 1000
+
+
+def test_micro_primitives_modes(micro_device):
+    """The micro path under no depth attachment (last wins by API order), depth
+    test without writes (last-wins pre-test against the loaded depth), a 3-way
+    tile-row shard (only owned tiles' samples), a partial last tile row, the
+    triangle program, and a one-pixel scissor."""
+    device = micro_device
+    s = mixed_micro_scene(84, 40_000, 300, 170, scenes.PROGRAM_FLAT_COLOR)
+    s.depth = False
+    assert_parity(device, s)
+    assert device.last_draw_stats()["micro_fragments"] > 1000
+    s = mixed_micro_scene(85, 40_000, 300, 170, scenes.PROGRAM_FLAT_COLOR)
+    s.depth_write = False  # (depth test, no writes: last wins among those passing the loaded depth)
+    assert_parity(device, s)
+    assert device.last_draw_stats()["micro_fragments"] > 1000
+    s = mixed_micro_scene(86, 40_000, 300, 170, scenes.PROGRAM_BLINN_PHONG)
+    for r in range(3):
+        assert_parity(device, s, shard=(r, 3))
+    s = mixed_micro_scene(87, 20_000, 300, 170, scenes.PROGRAM_TRIANGLE)
+    s.time = 1.25
+    assert_parity(device, s)
+    # a one-pixel scissor: every primitive's clipped bbox is that pixel, yet the
+    # large ones (extents far past 64 px) stay on the ordinary path
+    s = scenes.soup_scene(89, 3000, 200, 160, 60.0, scenes.PROGRAM_FLAT_COLOR)
+    assert_parity(device, s, scissor=(97, 61, 1, 1))
+    s = mixed_micro_scene(90, 30_000, 200, 160, scenes.PROGRAM_BLINN_PHONG)
+    assert_parity(device, s, scissor=(33, 21, 1, 1))
+
+
+def test_micro_primitives_repeat(micro_device):
+    """Back-to-back frames of a micro-heavy draw with no host sync in between:
+    the last frame equals the oracle's."""
+    s = mixed_micro_scene(88, 50_000, 256, 192, scenes.PROGRAM_FLAT_COLOR)
+    gc, gd = renderer.render_scene(micro_device, s, frames=3)
+    oc, od = oracle.render(s)
+    assert np.array_equal(gc, oc) and np.array_equal(gd.view(np.uint32), od.view(np.uint32))
 
 
 def test_determinism_repeat(device):

@@ -195,6 +195,7 @@ enum StatusWord : uint32_t {
     kStDroppedClip = 4,
     kStRouteMax = 5,        // partitioned draws: the largest per-destination entry total routed (since the last sync)
     kStRouteFallback = 6,   // partitioned draws whose received blocks overflowed (set up in full; since the last sync)
+    kStMicro = 7,           // covered micro primitives of the last draw
     kStWords = 16,
 };
 // Device counters of k_setup_bin, read by the draw's k_tile (tile 0 reports them
@@ -204,6 +205,7 @@ enum CounterWord : uint32_t {
     kCtMaxTile = 2,   // the largest tile list of the draw (pairs, including any past the slab)
     kCtPairs = 4,     // u64 (words 4-5): (tile, primitive) pairs of the draw
     kCtSchedTicket = 6,  // k_setup_bin workgroups past phase 2 (the last one builds the tile schedule)
+    kCtMicro = 7,        // covered micro primitives of the draw (DrawParams::micro)
     kCtWords = 32,
 };
 // draw_info words (written by k_setup_bin for k_tile)
@@ -299,6 +301,11 @@ struct DrawParams {
     uint32_t* tile_order;     // tile schedule (k_setup_bin's last workgroup -> k_tile), or nullptr: xcd_tile order
     uint32_t* win_bits;       // winner census (zr_device_set_profiling level 2): bit p = draw primitive p won a pixel
     uint32_t* status;         // host-mapped
+    // Micro primitives: k_setup_bin tests a primitive whose clipped
+    // pixel bbox is a single pixel (a small one) for coverage of that pixel's
+    // sample, and drops it -- no record, no bin entry -- when it yields no
+    // fragment (C4: most of its 10M primitives).  0: off (ZR_MICRO=0, A/B).
+    uint32_t micro;
     // push-constant state at the draw (zr_cmd_push_constants): the bytes ride in
     // the launch's kernel arguments, as Vulkan push constants ride in user SGPRs
     // (last, so the fields above keep their kernarg offsets)
@@ -345,6 +352,14 @@ inline uint32_t tile_threads_for(uint32_t ntiles, uint32_t cus, uint64_t prims, 
 // lane), at least 16, at most one per CU.  One per CU (the unpartitioned choice)
 // left most of a workgroup's waves idle and multiplied the per-tile counter
 // atomics (round 4, emulated rank of 8: C2 frame 43.6 -> 38.4 us, C3 equal).
+// Whether k_setup_bin tests micro primitives for their one sample
+// (DrawParams::micro): for draws of at least one primitive per pixel of the
+// render area, whose mean primitive is then sub-pixel.  C4 (10M over 2.07M
+// pixels): frame 406.9 -> 320.6 us; on C2 (0.5 per pixel, 0.15 % of its
+// primitives micro) the test measured +1.7 us of setup for nothing, so sparser
+// draws skip it (docs/EXPERIMENTS.md, round 5).
+inline bool use_micro_test(uint64_t prims, uint64_t pixels) { return prims >= pixels; }
+
 inline uint32_t records_setup_wgs(uint64_t entries, uint32_t cus) {
     const uint64_t w = (entries + 2047u) / 2048u;
     return (uint32_t)std::max<uint64_t>(1u, std::min<uint64_t>(cus ? cus : 1u, std::max<uint64_t>(16u, w)));

@@ -751,14 +751,34 @@ __device__ __forceinline__ BBox setup_finish_mesh(const DrawParams& P, uint32_t 
     return box[0];
 }
 
-// Setup of draw primitive `prim`; returns its tile bbox (empty when culled or
-// owning no tile).
+// A micro primitive: its clipped bbox is one pixel, so at most that pixel's
+// centre is a sample, and it is small (extents <= 64 px), so its edge values
+// there fit int32 (products below 2^28, as in k_tile's lane walk).  Whether it
+// covers the sample, by k_tile's biased sign test: one that does not yields no
+// fragment and needs neither a record nor a bin entry (DrawParams::micro; k_tile
+// tests the covered ones again, with their depth).
+__device__ __forceinline__ bool micro_covers(const PrimGeom& g) {
+    const int Sx = g.px0 * 256 + 128, Sy = g.py0 * 256 + 128;
+    const int* X = g.X;
+    const int* Y = g.Y;
+    const int w0 = (X[2] - X[1]) * (Sy - Y[1]) - (Y[2] - Y[1]) * (Sx - X[1]) - (int)((g.flags >> 1) & 1u);
+    const int w1 = (X[0] - X[2]) * (Sy - Y[2]) - (Y[0] - Y[2]) * (Sx - X[2]) - (int)((g.flags >> 2) & 1u);
+    const int w2 = (X[1] - X[0]) * (Sy - Y[0]) - (Y[1] - Y[0]) * (Sx - X[0]) - (int)((g.flags >> 3) & 1u);
+    return (w0 | w1 | w2) >= 0;
+}
+
+// Setup of draw primitive `prim`; returns its tile bbox (empty when culled,
+// owning no tile, or a micro primitive that misses its sample).
 __device__ __forceinline__ BBox setup_finish(const DrawParams& P, uint32_t prim, const PrimIn& in, uint32_t* s_hist,
-                                             int& nvalid, int& ndropped) {
+                                             int& nvalid, int& ndropped, int& nmicro) {
     BBox box{kEmptyBox, 0u};
     PrimGeom g;
     if (prim_geometry(P, in, g, ndropped)) {
         ++nvalid;
+        if (P.micro && g.px0 == g.px1 && g.py0 == g.py1 && (g.flags & kFlagSmall)) {
+            if (!micro_covers(g)) return box;  // no fragment: no record, no bin entry
+            ++nmicro;
+        }
         if (count_owned(P, g, s_hist)) box = write_record(P, prim, g);
     }
     return box;
@@ -1040,7 +1060,7 @@ __global__ __launch_bounds__(kSetupThreads) void k_setup_bin(DrawParams P) {
     }
 
     // ---- phase 1
-    int nvalid = 0, ndropped = 0;
+    int nvalid = 0, ndropped = 0, nmicro = 0;
     if (rec_mode) {  // the received entries: records stored at their draw ids, bboxes counted
         const DrawParams& P = kernarg_params();
         const uint32_t lane = tid & 63u, wave = tid >> 6;
@@ -1083,7 +1103,7 @@ __global__ __launch_bounds__(kSetupThreads) void k_setup_bin(DrawParams P) {
                     if constexpr (MESH)
                         box = setup_finish_mesh(P, prim, in[b], s_hist, nvalid, ndropped);
                     else
-                        box = setup_finish(P, prim, in[b], s_hist, nvalid, ndropped);
+                        box = setup_finish(P, prim, in[b], s_hist, nvalid, ndropped, nmicro);
                     // global: the overflow scan of any tile may need it; LDS: phase 4
                     P.bboxes[prim] = box;
                     if (P.bbox_lds) s_bbox[lb + b * 64u] = box;
@@ -1093,6 +1113,7 @@ __global__ __launch_bounds__(kSetupThreads) void k_setup_bin(DrawParams P) {
     }
     if (nvalid) atomicAdd(&s_misc[0], (uint32_t)nvalid);
     if (ndropped) atomicAdd(&s_misc[1], (uint32_t)ndropped);
+    if (nmicro) atomicAdd(&s_misc[6], (uint32_t)nmicro);
     __syncthreads();
     ZR_STAMP(1);
     if (P.debug & kDebugPhase1Only) return;
@@ -1127,6 +1148,7 @@ __global__ __launch_bounds__(kSetupThreads) void k_setup_bin(DrawParams P) {
         if (tid == 0) {
             if (s_misc[0]) atomicAdd(&P.counters[kCtSetup], s_misc[0]);
             if (s_misc[1]) atomicAdd(&P.counters[kCtDropped], s_misc[1]);
+            if (s_misc[6]) atomicAdd(&P.counters[kCtMicro], s_misc[6]);
             if (s_misc[2]) atomicMax(&P.counters[kCtMaxTile], s_misc[2]);
             if (s_misc[3]) atomicAdd(reinterpret_cast<unsigned long long*>(&P.counters[kCtPairs]), (unsigned long long)s_misc[3]);
         }
@@ -2234,6 +2256,7 @@ __global__ __launch_bounds__(NT, kTileWgs * kTileThreads / 256) void k_tile(Draw
         const unsigned long long pairs = *reinterpret_cast<const unsigned long long*>(&P.counters[kCtPairs]);
         st[kStTrianglesSetup] = P.counters[kCtSetup];
         st[kStDroppedClip] = P.counters[kCtDropped];
+        st[kStMicro] = P.counters[kCtMicro];
         st[kStTotalPairs] = pairs > 0xFFFFFFFFull ? 0xFFFFFFFFu : (uint32_t)pairs;
         if (top > slab) {  // draws run in stream order
             st[kStOverflow] += 1u;

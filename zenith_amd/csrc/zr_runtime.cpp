@@ -258,6 +258,7 @@ struct zr_device_t {
     int tile_sched = -1;       // ZR_TILE_SCHED=0/1 forces the heaviest-first tile schedule (A/B); -1: use_tile_schedule
     uint32_t rec_wgs = 0;      // ZR_REC_WGS: k_setup_bin workgroups of partitioned (records-mode) draws; 0: one per CU
     int bin_stage = -1;        // ZR_BIN_STAGE: k_setup_bin phase 4 staged through LDS (1), direct (0), default (-1)
+    int micro = -1;            // ZR_MICRO=0/1: setup's micro-primitive test off / on; -1: use_micro_test
     int cu_count = 0;
     uint32_t occupancy_checked_tiles = 0;
     bool occupancy_checked_mesh = false;
@@ -471,6 +472,7 @@ zr_result device_sync(zr_device* d) {
     d->last.bin_pairs = st[kStTotalPairs];
     d->last.triangles_setup = st[kStTrianglesSetup];
     d->last.triangles_dropped_clip = st[kStDroppedClip];
+    d->last.micro_fragments = st[kStMicro];
     d->overflowed_draws += st[kStOverflow];
     d->last.overflowed_draws = d->overflowed_draws;
     // partitioned draws since the previous sync point
@@ -878,6 +880,9 @@ zr_result exec_draw(zr_device* d, ExecState& s, const Cmd& c, bool indexed) {
         const bool on = d->bin_stage > 0 || (d->bin_stage < 0 && kBinStageDefault && !overlap_setup);
         P.bin_stage = on && cap >= 1024u ? (uint32_t)cap : 0u;
     }
+    // (records mode never runs setup_finish: no effect there)
+    P.micro = (d->micro < 0 ? use_micro_test(prims, (uint64_t)(P.ra_x1 - P.ra_x0 + 1) * (uint64_t)(P.ra_y1 - P.ra_y0 + 1))
+                            : d->micro != 0) ? 1u : 0u;
     P.tile_threads = d->tile_threads ? d->tile_threads
                                      : tile_threads_for(P.ntiles, (uint32_t)std::max(d->cu_count, 1), prims, partitioned);
     P.rec_table = (d->rec_table < 0 ? use_record_table(prims, P.tiles_x, P.tiles_y) : d->rec_table != 0) ? 1u : 0u;
@@ -1140,6 +1145,7 @@ ZR_API zr_result zr_device_create(int32_t hip_device, zr_device** out) {
     if (const char* ts = getenv("ZR_TILE_SCHED")) d->tile_sched = strtoul(ts, nullptr, 0) != 0 ? 1 : 0;
     if (const char* rw = getenv("ZR_REC_WGS")) d->rec_wgs = (uint32_t)strtoul(rw, nullptr, 0);
     if (const char* bs = getenv("ZR_BIN_STAGE")) d->bin_stage = atoi(bs);
+    if (const char* mi = getenv("ZR_MICRO")) d->micro = atoi(mi) != 0 ? 1 : 0;
     if (const char* nt = getenv("ZR_TILE_NT")) {
         const unsigned long v = strtoul(nt, nullptr, 0);
         d->tile_threads = v >= 512 ? 512u : v ? 256u : 0u;
