@@ -50,6 +50,9 @@ namespace zr {
 #ifndef ZR_TAB
 #define ZR_TAB 1
 #endif
+#ifndef ZR_RESOLVE_DEDUP512
+#define ZR_RESOLVE_DEDUP512 0  // 1: 512-thread tiles resolve through resolve_tile (each distinct winner fetched once per tile)
+#endif
 #ifndef ZR_TILE_DEBUG
 #define ZR_TILE_DEBUG 0      // 1: k_tile honours the ZR_DEBUG timing switches and stamps
                              // (the checks cost the production kernel SGPRs)
@@ -2191,7 +2194,7 @@ __global__ __launch_bounds__(NT, kTileWgs * kTileThreads / 256) void k_tile(Draw
     float* s_initd = reinterpret_cast<float*>(s_bucket + kSortBuckets);  // [kTilePixels] (INITD)
     // 512-thread tiles: the record table of the resolve (rec_table_insert); last-wins
     // modes need the records' depth terms, which it does not hold
-    constexpr bool kTab = ZR_TAB && NT >= 512 && MODE != kDepthLastWins && PROG != kProgMesh && !INITD;
+    constexpr bool kTab = ZR_TAB && !ZR_RESOLVE_DEDUP512 && NT >= 512 && MODE != kDepthLastWins && PROG != kProgMesh && !INITD;
     int4* s_trec = reinterpret_cast<int4*>(s_bucket + kSortBuckets);        // [kSortCap]
     uint32_t* s_thash = reinterpret_cast<uint32_t*>(s_trec + kSortCap);      // [kRecHashSlots]
     uint32_t& s_claim = s_misc[0];   // next 64-entry chunk of the segment to rasterize
@@ -2510,7 +2513,7 @@ __global__ __launch_bounds__(NT, kTileWgs * kTileThreads / 256) void k_tile(Draw
 
     // Resolve (the index width is a template parameter so a winner's record and
     // index loads are issued back to back).
-    if (NT >= 512) {
+    if (NT >= 512 && !ZR_RESOLVE_DEDUP512) {
         if (P.index_size == 4)
             resolve_pixels<PROG, MODE, true, NT, kTab>(kernarg_params(), x0, y0, s_key, s_srgb, s_thash, s_trec, s_sorted);
         else
