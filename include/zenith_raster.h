@@ -143,6 +143,10 @@ typedef struct zr_draw_stats {
      * their sample: setup tests each one and drops those that miss it before
      * they are binned */
     uint64_t micro_fragments;
+    /* (tile, primitive) pairs of the last draw stored in pool runs past their
+     * tiles' slabs, and those runs; bin_capacity counts slabs and
+     * pool together */
+    uint64_t bin_pool_pairs, bin_pool_runs;
 } zr_draw_stats;
 ZR_API zr_result zr_device_last_draw_stats(zr_device *dev, zr_draw_stats *out);
 /* Last error message recorded on this thread (for logging; never NULL). */

@@ -176,27 +176,96 @@ def test_bin_overflow_spill(monkeypatch):
         dev.close()
 
 
-def test_slab_overflow_one_tile():
-    """Tile lists live in fixed per-tile slabs (bin buffer / tiles): a draw whose
-    pairs fit the buffer but whose one crowded tile outgrows its slab rasterizes
-    that tile by the record scan and every other tile from its list, in the same
-    pass; the runtime then grows the slabs."""
+def crowded_tile_scene():
+    """9000 small triangles in the 32x32 tile (5, 7) of a 640x480 target among
+    3000 spread ones: one tile list ~60x the mean."""
     w, h = 640, 480
     dense = scenes.soup_arrays(41, 9000, 32, 32, 2.0, False)  # 9000 small triangles, most in one 32x32 tile
     dense[:, 0] = dense[:, 0] * (32.0 / w) + (2 * 32 * 5 + 32) / w - 1.0  # tile (5, 7)
     dense[:, 1] = dense[:, 1] * (32.0 / h) + (2 * 32 * 7 + 32) / h - 1.0
     sparse = scenes.soup_arrays(42, 3000, w, h, 10.0, False)
     v = np.concatenate([sparse[:4500], dense, sparse[4500:]]).astype(np.float32)
-    s = scenes.Scene("slab_overflow", w, h, scenes.PROGRAM_FLAT_COLOR, v, np.arange(len(v), dtype=np.uint32),
-                     depth=True)
+    return scenes.Scene("slab_overflow", w, h, scenes.PROGRAM_FLAT_COLOR, v, np.arange(len(v), dtype=np.uint32),
+                        depth=True)
+
+
+def test_slab_overflow_one_tile():
+    """A crowded tile whose list outgrows its slab keeps its excess in pool runs
+    (DrawParams::runs), read after the slab part, with no record scan: on the
+    first draw (slabs of a third of the buffer) and on later ones (slabs of the
+    measured target, bin_slab_target)."""
+    s = crowded_tile_scene()
     dev = rhi.RenderDevice(0)
     try:
-        assert_parity(dev, s)
-        st = dev.last_draw_stats()
-        # 2^20 entries over 300 tiles: slabs of 3495 < the crowded tile's ~8900
-        assert st["overflowed_draws"] == 1 and st["bin_pairs"] < (1 << 20)
-        assert_parity(dev, s)
-        assert dev.last_draw_stats()["overflowed_draws"] == 1  # grown: no new overflow
+        for _ in range(3):
+            assert_parity(dev, s)
+            st = dev.last_draw_stats()
+            assert st["overflowed_draws"] == 0, st
+            assert st["bin_pool_runs"] > 0 and 0 < st["bin_pool_pairs"] < st["bin_pairs"], st
+    finally:
+        dev.close()
+
+
+@pytest.mark.parametrize("slab", ["0", "24", "300"])
+def test_pool_runs(monkeypatch, slab):
+    """Slabs forced small (ZR_BIN_SLAB; 0: every pair in a pool run): every tile
+    list is read through its run table -- soups on 256- and 512-thread tiles with
+    the record table on and off, a tile-row shard, the camera program's fans, the
+    wave path, lists of several 1024-entry segments, records-mode (partitioned)
+    setup and repeated frames -- exact, with no record scan."""
+    monkeypatch.setenv("ZR_BIN_SLAB", slab)
+    for nt, table in (("256", "1"), ("512", "1"), ("512", "0")):
+        monkeypatch.setenv("ZR_TILE_NT", nt)
+        monkeypatch.setenv("ZR_REC_TABLE", table)
+        dev = rhi.RenderDevice(0)
+        try:
+            assert_parity(dev, scenes.config_scene("c1", n=30000, width=640, height=360))
+            assert_parity(dev, scenes.soup_scene(18, 4000, 512, 384, 12.0, scenes.PROGRAM_BLINN_PHONG), shard=(1, 3))
+            assert_parity(dev, scenes.soup_scene(17, 300, 512, 384, 150.0, scenes.PROGRAM_FLAT_COLOR))
+            assert_parity(dev, crowded_tile_scene())
+            assert dev.last_draw_stats()["bin_pool_runs"] > 0
+            assert_parity(dev, scenes.cerberus_scene(640, 480))
+            assert dev.last_draw_stats()["overflowed_draws"] == 0
+        finally:
+            dev.close()
+    monkeypatch.delenv("ZR_TILE_NT")
+    monkeypatch.delenv("ZR_REC_TABLE")
+    dev = rhi.RenderDevice(0)
+    try:
+        # frames back to back: each tile pass resets the run words the next
+        # draw's setup fills (a tile resetting its run word before every wave had
+        # read it sent the others past its slab)
+        s = scenes.config_scene("c2", n=200_000)
+        gc, gd = renderer.render_scene(dev, s, frames=8)
+        oc, od = oracle.render(s, nthreads=16)
+        assert np.array_equal(gc, oc) and np.array_equal(gd.view(np.uint32), od.view(np.uint32))
+        assert dev.last_draw_stats()["overflowed_draws"] == 0
+    finally:
+        dev.close()
+    assert_partitioned_parity(scenes.soup_scene(70, 20000, 320, 240, 10.0, scenes.PROGRAM_BLINN_PHONG), 3)
+
+
+@pytest.mark.parametrize("cfg", ["c2x", "c3x"])
+def test_clustered_first_frame(cfg):
+    """Gaussian-clustered 1M-triangle scenes (scenes.clustered_scene; c2x at 1080p,
+    central tiles ~40x the mean list; c3x at 4K): on a fresh device the first
+    frame already holds every pair (the crowded tiles' excess in pool runs, no
+    tile takes the record scan), the second frame too (slabs of the measured
+    target), both exact; the bin buffer then holds at most 2x the pairs plus 512
+    entries per tile."""
+    s = scenes.config_scene(cfg)
+    oc, od = oracle.render(s, nthreads=16)
+    ntiles = -(-s.width // 32) * -(-s.height // 32)
+    dev = rhi.RenderDevice(0)
+    try:
+        for frame in range(2):
+            gc, gd = renderer.render_scene(dev, s)
+            st = dev.last_draw_stats()
+            assert st["overflowed_draws"] == 0, (frame, st)
+            assert st["bin_pool_runs"] > 0, (frame, st)
+            assert np.array_equal(gc, oc), frame
+            assert np.array_equal(gd.view(np.uint32), od.view(np.uint32)), frame
+        assert st["bin_capacity"] <= 2 * st["bin_pairs"] + 512 * ntiles, st
     finally:
         dev.close()
 

@@ -87,6 +87,23 @@ constexpr uint32_t kEmptyBox = 0xFFFFFFFFu;
 // tile's entries by it so that a 64-lane chunk holds walks of similar length).
 constexpr uint32_t kBinPrimBits = 26;
 constexpr uint32_t kBinPrimMask = (1u << kBinPrimBits) - 1u;
+// k_setup_bin's cursor for a run the pool could not hold: its pairs are dropped
+// (phase 4 stores only below 2^31; bin buffers stay under 2^30 entries) and the
+// tile takes k_tile's record scan.
+constexpr uint32_t kDropCursor = 0xC0000000u;
+// run_counts[t] (DrawParams::runs): pool runs of tile t in bits [0, 9), the slab
+// fill in bits [9, 30) with kRunFill when a run straddled the slab end, kRunDropped
+// when a run was dropped.  Slabs are capped at kMaxSlab entries so the fill fits.
+constexpr uint32_t kRunCountMask = 0x1FFu;
+constexpr uint32_t kRunFillShift = 9;
+constexpr uint32_t kMaxSlab = (1u << 21) - 1u;
+constexpr uint32_t kRunFill = 1u << 30;
+constexpr uint32_t kRunDropped = 1u << 31;
+// tile_counts[t] bit 31: the tile has a pool run (set by k_setup_bin pool_run), so
+// k_tile reads its run word -- a tile without one reads nothing more than its count
+// (an extra load and reset store of the run word per tile: C3 tile pass +4 us)
+constexpr uint32_t kCountRuns = 1u << 31;
+constexpr uint32_t kMaxRunsPerTile = 256;  // k_tile keeps a tile's run table in its 512-word wave-path queue
 struct alignas(8) BBox {
     uint32_t bb0, bb1;  // as TriRecord::bb0/bb1
 };
@@ -187,16 +204,23 @@ enum : uint32_t { kDebugSkipRaster = 1u, kDebugSkipShade = 2u, kDebugLoadOnly = 
                   kDebugIdentityVids = 2048u, kDebugSameVids = 4096u, kDebugSameRecord = 8192u };
 
 // Status words in host-mapped pinned memory (read by the runtime at sync points).
+constexpr uint32_t kSlabSlots = 48;  // draws per sync interval that report their slab target
 enum StatusWord : uint32_t {
     kStTotalPairs = 0,      // (tile, primitive) pairs of the last draw (saturating)
-    kStOverflow = 1,        // draws with a tile list longer than its slab (since the last sync)
-    kStMaxPairs = 2,        // bin entries (ntiles * longest list) the largest such draw needs
+    kStOverflow = 1,        // draws with a pair run the pool could not hold (since the last sync)
+    // (word 2 unused)
     kStTrianglesSetup = 3,
     kStDroppedClip = 4,
     kStRouteMax = 5,        // partitioned draws: the largest per-destination entry total routed (since the last sync)
     kStRouteFallback = 6,   // partitioned draws whose received blocks overflowed (set up in full; since the last sync)
     kStMicro = 7,           // covered micro primitives of the last draw
-    kStWords = 16,
+    kStBinNeed = 8,         // the largest bin buffer a draw with a dropped run asked for since the last sync
+                            // (entries, saturating): tiles x bin_slab_target + the pool entries its runs asked for
+    kStPoolPairs = 9,       // pairs the last draw put in pool runs (saturating)
+    kStPoolRuns = 10,       // pool runs of the last draw
+    kStSlabSlot0 = 16,      // [kSlabSlots]: the slab target (bin_slab_target) of the draw given slot i (DrawParams::stat_slot)
+    kStPoolSlot0 = 64,      // [kSlabSlots]: the pool entries that draw's runs asked for (saturating)
+    kStWords = 112,
 };
 // Device counters of k_setup_bin, read by the draw's k_tile (tile 0 reports them
 // and resets them, as every tile resets its count, so a draw needs no memset).
@@ -206,6 +230,8 @@ enum CounterWord : uint32_t {
     kCtPairs = 4,     // u64 (words 4-5): (tile, primitive) pairs of the draw
     kCtSchedTicket = 6,  // k_setup_bin workgroups past phase 2 (the last one builds the tile schedule)
     kCtMicro = 7,        // covered micro primitives of the draw (DrawParams::micro)
+    kCtPoolTop = 8,      // u64 (words 8-9): pool entries the draw's runs asked for (the bump allocator; may pass pool_cap)
+    kCtPoolRuns = 10,    // pool runs the draw registered
     kCtWords = 32,
 };
 // draw_info words (written by k_setup_bin for k_tile)
@@ -285,11 +311,11 @@ struct DrawParams {
     TriRecord* records_big;   // [prims] full records, written for large primitives only
     float4* mesh_edges;       // mesh program: [prims][3] homogeneous edge coefficients (shade_mesh)
     BBox* bboxes;             // [prims]; bb0 == kEmptyBox when culled / no owned tile
-    uint32_t* tile_counts;    // [ntiles] pairs per tile (zero between draws)
+    uint32_t* tile_counts;    // [ntiles] pairs per tile | kCountRuns (zero between draws)
     uint32_t* draw_info;      // [kInfoWords] (DrawInfoWord)
     uint32_t* counters;       // [kCtWords] (CounterWord)
-    uint32_t* bins;           // [ntiles * slab] tile t's list at [t * slab, t * slab + count): id | area bucket
-    uint32_t slab;            // list capacity per tile (host: bin buffer / ntiles)
+    uint32_t* bins;           // [pool_off + pool_cap] tile t's slab at [t * slab, (t + 1) * slab), then the pool
+    uint32_t slab;            // slab entries per tile
     uint32_t setup_wgs;       // workgroups of k_setup_bin (one per CU at most)
     uint32_t unit_shift;      // log2 primitives per claim unit (64 lanes * batch * rounds)
     uint32_t units;           // claim units of the draw: ceil(prims / unit size)
@@ -306,9 +332,23 @@ struct DrawParams {
     // sample, and drops it -- no record, no bin entry -- when it yields no
     // fragment (C4: most of its 10M primitives).  0: off (ZR_MICRO=0, A/B).
     uint32_t micro;
+    // Overflow runs: a workgroup whose run of pairs for tile t does
+    // not fit what is left of t's slab stores it in the pool instead,
+    // bins[pool_off + base, + its pairs) from a bump allocator (kCtPoolTop), and
+    // registers (pool_off + base, pairs) in runs[t * run_cap + d], d from
+    // run_counts[t] (one run per setup workgroup and tile).  The run that
+    // straddles the slab end records its offset, the slab's fill (kRunFill); a run
+    // the pool cannot hold is dropped (kRunDropped) and k_tile takes that tile by
+    // its record scan.
+    uint32_t pool_off, pool_cap, run_cap;
+    uint32_t stat_slot;       // status slot for this draw's slab target (kStSlabSlot0 + i), or >= kSlabSlots: none
+    uint2* runs;              // [ntiles * run_cap] (bins index, pairs)
+    uint32_t* run_counts;     // [ntiles] (kRunCountMask etc.; zero between draws: k_tile resets it)
     // push-constant state at the draw (zr_cmd_push_constants): the bytes ride in
     // the launch's kernel arguments, as Vulkan push constants ride in user SGPRs
-    // (last, so the fields above keep their kernarg offsets)
+    // (last, so the fields above keep their kernarg offsets; fields added later
+    // go above it, after the older ones, for the same reason: k_tile's reloads of
+    // the parameters are grouped scalar loads)
     float push[kMaxPushWords];
 };
 
@@ -359,6 +399,26 @@ inline uint32_t tile_threads_for(uint32_t ntiles, uint32_t cus, uint64_t prims, 
 // primitives micro) the test measured +1.7 us of setup for nothing, so sparser
 // draws skip it (docs/EXPERIMENTS.md, round 5).
 inline bool use_micro_test(uint64_t prims, uint64_t pixels) { return prims >= pixels; }
+
+// The slab (entries per tile) a draw's tiles want: the draw's mean list length
+// plus three standard deviations of a Poisson count plus 64, so uniform scenes do
+// not overflow (C2: mean 645, longest 741, target 785) and skewed scenes put only
+// their crowded tiles' excess in the pool.  Evaluated by k_tile's tile 0 (the
+// draw's pair total is known there) and applied by the runtime to later draws.
+__host__ __device__ inline uint32_t bin_slab_target(uint64_t pairs, uint32_t ntiles) {
+    if (!ntiles) return 0;
+    const float mean = (float)pairs / (float)ntiles;
+    const float t = mean + 3.0f * sqrtf(mean) + 64.0f;
+    return t >= (float)kMaxSlab ? kMaxSlab : (uint32_t)t;
+}
+
+// The bin buffer (entries) of a scratch set's first draw, before any draw has
+// been measured: twice the primitives plus 256 per tile.  That draw takes slabs of
+// a third of it (zr_runtime ensure_scratch) and the pool the rest, which holds
+// the Gaussian-clustered c2x / c3x scenes' first frames without a dropped run.
+inline uint64_t bin_default_capacity(uint64_t prims, uint32_t ntiles) {
+    return std::max<uint64_t>(1ull << 20, 2 * prims + 256ull * ntiles);
+}
 
 inline uint32_t records_setup_wgs(uint64_t entries, uint32_t cus) {
     const uint64_t w = (entries + 2047u) / 2048u;

@@ -939,7 +939,7 @@ __device__ void build_tile_schedule(const DrawParams& P, uint32_t nt, uint32_t* 
     const uint32_t shift = top >= kSchedBuckets ? 32u - __clz(top / kSchedBuckets) : 0u;  // top >> shift < 64
     __syncthreads();
     auto key = [&](uint32_t t, uint32_t& x) {  // XCD and descending-weight bucket of tile t
-        const uint32_t c = __hip_atomic_fetch_add(&P.tile_counts[t], 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        const uint32_t c = __hip_atomic_fetch_add(&P.tile_counts[t], 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) & ~kCountRuns;
         x = xcd_block(t, nt) & 7u;
         return kSchedBuckets - 1u - min(c >> shift, kSchedBuckets - 1u);
     };
@@ -983,12 +983,14 @@ __device__ void build_tile_schedule(const DrawParams& P, uint32_t nt, uint32_t* 
 //            64-B requests); the value returned is this workgroup's offset inside
 //            the tile's list
 //   phase 4  scatter the workgroup's (tile, primitive) pairs straight into the
-//            tile's slab: tile t's list lives at bins[t * slab, (t + 1) * slab),
-//            so a list start needs no scan of the totals (the round-1 design's
-//            grid barrier + phase 3 scan cost ~6 us of a C2 frame).  Pairs past a
-//            full slab are dropped and counted: k_tile rasterizes that tile
-//            exactly by scanning every record's bbox, and the runtime grows the
-//            bin buffer at the next sync point.
+//            tile's slab: tile t's list starts at bins[t * slab], so a list
+//            start needs no scan of the totals (the round-1 design's grid
+//            barrier + phase 3 scan cost ~6 us of a C2 frame).  A workgroup's
+//            pairs that do not fit the rest of the slab go to a pool run
+//            (pool_run); a run the pool cannot hold is dropped and counted:
+//            k_tile rasterizes that tile exactly by scanning every record's
+//            bbox, and the runtime grows the bin buffer at the next sync point
+//            (DESIGN.md §4).
 // Order inside a tile's list is arbitrary (whatever order the atomics returned),
 // which is free: visibility keys carry the primitive sequence (k_tile).  The
 // counters return to zero in k_tile, so a draw needs no memset.
@@ -996,6 +998,59 @@ __device__ void build_tile_schedule(const DrawParams& P, uint32_t nt, uint32_t* 
     do {                                                                                    \
         if ((P.debug & kDebugStamps) && tid == 0) P.dbg_ts[w * 8 + (i)] = __builtin_amdgcn_s_memrealtime(); \
     } while (0)
+
+// Phase 2's overflow run (DrawParams::runs): this workgroup's c pairs for tile t,
+// reserved at offset o (ov: the count the atomic returned) of the tile's list, do not fit the rest of its slab; they
+// go to the pool.  The run takes a slot in t's run table and an offset inside the
+// workgroup's pool allocation (an LDS counter, s_pool[0]); the allocation itself
+// is one atomic per workgroup after the tile loop (pool_commit), which turns the
+// returned kPoolPending | slot into the run's bin position.  (One pool atomic per
+// run: the clustered c2x scene's ~31k runs queued on that address, setup
+// 772 us.)  Returns kDropCursor when t's run table is full.
+constexpr uint32_t kPoolPending = 0x40000000u;
+__device__ __noinline__ uint32_t pool_run(const DrawParams& P, uint32_t t, uint32_t ov, uint32_t c, uint32_t* s_pool) {
+    uint32_t* rc = &P.run_counts[t];
+    if (!(ov & kCountRuns)) atomicOr(&P.tile_counts[t], kCountRuns);  // (the first run of the tile, as far as this workgroup saw)
+    const uint32_t o = ov & ~kCountRuns;
+    if (o < P.slab) atomicOr(rc, kRunFill | (o << kRunFillShift));  // the slab holds [0, o) of the list
+    const uint32_t d = atomicAdd(rc, 1u) & kRunCountMask;
+    if (d >= P.run_cap) {
+        atomicOr(rc, kRunDropped);
+        return kDropCursor;
+    }
+    P.runs[(size_t)t * P.run_cap + d] = make_uint2(atomicAdd(&s_pool[0], c), c);
+    atomicAdd(&s_pool[1], 1u);
+    return kPoolPending | d;
+}
+
+// After phase 2's tile loop (same thread -> tile mapping): the workgroup's pool
+// runs take one allocation of s_pool[0] entries; each pending cursor becomes its
+// run's position, or kDropCursor (and the tile's kRunDropped) when the pool is full.
+__device__ __noinline__ void pool_commit(const DrawParams& P, uint32_t* s_hist, uint32_t* s_pool, uint32_t rot) {
+    const uint32_t nt = P.ntiles, tid = threadIdx.x;
+    if (tid == 0) {
+        const unsigned long long base =
+            atomicAdd(reinterpret_cast<unsigned long long*>(&P.counters[kCtPoolTop]), (unsigned long long)s_pool[0]);
+        s_pool[2] = base + s_pool[0] <= P.pool_cap ? P.pool_off + (uint32_t)base : kDropCursor;
+        atomicAdd(&P.counters[kCtPoolRuns], s_pool[1]);
+    }
+    __syncthreads();
+    const uint32_t pb = s_pool[2];
+    for (uint32_t i = tid; i < nt; i += kSetupThreads) {
+        const uint32_t t = i + rot < nt ? i + rot : i + rot - nt;
+        const uint32_t v = s_hist[t];
+        if ((v >> 30) != 1u) continue;  // not pending
+        uint2* e = &P.runs[(size_t)t * P.run_cap + (v & kRunCountMask)];
+        if (pb != kDropCursor) {
+            const uint32_t x = pb + e->x;
+            e->x = x;
+            s_hist[t] = x;
+        } else {
+            atomicOr(&P.run_counts[t], kRunDropped);
+            s_hist[t] = kDropCursor;
+        }
+    }
+}
 
 // i-th unit of primitives owned by workgroup w: interleaved (unit u -> workgroup
 // u mod G), so every workgroup streams from the whole input at once (contiguous
@@ -1132,8 +1187,9 @@ __global__ __launch_bounds__(kSetupThreads) void k_setup_bin(DrawParams P) {
         for (uint32_t i = tid; i < nt; i += kSetupThreads) {
             const uint32_t t = i + rot < nt ? i + rot : i + rot - nt;
             const uint32_t c = s_hist[t];
-            const uint32_t o = c ? __hip_atomic_fetch_add(&P.tile_counts[t], c, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) : 0u;
-            s_hist[t] = t * P.slab + o;
+            const uint32_t ov = c ? __hip_atomic_fetch_add(&P.tile_counts[t], c, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) : 0u;
+            const uint32_t o = ov & ~kCountRuns;
+            s_hist[t] = o + c <= P.slab ? t * P.slab + o : pool_run(P, t, ov, c, s_misc + 8);
             if (P.bin_stage) s_lcur[t] = c;
             top = max(top, o + c);
             sum += c;
@@ -1154,6 +1210,10 @@ __global__ __launch_bounds__(kSetupThreads) void k_setup_bin(DrawParams P) {
             if (s_misc[6]) atomicAdd(&P.counters[kCtMicro], s_misc[6]);
             if (s_misc[2]) atomicMax(&P.counters[kCtMaxTile], s_misc[2]);
             if (s_misc[3]) atomicAdd(reinterpret_cast<unsigned long long*>(&P.counters[kCtPairs]), (unsigned long long)s_misc[3]);
+        }
+        if (s_misc[8]) {  // (the barrier above: every pool_run of this workgroup is done)
+            pool_commit(P, s_hist, s_misc + 8, rot);
+            __syncthreads();
         }
         if (P.tile_order) {
             // The last workgroup to take a ticket sees every tile's final count: the
@@ -1183,7 +1243,7 @@ __global__ __launch_bounds__(kSetupThreads) void k_setup_bin(DrawParams P) {
         // (the parameters the loops use, read once: kernarg_params() would reload them
         // per iteration)
         uint32_t* const bins = P.bins;
-        const uint32_t slab = P.slab, sG = P.shard_count, srank = P.shard_rank, tiles_x = P.tiles_x;
+        const uint32_t sG = P.shard_count, srank = P.shard_rank, tiles_x = P.tiles_x;
         const uint32_t full_rows = P.full_rows, own_rows = P.own_rows, left_lo = P.left_lo, left_hi = P.left_hi;
         auto scatter = [&](uint32_t rec, const BBox bb) {
             if (bb.bb0 == kEmptyBox) return;
@@ -1200,7 +1260,7 @@ __global__ __launch_bounds__(kSetupThreads) void k_setup_bin(DrawParams P) {
                 const uint32_t steps = (uint32_t)(((cx1 - cx0 + 2) >> 1) * (cy1 - cy0 + 1));
                 const uint32_t bucket = min((steps - 1u) >> 1, kSortBuckets - 1u);
                 const uint32_t pos = atomicAdd(&s_hist[t], 1u);
-                if (pos - t * slab < slab) bins[pos] = rec | (bucket << kBinPrimBits);
+                if (pos < 0x80000000u) bins[pos] = rec | (bucket << kBinPrimBits);  // (not a dropped run)
             });
         };
         uint32_t nown = 0;
@@ -1250,7 +1310,7 @@ __global__ __launch_bounds__(kSetupThreads) void k_setup_bin(DrawParams P) {
                 const uint32_t bucket = min((steps - 1u) >> 1, kSortBuckets - 1u);
                 const uint32_t l = atomicAdd(&s_lcur[t], 1u);
                 const uint32_t pos = s_hist[t] + l;
-                s_stage[l] = make_uint2(pos - t * slab < slab ? pos : 0xFFFFFFFFu, rec | (bucket << kBinPrimBits));
+                s_stage[l] = make_uint2(pos < 0x80000000u ? pos : 0xFFFFFFFFu, rec | (bucket << kBinPrimBits));
             });
         };
         for (uint32_t j = tid; staged && j < (nown << P.unit_shift); j += kSetupThreads) {
@@ -2231,13 +2291,70 @@ __global__ __launch_bounds__(NT, kTileWgs * kTileThreads / 256) void k_tile(Draw
             ent[k] = i < n ? bp[i] : 0u;  // prim | cost bucket (k_setup_bin phase 4)
         }
     };
+    // A list with pool runs (rare: crowded tiles) is loaded through the run table,
+    // held in the wave-path queue's LDS (free between segments): run bases in
+    // s_big[0, 256), exclusive pair offsets in s_big[256, 512); a position past the
+    // slab part finds its run by binary search.
+    static_assert(NT >= (int)kMaxRunsPerTile && 2u * kMaxRunsPerTile <= kBigQueue, "run table staging");
+    auto load_segment_runs = [&](uint32_t seg, uint32_t n, uint32_t slab_len, uint32_t nruns) {
+        const DrawParams& P = kernarg_params();  // (re-loaded here, not held across the pass)
+        // one descriptor per thread (the loads in flight together), then wave 0's
+        // exclusive scan of the run lengths
+        if (threadIdx.x < nruns) {
+            const uint2 r = P.runs[(size_t)t * P.run_cap + threadIdx.x];
+            s_big[threadIdx.x] = r.x;
+            s_big[kMaxRunsPerTile + threadIdx.x] = r.y;
+        }
+        __syncthreads();
+        if (threadIdx.x < 64) {
+            uint32_t carry = 0;
+            for (uint32_t i0 = 0; i0 < nruns; i0 += 64u) {
+                const uint32_t i = i0 + threadIdx.x;
+                const uint32_t len = i < nruns ? s_big[kMaxRunsPerTile + i] : 0u;
+                uint32_t inc = len;
+#pragma unroll
+                for (int d = 1; d < 64; d <<= 1) {
+                    const uint32_t y = __shfl_up(inc, d, 64);
+                    if ((int)threadIdx.x >= d) inc += y;
+                }
+                if (i < nruns) s_big[kMaxRunsPerTile + i] = carry + inc - len;
+                carry += (uint32_t)__shfl((int)inc, 63, 64);
+            }
+        }
+        __syncthreads();
+        // the segment's entries to s_sorted (free until the sort rewrites [0, n)),
+        // then to the registers load_segment fills
+        for (uint32_t i = threadIdx.x; i < n; i += NT) {
+            const uint32_t p = seg + i;
+            uint32_t e;
+            if (p < slab_len) {
+                e = P.bins[lbeg + p];
+            } else {
+                const uint32_t q = p - slab_len;
+                uint32_t lo = 0, hi = nruns;  // the last run whose offset is <= q
+                while (hi - lo > 1u) {
+                    const uint32_t mid = (lo + hi) >> 1;
+                    if (s_big[kMaxRunsPerTile + mid] <= q) lo = mid; else hi = mid;
+                }
+                e = P.bins[s_big[lo] + (q - s_big[kMaxRunsPerTile + lo])];
+            }
+            s_sorted[i] = e;
+        }
+        __syncthreads();
+#pragma unroll
+        for (uint32_t k = 0; k < kPerThread; ++k) {
+            const uint32_t i = threadIdx.x + k * NT;
+            ent[k] = i < n ? s_sorted[i] : 0u;
+        }
+    };
     if (!(tile_debug(P) & kDebugSkipRaster)) load_segment(0, min(kSortCap, slab));
-    const uint32_t count = P.tile_counts[t];
-    // A tile whose list outgrew its slab (the runtime grows the bin buffer for
-    // later draws) is rasterized exactly but slowly: it scans every record's bbox
-    // (k_setup_bin stored them all) instead of reading its list.
-    const bool spill = count > slab;
-    const uint32_t cnt = spill ? 0u : count;
+    const uint32_t count_v = P.tile_counts[t];
+    const uint32_t count = count_v & ~kCountRuns;
+    // The list: the slab's first slab_len entries, then the tile's pool runs
+    // (k_setup_bin pool_run), count entries in all.  A tile with a dropped run (the
+    // pool was full; the runtime grows the bin buffer for later draws) is
+    // rasterized exactly but slowly: it scans every record's bbox (k_setup_bin
+    // stored them all) instead.  Only a tile with kCountRuns reads its run word.
 
     for (int i = threadIdx.x; i < kTilePixels; i += NT) {
         const int px = x0 + (i & (kTile - 1)), py = y0 + (i >> kTileShift);
@@ -2251,29 +2368,52 @@ __global__ __launch_bounds__(NT, kTileWgs * kTileThreads / 256) void k_tile(Draw
     if (tab)
         for (uint32_t i = threadIdx.x; i < kRecHashSlots; i += NT) s_thash[i] = 0u;
     if (threadIdx.x < 2) s_dbg[threadIdx.x] = 0u;
-    // tile 0 reports the draw's setup and binning stats (k_setup_bin's counters,
-    // complete before this launch) and flags a slab overflow to the runtime
-    if (t == 0 && threadIdx.x == 0) {
-        volatile uint32_t* st = P.status;
-        const uint32_t top = P.counters[kCtMaxTile];
+    // The first block dispatched reports the draw's setup and binning stats
+    // (k_setup_bin's counters, complete before this launch) to the runtime's status
+    // words: plain stores, no read of host memory unless a run was dropped
+    // (volatile accesses wait for each one to cross the bus).  Draws run in stream
+    // order; the host reads the words after a stream sync.
+    if (blockIdx.x == 0 && threadIdx.x == 0) {
+        uint32_t* st = P.status;
         const unsigned long long pairs = *reinterpret_cast<const unsigned long long*>(&P.counters[kCtPairs]);
+        const unsigned long long pool = *reinterpret_cast<const unsigned long long*>(&P.counters[kCtPoolTop]);
         st[kStTrianglesSetup] = P.counters[kCtSetup];
         st[kStDroppedClip] = P.counters[kCtDropped];
         st[kStMicro] = P.counters[kCtMicro];
         st[kStTotalPairs] = pairs > 0xFFFFFFFFull ? 0xFFFFFFFFu : (uint32_t)pairs;
-        if (top > slab) {  // draws run in stream order
-            st[kStOverflow] += 1u;
-            const unsigned long long need = (unsigned long long)top * P.ntiles;  // bin entries for slabs of `top`
+        st[kStPoolPairs] = pool > 0xFFFFFFFFull ? 0xFFFFFFFFu : (uint32_t)pool;
+        st[kStPoolRuns] = P.counters[kCtPoolRuns];
+        const uint32_t target = bin_slab_target(pairs, P.ntiles);
+        if (pool > P.pool_cap) {  // a dropped run: the buffer this draw asks for (read-modify-write only here)
+            const unsigned long long need = (unsigned long long)P.ntiles * target + pool;
             const uint32_t need32 = need > 0x80000000ull ? 0x80000000u : (uint32_t)need;
-            if (need32 > st[kStMaxPairs]) st[kStMaxPairs] = need32;
+            const uint32_t ov = st[kStOverflow], bn = st[kStBinNeed];
+            st[kStOverflow] = ov + 1u;
+            if (need32 > bn) st[kStBinNeed] = need32;
+        }
+        if (P.stat_slot < kSlabSlots) {  // (the runtime derives the buffer the draw asks for from these)
+            st[kStSlabSlot0 + P.stat_slot] = target;
+            st[kStPoolSlot0 + P.stat_slot] = pool > 0xFFFFFFFFull ? 0xFFFFFFFFu : (uint32_t)pool;
         }
     }
     __syncthreads();
+    const bool has_runs = (__builtin_amdgcn_readfirstlane((int)count_v) & (int)kCountRuns) != 0;
+    const uint32_t rcw = has_runs ? (uint32_t)__builtin_amdgcn_readfirstlane((int)P.run_counts[t]) : 0u;
+    const bool spill = (rcw & kRunDropped) != 0u;
+    const uint32_t cnt = spill ? 0u : count;
+    // (the segment loop reads slab_len and the run count back from LDS, each wave
+    // its own leader's copy: held in registers across the pass they cost the C2
+    // instance VGPR spills)
+    if ((threadIdx.x & 63u) == 0) {
+        s_misc[8] = (rcw & kRunFill) ? (rcw & ~(kRunFill | kRunDropped)) >> kRunFillShift : min(count, slab);
+        s_misc[9] = min(rcw & kRunCountMask, P.run_cap);
+    }
     // k_setup_bin's counters back to zero for the next draw on this scratch set:
-    // each tile its own count (every wave has read it: the barrier above), tile 0
-    // the draw counters
+    // each tile its own count (every wave has read it: the barrier above) and, at
+    // the end of the tile, its run word (read after that barrier), block 0 the draw
+    // counters
     if (threadIdx.x == 0) P.tile_counts[t] = 0u;
-    if (t == 0)
+    if (blockIdx.x == 0)
         for (uint32_t i = threadIdx.x; i < kCtWords; i += NT) P.counters[i] = 0u;
 
     const uint32_t wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
@@ -2287,10 +2427,18 @@ __global__ __launch_bounds__(NT, kTileWgs * kTileThreads / 256) void k_tile(Draw
         // lane per entry loads the 64-B record, and the wave walks the chunk.
         for (uint32_t seg = 0; seg < cnt; seg += kSortCap) {
             const uint32_t n = min(kSortCap, cnt - seg);
-            if (seg) load_segment(seg, n);
+            // a list with pool runs loads its segments past the slab part through
+            // the run table (s_misc[9]: runs, s_misc[8]: the slab part's length)
+            const uint32_t nr = (uint32_t)__builtin_amdgcn_readfirstlane((int)s_misc[9]);
+            const uint32_t slab_len = (uint32_t)__builtin_amdgcn_readfirstlane((int)s_misc[8]);
+            if (nr && seg + n > slab_len) {
+                load_segment_runs(seg, n, slab_len, nr);
+            } else if (seg) {
+                load_segment(seg, n);
+            }
             const DrawParams& P = kernarg_params();  // re-loaded per segment, not held across the pass
             if (threadIdx.x < kSortBuckets) s_bucket[threadIdx.x] = 0u;
-            if (threadIdx.x == 0) s_claim = s_nbig = s_bclaim = 0u;
+            if (threadIdx.x < 3) s_misc[threadIdx.x] = 0u;  // s_claim, s_nbig, s_bclaim
             __syncthreads();
             uint32_t pr[kPerThread], bk[kPerThread], sl[kPerThread];
 #pragma unroll
@@ -2525,6 +2673,9 @@ __global__ __launch_bounds__(NT, kTileWgs * kTileThreads / 256) void k_tile(Draw
         resolve_tile<PROG, MODE, false, NT>(kernarg_params(), x0, y0, s_key, s_u, kUnionWords, s_nwin, s_srgb,
                                            stamp ? ts : nullptr);
     }
+    // (s_misc[9]: the run count, >= 1 for a tile with kCountRuns; every wave read
+    // the run word before the segment loop)
+    if (threadIdx.x == 0 && s_misc[9]) P.run_counts[t] = 0u;
     if (stamp) {
         ts[4] = __builtin_amdgcn_s_memrealtime();
         ts[7] = ((unsigned long long)s_dbg[1] << 32) | s_dbg[0];

@@ -13,6 +13,7 @@
 #include <cstring>
 #include <map>
 #include <string>
+#include <unordered_map>
 #include <vector>
 
 #include "zenith_raster.h"
@@ -208,6 +209,10 @@ struct ScratchSet {
     uint64_t counters_cap = 0;
     uint32_t* bins = nullptr;
     uint64_t bins_cap = 0;
+    uint2* runs = nullptr;           // pool run table: [ntiles * run_cap] (DrawParams::runs)
+    uint64_t runs_cap = 0;
+    uint32_t* run_counts = nullptr;  // [ntiles] (zero between draws: k_tile resets it)
+    uint64_t run_counts_cap = 0;
     uint32_t* tile_order = nullptr;  // k_tile's block -> tile schedule (k_setup_bin's last workgroup writes it)
     uint64_t tile_order_cap = 0;
     uint8_t* xsend = nullptr;   // partitioned setup: exchange blocks (bytes)
@@ -264,8 +269,19 @@ struct zr_device_t {
     bool occupancy_checked_mesh = false;
     uint32_t tile_threads = 0; // k_tile workgroup size override (ZR_TILE_NT: 256, 512; 0 = by tile count)
     uint32_t debug = 0;
-    uint64_t initial_bins = 0;  // 0 = max(2^20, 2 * primitives of the first draw)
-    uint64_t min_bins = 0;      // bin capacity an overflow asked for
+    uint64_t initial_bins = 0;  // ZR_BIN_CAPACITY; 0 = bin_default_capacity of the first draw
+    uint64_t bins_want = 0;     // bin buffer the last sync's draws asked for (+10 %; 0: none measured yet)
+    uint64_t bins_want_max = 0; // ... the most any sync asked for since the last shrink check
+    uint32_t bins_syncs = 0;    // syncs with draws since the last shrink check
+    // slab targets (bin_slab_target) measured per draw shape, (tiles << 32) | primitives;
+    // the draws since the last sync, in status-slot order (DrawParams::stat_slot)
+    struct BinShape {
+        uint32_t target = 0;  // bin_slab_target
+        uint32_t pool = 0;    // pool entries its runs asked for (at the slab it had)
+    };
+    std::unordered_map<uint64_t, BinShape> bin_shapes;
+    std::vector<uint64_t> slab_keys;
+    uint32_t forced_slab = ~0u; // ZR_BIN_SLAB: every draw's slab (tests: pool runs everywhere)
     unsigned long long* dbg_ts = nullptr;  // kDebugStamps
     uint32_t dbg_wgs = 0, dbg_tiles = 0;
     std::string dbg_ts_path;
@@ -463,6 +479,8 @@ void dump_stamps(zr_device* d) {
     fclose(f);
 }
 
+constexpr uint32_t kBinShrinkSyncs = 16;
+
 zr_result device_sync(zr_device* d) {
     zr_result rc = set_device(d);
     if (rc) return rc;
@@ -473,8 +491,8 @@ zr_result device_sync(zr_device* d) {
     d->last.triangles_setup = st[kStTrianglesSetup];
     d->last.triangles_dropped_clip = st[kStDroppedClip];
     d->last.micro_fragments = st[kStMicro];
-    d->overflowed_draws += st[kStOverflow];
-    d->last.overflowed_draws = d->overflowed_draws;
+    d->last.bin_pool_pairs = st[kStPoolPairs];
+    d->last.bin_pool_runs = st[kStPoolRuns];
     // partitioned draws since the previous sync point
     if (st[kStRouteMax]) {  // kept from the last interval with partitioned draws
         d->last.route_max_entries = st[kStRouteMax];
@@ -485,26 +503,54 @@ zr_result device_sync(zr_device* d) {
     st[kStRouteFallback] = 0;
     d->pending.clear();
     if (d->dbg_ts && !d->dbg_ts_path.empty()) dump_stamps(d);
+    // Bin buffer sizing: later draws take slabs of the target the
+    // draws since the last sync asked for, and the buffer grows to what they asked
+    // for -- slabs plus the pool their runs needed -- when it is smaller (a draw with
+    // a dropped run rasterized that tile by k_tile's record scan).  Every
+    // kBinShrinkSyncs syncs it shrinks to the most any of them asked for when it is
+    // more than 1.5x that (not per sync: a device alternating between a light and a
+    // heavy scene would reallocate, and drop runs, every time).  (Capped at 2^30
+    // entries, 4 GiB: a larger draw keeps using the exact spill path.)
+    uint64_t need = st[kStBinNeed];  // (draws with a dropped run; the others from their slots)
+    st[kStBinNeed] = 0;
+    for (size_t i = 0; i < d->slab_keys.size(); ++i) {
+        const uint32_t target = st[kStSlabSlot0 + i], pool = st[kStPoolSlot0 + i];
+        if (!target) continue;
+        need = std::max<uint64_t>(need, (d->slab_keys[i] >> 32) * target + pool);
+        st[kStSlabSlot0 + i] = 0;
+        st[kStPoolSlot0 + i] = 0;
+        if (d->bin_shapes.size() >= 1024) d->bin_shapes.clear();  // (shapes that come and go)
+        zr_device_t::BinShape& v = d->bin_shapes[d->slab_keys[i]];
+        if (v.target != target || v.pool != pool) d->scratch_gen++;  // recorded graphs bake the slab in
+        v.target = target;
+        v.pool = pool;
+    }
+    d->slab_keys.clear();
     if (st[kStOverflow]) {
-        // Draws with a tile list longer than its slab (bin buffer / tiles) had that
-        // tile rasterized exactly by k_tile's scan of all records (slow); size the
-        // buffer so that every tile of the largest such draw gets a slab of its
-        // longest list, and later draws read tile lists again.  (Capped at 2^30
-        // entries, 4 GiB: a larger draw keeps using the exact spill path.)
-        const uint64_t need = std::min<uint64_t>((uint64_t)st[kStMaxPairs] * 5 / 4 + 4096, 1ull << 30);
+        d->overflowed_draws += st[kStOverflow];
         st[kStOverflow] = 0;
-        d->min_bins = std::max(d->min_bins, need);  // also for a scratch set not allocated yet
+    }
+    if (need) {
+        d->bins_want = std::min<uint64_t>(std::max<uint64_t>(need + need / 10 + 4096, 1ull << 20), 1ull << 30);
+        d->bins_want_max = std::max(d->bins_want_max, d->bins_want);
+        const bool check = ++d->bins_syncs >= kBinShrinkSyncs;
         for (ScratchSet& S : d->sets) {
-            if (!S.bins || S.bins_cap >= need) continue;
+            if (!S.bins || (S.bins_cap >= need && (!check || S.bins_cap * 2 <= d->bins_want_max * 3))) continue;
             ZR_HIP(hipFree(S.bins));
             S.bins = nullptr;
             void* p = nullptr;
-            ZR_HIP(hipMalloc(&p, need * 4));
+            const uint64_t size = check ? d->bins_want_max : d->bins_want;
+            ZR_HIP(hipMalloc(&p, size * 4));
             S.bins = (uint32_t*)p;
-            S.bins_cap = need;
+            S.bins_cap = size;
+            d->scratch_gen++;
         }
-        d->scratch_gen++;
+        if (check) {
+            d->bins_want_max = 0;
+            d->bins_syncs = 0;
+        }
     }
+    d->last.overflowed_draws = d->overflowed_draws;
     d->last.bin_capacity = d->sets[0].bins_cap;
     for (const ScratchSet& S : d->sets)
         if (S.bins) d->last.bin_capacity = std::min<uint64_t>(d->last.bin_capacity, S.bins_cap);
@@ -636,8 +682,15 @@ zr_result ensure_scratch(zr_device* d, ScratchSet& S, DrawParams& P) {
         if ((rc = grow(d, S.counters, S.counters_cap, kCtWords, 4))) return rc;
         ZR_HIP(hipMemset(S.counters, 0, S.counters_cap * 4));
     }
+    {  // per-tile run words start at zero; k_tile leaves them zero after every draw
+        const uint64_t cap = S.run_counts_cap;
+        if ((rc = grow(d, S.run_counts, S.run_counts_cap, P.ntiles + 1, 4))) return rc;
+        if (S.run_counts_cap != cap) ZR_HIP(hipMemset(S.run_counts, 0, S.run_counts_cap * 4));
+    }
+    P.run_cap = std::min<uint32_t>(P.setup_wgs, kMaxRunsPerTile);
+    if ((rc = grow(d, S.runs, S.runs_cap, (uint64_t)P.ntiles * P.run_cap, sizeof(uint2)))) return rc;
     if (!S.bins) {
-        const uint64_t want = std::max(d->min_bins, d->initial_bins ? d->initial_bins : std::max<uint64_t>(1u << 20, prims * 2));
+        const uint64_t want = std::max(d->bins_want, d->initial_bins ? d->initial_bins : bin_default_capacity(prims, P.ntiles));
         if ((rc = grow(d, S.bins, S.bins_cap, want, 4))) return rc;
     }
     if (!S.setup_done) {
@@ -653,8 +706,34 @@ zr_result ensure_scratch(zr_device* d, ScratchSet& S, DrawParams& P) {
     P.draw_info = S.draw_info;
     P.counters = S.counters;
     P.bins = S.bins;
-    // tile t's list lives at bins[t * slab, (t + 1) * slab)
-    P.slab = (uint32_t)std::min<uint64_t>(S.bins_cap / std::max<uint32_t>(P.ntiles, 1u), 0xFFFFFFFFull / std::max<uint32_t>(P.ntiles, 1u));
+    P.runs = S.runs;
+    P.run_counts = S.run_counts;
+    // tile t's slab is bins[t * slab, (t + 1) * slab), the pool the rest.  Before
+    // any measurement of the draw's shape: slabs of a third of the buffer.  After:
+    // the buffer less the pool the shape's runs asked for (+10 %, and at least an
+    // eighth of the buffer) over the tiles, but no less than the shape's target --
+    // a buffer larger than the pairs need (the 2^20-entry floor; C2's 2 x prims)
+    // goes to the slabs, where no run is needed (cerberus: the target slab put its
+    // crowded tiles' excess in runs, setup +8 us).
+    const uint64_t nt = std::max<uint32_t>(P.ntiles, 1u), cap = S.bins_cap;
+    const uint64_t key = ((uint64_t)P.ntiles << 32) | P.draw_prims;
+    const auto shape = d->bin_shapes.find(key);
+    uint64_t slab = cap / (3 * nt);
+    if (d->forced_slab != ~0u) {
+        slab = d->forced_slab;
+    } else if (shape != d->bin_shapes.end()) {
+        const uint64_t pool = std::max<uint64_t>((uint64_t)shape->second.pool * 11 / 10 + 4096, cap / 8);
+        slab = std::max<uint64_t>(shape->second.target, cap > pool ? (cap - pool) / nt : 0);
+    }
+    slab = std::min<uint64_t>({slab, cap / nt, (uint64_t)kMaxSlab});
+    P.slab = (uint32_t)slab;
+    P.pool_off = (uint32_t)(slab * P.ntiles);
+    P.pool_cap = (uint32_t)(S.bins_cap - slab * P.ntiles);
+    P.stat_slot = ~0u;
+    if (!d->capturing && d->slab_keys.size() < kSlabSlots) {
+        P.stat_slot = (uint32_t)d->slab_keys.size();
+        d->slab_keys.push_back(key);
+    }
     P.status = d->status_dev;
     return ZR_SUCCESS;
 }
@@ -940,6 +1019,7 @@ zr_result exec_draw(zr_device* d, ExecState& s, const Cmd& c, bool indexed) {
         if (d->debug) {
             ZR_HIP(hipMemsetAsync(P.counters, 0, kCtWords * 4, ss));
             ZR_HIP(hipMemsetAsync(P.tile_counts, 0, (size_t)P.ntiles * 4, ss));
+            ZR_HIP(hipMemsetAsync(P.run_counts, 0, (size_t)P.ntiles * 4, ss));
         }
         return ZR_SUCCESS;
     };
@@ -1139,6 +1219,7 @@ ZR_API zr_result zr_device_create(int32_t hip_device, zr_device** out) {
     if (const char* dbg = getenv("ZR_DEBUG")) d->debug = (uint32_t)strtoul(dbg, nullptr, 0);
     if (const char* p = getenv("ZR_DEBUG_TS")) d->dbg_ts_path = p;
     if (const char* cap = getenv("ZR_BIN_CAPACITY")) d->initial_bins = std::max<uint64_t>(64, strtoull(cap, nullptr, 0));
+    if (const char* sl = getenv("ZR_BIN_SLAB")) d->forced_slab = (uint32_t)std::min<uint64_t>(strtoull(sl, nullptr, 0), kMaxSlab);
     if (const char* g = getenv("ZR_GRAPH")) d->use_graphs = strtoul(g, nullptr, 0) != 0;
     if (const char* o = getenv("ZR_SETUP_OVERLAP")) d->setup_overlap = strtoul(o, nullptr, 0) != 0 ? 1 : 0;
     if (const char* rt = getenv("ZR_REC_TABLE")) d->rec_table = strtoul(rt, nullptr, 0) != 0 ? 1 : 0;
@@ -1183,7 +1264,7 @@ ZR_API void zr_device_destroy(zr_device* d) {
     if (d->dbg_ts) (void)hipFree(d->dbg_ts);
     if (d->win_bits) (void)hipFree(d->win_bits);
     for (ScratchSet& S : d->sets) {
-        for (void* p : {(void*)S.records, (void*)S.records_big, (void*)S.mesh_edges, (void*)S.bboxes, (void*)S.tile_counts,
+        for (void* p : {(void*)S.runs, (void*)S.run_counts, (void*)S.records, (void*)S.records_big, (void*)S.mesh_edges, (void*)S.bboxes, (void*)S.tile_counts,
                         (void*)S.draw_info, (void*)S.counters, (void*)S.bins, (void*)S.xsend, (void*)S.xrecv,
                         (void*)S.gids, (void*)S.tile_order})
             if (p) (void)hipFree(p);

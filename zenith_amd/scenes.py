@@ -215,6 +215,26 @@ def soup_arrays(seed: int, n: int, width: int, height: int, L: float, normals: b
     return out.reshape(n * 3, cols)
 
 
+def clustered_scene(seed: int, n: int, width: int, height: int, L: float, program: int, sigma: float = 0.12,
+                    name: str | None = None) -> Scene:
+    """A soup whose triangle centres are Gaussian around the screen centre
+    (sigma in NDC units, clipped to [-1, 1]) instead of uniform: a skewed scene
+    whose central tiles hold many times the mean list length (the bin layout's
+    worst case: DESIGN.md §4).  Same per-vertex stream
+    as soup_scene otherwise."""
+    verts = soup_arrays(seed, n, width, height, L, program == PROGRAM_BLINN_PHONG).reshape(n, 3, -1)
+    t = np.arange(n, dtype=np.uint64) * np.uint64(32)
+    u1 = np.maximum(_uniform(seed + 7919, t + np.uint64(30)), 2.0 ** -24)
+    u2 = _uniform(seed + 7919, t + np.uint64(31))
+    r = np.sqrt(-2.0 * np.log(u1)) * sigma
+    c = np.stack([r * np.cos(2 * np.pi * u2), r * np.sin(2 * np.pi * u2)], axis=1)
+    c = np.clip(c, -1.0, 1.0)
+    old_c = verts[:, :, :2].mean(axis=1, keepdims=True)
+    verts[:, :, :2] += (c[:, None, :] - old_c).astype(np.float32)
+    return Scene(name or f"clustered_s{seed}_n{n}", width, height, program, verts.reshape(3 * n, -1),
+                 np.arange(3 * n, dtype=np.uint32), depth=True, cull_mode=CULL_NONE)
+
+
 CONFIGS = {
     # id: (seed, triangles, width, height, L px, program)   SURVEY.md §8d table
     "c1": (1, 100_000, 1920, 1080, 12.0, PROGRAM_FLAT_COLOR),
@@ -224,6 +244,9 @@ CONFIGS = {
     # not a BASELINE config: the reference's real asset through the camera program
     # (SURVEY.md §8f rows 2-3), 33,543 triangles at 1080p
     "cerberus": (None, 33_543, 1920, 1080, None, PROGRAM_MESH),
+    # not BASELINE configs: C2's and C3's triangles, Gaussian-clustered (clustered_scene)
+    "c2x": (12, 1_000_000, 1920, 1080, 6.0, PROGRAM_BLINN_PHONG),
+    "c3x": (13, 1_000_000, 3840, 2160, 12.0, PROGRAM_BLINN_PHONG),
 }
 
 
@@ -241,6 +264,8 @@ def config_scene(cfg: str, n: int | None = None, width: int | None = None,
     seed, tris, w, h, L, prog = CONFIGS[cfg]
     if cfg == "cerberus":
         return cerberus_scene(width or w, height or h)
+    if cfg.endswith("x"):
+        return clustered_scene(seed, n or tris, width or w, height or h, L, prog, name=cfg)
     return soup_scene(seed, n or tris, width or w, height or h, L, prog, name=cfg)
 
 
