@@ -147,6 +147,9 @@ typedef struct zr_draw_stats {
      * tiles' slabs, and those runs; bin_capacity counts slabs and
      * pool together */
     uint64_t bin_pool_pairs, bin_pool_runs;
+    /* tile jobs of the last draw beyond one per tile: long tile lists split
+     * over several workgroups */
+    uint64_t tile_jobs;
 } zr_draw_stats;
 ZR_API zr_result zr_device_last_draw_stats(zr_device *dev, zr_draw_stats *out);
 /* Last error message recorded on this thread (for logging; never NULL). */

@@ -245,6 +245,51 @@ def test_pool_runs(monkeypatch, slab):
     assert_partitioned_parity(scenes.soup_scene(70, 20000, 320, 240, 10.0, scenes.PROGRAM_BLINN_PHONG), 3)
 
 
+@pytest.mark.parametrize("jobs", ["256", "1000"])
+def test_tile_jobs(monkeypatch, jobs):
+    """Tile lists split into jobs of ZR_JOBS entries, each its own k_tile block,
+    merging keys with 64-bit atomic mins; the last job of a tile resolves it.
+    Exact on 256- and 512-thread tiles with the record table on and off, a
+    tile-row shard, the camera program's fans, the wave path, a crowded tile
+    (~35 jobs), depth ops without writes (initial-depth tiles), jobs over pool
+    runs (slabs forced small), repeated frames and records-mode setup."""
+    monkeypatch.setenv("ZR_JOBS", jobs)
+    for nt, table, slab in (("256", "1", None), ("512", "1", None), ("512", "0", "24")):
+        monkeypatch.setenv("ZR_TILE_NT", nt)
+        monkeypatch.setenv("ZR_REC_TABLE", table)
+        if slab:
+            monkeypatch.setenv("ZR_BIN_SLAB", slab)
+        dev = rhi.RenderDevice(0)
+        try:
+            assert_parity(dev, scenes.config_scene("c1", n=30000, width=640, height=360))
+            assert_parity(dev, scenes.soup_scene(18, 4000, 512, 384, 12.0, scenes.PROGRAM_BLINN_PHONG), shard=(1, 3))
+            assert_parity(dev, scenes.soup_scene(17, 300, 512, 384, 150.0, scenes.PROGRAM_FLAT_COLOR))
+            assert_parity(dev, crowded_tile_scene())
+            assert dev.last_draw_stats()["tile_jobs"] >= 4  # (the crowded tile: ~8000 entries)
+            assert_parity(dev, scenes.cerberus_scene(640, 480))
+            for op, clear in ((scenes.OP_LEQUAL, 1.0), (scenes.OP_GREATER, 0.0)):
+                s = scenes.soup_scene(72, 6000, 200, 160, 14.0, scenes.PROGRAM_FLAT_COLOR)
+                s.depth_op, s.depth_clear = op, clear
+                assert_parity(dev, s)
+                s.depth_write = False  # last-wins keys over the loaded depth
+                assert_parity(dev, s)
+            assert dev.last_draw_stats()["overflowed_draws"] == 0
+        finally:
+            dev.close()
+    for k in ("ZR_TILE_NT", "ZR_REC_TABLE", "ZR_BIN_SLAB"):
+        monkeypatch.delenv(k, raising=False)
+    dev = rhi.RenderDevice(0)
+    try:
+        s = scenes.config_scene("c2")  # (645 entries per tile: 2-3 jobs each)
+        gc, gd = renderer.render_scene(dev, s, frames=4)
+        oc, od = oracle.render(s, nthreads=16)
+        assert np.array_equal(gc, oc) and np.array_equal(gd.view(np.uint32), od.view(np.uint32))
+        assert (dev.last_draw_stats()["tile_jobs"] > 0) == (jobs == "256")  # (longest C2 list: 741)
+    finally:
+        dev.close()
+    assert_partitioned_parity(scenes.soup_scene(70, 20000, 320, 240, 10.0, scenes.PROGRAM_BLINN_PHONG), 3)
+
+
 @pytest.mark.parametrize("cfg", ["c2x", "c3x"])
 def test_clustered_first_frame(cfg):
     """Gaussian-clustered 1M-triangle scenes (scenes.clustered_scene; c2x at 1080p,
@@ -258,11 +303,13 @@ def test_clustered_first_frame(cfg):
     ntiles = -(-s.width // 32) * -(-s.height // 32)
     dev = rhi.RenderDevice(0)
     try:
-        for frame in range(2):
+        for frame in range(3):
             gc, gd = renderer.render_scene(dev, s)
             st = dev.last_draw_stats()
             assert st["overflowed_draws"] == 0, (frame, st)
             assert st["bin_pool_runs"] > 0, (frame, st)
+            # (from the second frame its crowded tiles are split into tile jobs)
+            assert (st["tile_jobs"] > 0) == (frame > 0), (frame, st)
             assert np.array_equal(gc, oc), frame
             assert np.array_equal(gd.view(np.uint32), od.view(np.uint32)), frame
         assert st["bin_capacity"] <= 2 * st["bin_pairs"] + 512 * ntiles, st

@@ -108,6 +108,10 @@ struct alignas(8) BBox {
     uint32_t bb0, bb1;  // as TriRecord::bb0/bb1
 };
 constexpr uint32_t kMaxTilesPerPass = 16384;  // LDS histogram of the setup pass (64 KB)
+constexpr uint32_t kJobTileBits = 14;          // tile_order item: tile | part << kJobTileBits (tiles < kMaxTilesPerPass)
+constexpr uint32_t kJobTileMask = (1u << kJobTileBits) - 1u;
+constexpr uint32_t kJobNone = 0xFFFFFFFFu;     // tile_order item of a spare block (job grids)
+static_assert((1u << kJobTileBits) == kMaxTilesPerPass, "job items hold any tile index");
 constexpr uint32_t kMaxPushBytes = 128;       // ZR_MAX_PUSH_CONSTANTS_SIZE (Vulkan's guaranteed minimum)
 constexpr uint32_t kMaxPushWords = kMaxPushBytes / 4;
 
@@ -218,9 +222,12 @@ enum StatusWord : uint32_t {
                             // (entries, saturating): tiles x bin_slab_target + the pool entries its runs asked for
     kStPoolPairs = 9,       // pairs the last draw put in pool runs (saturating)
     kStPoolRuns = 10,       // pool runs of the last draw
+    kStJobsDenied = 11,     // draws whose tile jobs did not fit DrawParams::job_pad / job_slots (since the last sync)
+    kStJobs = 12,           // tile jobs of the last draw beyond one per tile
     kStSlabSlot0 = 16,      // [kSlabSlots]: the slab target (bin_slab_target) of the draw given slot i (DrawParams::stat_slot)
     kStPoolSlot0 = 64,      // [kSlabSlots]: the pool entries that draw's runs asked for (saturating)
-    kStWords = 112,
+    kStMaxSlot0 = 112,      // [kSlabSlots]: that draw's longest tile list
+    kStWords = 160,
 };
 // Device counters of k_setup_bin, read by the draw's k_tile (tile 0 reports them
 // and resets them, as every tile resets its count, so a draw needs no memset).
@@ -232,12 +239,15 @@ enum CounterWord : uint32_t {
     kCtMicro = 7,        // covered micro primitives of the draw (DrawParams::micro)
     kCtPoolTop = 8,      // u64 (words 8-9): pool entries the draw's runs asked for (the bump allocator; may pass pool_cap)
     kCtPoolRuns = 10,    // pool runs the draw registered
+    kCtJobsDenied = 11,  // 1: the draw's tile jobs did not fit (build_job_schedule)
+    kCtJobs = 12,        // tile jobs of the draw beyond one per tile
     kCtWords = 32,
 };
 // draw_info words (written by k_setup_bin for k_tile)
 enum DrawInfoWord : uint32_t {
     kInfoRecords = 0,     // setup records the overflow scan covers (bboxes[0, n))
     kInfoByPosition = 1,  // 1: bboxes are indexed by received position, records by gids[position] (records mode)
+    kInfoJobEntries = 2,  // entries per tile job of the draw (0: one job per tile; k_setup_bin build_job_schedule)
     kInfoWords = 4,
 };
 
@@ -344,6 +354,18 @@ struct DrawParams {
     uint32_t stat_slot;       // status slot for this draw's slab target (kStSlabSlot0 + i), or >= kSlabSlots: none
     uint2* runs;              // [ntiles * run_cap] (bins index, pairs)
     uint32_t* run_counts;     // [ntiles] (kRunCountMask etc.; zero between draws: k_tile resets it)
+    // Tile jobs: a list longer than job_entries is split into
+    // jobs of job_entries entries, each its own k_tile block (tile_order items
+    // t | part << kJobTileBits, built by k_setup_bin's last workgroup), which
+    // store their keys to job_keys[job_slot[t] + part]; the last job of the tile
+    // (job_tickets) folds them in with a min and resolves it.  job_entries 0: off.
+    // tile_order: [0, job_pad) parts 1.. (and spare kJobNone blocks), then the
+    // tiles (the schedule, or xcd_tile order when tile_sched is 0).
+    uint32_t job_entries, job_pad, job_slots;  // job_pad: k_tile blocks for parts 1.. (a multiple of 8)
+    uint32_t tile_sched;             // 1: tile_order[job_pad, + ntiles) holds the heaviest-first tile schedule
+    uint32_t* job_slot;              // [ntiles] first key buffer of a split tile (one per job)
+    unsigned long long* job_keys;    // [job_slots][kTilePixels] key buffers
+    uint32_t* job_tickets;           // [job_slots] per split tile, at its first buffer (zero between draws)
     // push-constant state at the draw (zr_cmd_push_constants): the bytes ride in
     // the launch's kernel arguments, as Vulkan push constants ride in user SGPRs
     // (last, so the fields above keep their kernarg offsets; fields added later
@@ -419,6 +441,13 @@ __host__ __device__ inline uint32_t bin_slab_target(uint64_t pairs, uint32_t nti
 inline uint64_t bin_default_capacity(uint64_t prims, uint32_t ntiles) {
     return std::max<uint64_t>(1ull << 20, 2 * prims + 256ull * ntiles);
 }
+
+// Tile jobs (DrawParams::job_entries): a shape whose longest list exceeded four
+// jobs of kTileJobEntries (two 1024-entry segments each) splits its long lists
+// -- one workgroup walking 30 segments of a crowded tile was the clustered c2x
+// scene's tile pass.
+constexpr uint32_t kTileJobEntries = 2048;
+inline bool use_tile_jobs(uint32_t max_tile) { return max_tile > 4u * kTileJobEntries; }
 
 inline uint32_t records_setup_wgs(uint64_t entries, uint32_t cus) {
     const uint64_t w = (entries + 2047u) / 2048u;

@@ -932,7 +932,7 @@ __device__ __forceinline__ uint32_t xcd_block(uint32_t t, uint32_t n) {
 // pass has ~2 tiles per wave slot at C2; without it its last ~15 us ran at 0.77
 // occupancy, docs/EXPERIMENTS.md).  Counting sort over kSchedBuckets weight
 // classes per XCD (s_sched: 8 x kSchedBuckets words of LDS).
-__device__ void build_tile_schedule(const DrawParams& P, uint32_t nt, uint32_t* s_sched) {
+__device__ void build_tile_schedule(const DrawParams& P, uint32_t nt, uint32_t* s_sched, uint32_t* order) {
     const uint32_t tid = threadIdx.x;
     for (uint32_t i = tid; i < 8u * kSchedBuckets; i += kSetupThreads) s_sched[i] = 0u;
     const uint32_t top = __hip_atomic_fetch_max(&P.counters[kCtMaxTile], 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
@@ -965,8 +965,71 @@ __device__ void build_tile_schedule(const DrawParams& P, uint32_t nt, uint32_t* 
         uint32_t x;
         const uint32_t k = key(t, x);
         const uint32_t l = atomicAdd(&s_sched[x * kSchedBuckets + k], 1u);  // rank of t within its XCD
-        P.tile_order[l * 8u + x] = t;  // block l * 8 + x runs on XCD x (a bijection on [0, nt))
+        order[l * 8u + x] = t;  // block l * 8 + x runs on XCD x (a bijection on [0, nt))
     }
+}
+
+// Tile jobs (DrawParams::job_entries), built by the same last workgroup.  A
+// tile whose list is longer than J (and takes no record scan) becomes
+// K = ceil(count / J) jobs, part p covering list entries [p J, (p + 1) J), with
+// K key buffers from job_slot[t].  Part 0 keeps the tile's block in the usual
+// order (blocks [job_pad, job_pad + nt)); parts 1.. take blocks of [0, job_pad)
+// spread like their tile (block b % 8 = the tile's XCD in that order, for L2
+// locality only); the blocks of [0, job_pad) left over get kJobNone.  When the
+// parts do not fit (an XCD's share of job_pad, or the key buffers) no tile is
+// split and the draw is counted (kCtJobsDenied) for the runtime to size them up.  k_tile derives K from the
+// same count and run word.
+__device__ uint32_t tile_jobs(uint32_t count, uint32_t run_word, uint32_t J) {
+    return (J && !(run_word & kRunDropped) && count > J) ? (count + J - 1u) / J : 1u;
+}
+
+__device__ void build_job_schedule(const DrawParams& P, uint32_t nt, uint32_t* s_buf) {
+    const uint32_t tid = threadIdx.x, J = P.job_entries, per_xcd = P.job_pad / 8u;
+    uint32_t* s_cnt = s_buf;       // [8] parts per XCD, then their cursors
+    uint32_t* s_tot = s_buf + 8;   // [0] key buffers (jobs of split tiles), [1] buffer cursor, [2] denied
+    if (tid < 16u) s_buf[tid] = 0u;
+    __syncthreads();
+    // pass 1: every tile's job count, parked in job_slot[t] (this thread reads it
+    // back in pass 2), and the parts each XCD gets
+    for (uint32_t t = tid; t < nt; t += kSetupThreads) {
+        const uint32_t c = __hip_atomic_load(&P.tile_counts[t], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        const uint32_t w = (c & kCountRuns) ? __hip_atomic_load(&P.run_counts[t], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) : 0u;
+        const uint32_t K = tile_jobs(c & ~kCountRuns, w, J);
+        P.job_slot[t] = K;
+        if (K > 1u) {
+            atomicAdd(&s_cnt[xcd_block(t, nt) & 7u], K - 1u);
+            atomicAdd(&s_tot[0], K);
+        }
+    }
+    __syncthreads();
+    if (tid == 0) {
+        bool ok = s_tot[0] <= P.job_slots;
+        for (uint32_t x = 0; x < 8u; ++x) ok = ok && s_cnt[x] <= per_xcd;
+        s_tot[2] = ok ? 0u : 1u;
+        P.draw_info[kInfoJobEntries] = ok ? J : 0u;
+        if (!ok) atomicAdd(&P.counters[kCtJobsDenied], 1u);
+    }
+    __syncthreads();
+    const bool ok = s_tot[2] == 0u;
+    if (tid < 8u) {
+        const uint32_t extra = ok ? s_cnt[tid] : 0u;
+        s_cnt[16 + tid] = extra;  // (parts per XCD; s_cnt[0, 8) become the cursors)
+        s_cnt[tid] = 0u;
+        if (extra) atomicAdd(&P.counters[kCtJobs], extra);
+    }
+    __syncthreads();
+    // pass 2: key slots and part items (same thread -> tile mapping as pass 1)
+    for (uint32_t t = tid; ok && t < nt; t += kSetupThreads) {
+        const uint32_t K = P.job_slot[t];
+        if (K <= 1u) continue;
+        const uint32_t x = xcd_block(t, nt) & 7u;
+        P.job_slot[t] = atomicAdd(&s_tot[1], K);  // (K key buffers, one per job)
+        const uint32_t l0 = atomicAdd(&s_cnt[x], K - 1u);
+        for (uint32_t p = 1; p < K; ++p) P.tile_order[(l0 + p - 1u) * 8u + x] = t | (p << kJobTileBits);
+    }
+    for (uint32_t i = tid; i < P.job_pad; i += kSetupThreads)  // the spare part blocks
+        if ((i >> 3) >= s_cnt[16 + (i & 7u)]) P.tile_order[i] = kJobNone;
+    __syncthreads();  // (s_buf is build_tile_schedule's next)
 }
 
 // ----------------------------------------------------------- k_setup_bin
@@ -1115,6 +1178,7 @@ __global__ __launch_bounds__(kSetupThreads) void k_setup_bin(DrawParams P) {
     if (w == 0 && tid == 0) {
         P.draw_info[kInfoRecords] = MESH ? kMeshFans * n_pos : n_pos;
         P.draw_info[kInfoByPosition] = rec_mode ? 1u : 0u;
+        P.draw_info[kInfoJobEntries] = 0u;  // (build_job_schedule sets it, after this store: the ticket orders them)
     }
 
     // ---- phase 1
@@ -1215,7 +1279,7 @@ __global__ __launch_bounds__(kSetupThreads) void k_setup_bin(DrawParams P) {
             pool_commit(P, s_hist, s_misc + 8, rot);
             __syncthreads();
         }
-        if (P.tile_order) {
+        if (P.tile_order) {  // (the tile schedule and / or tile jobs)
             // The last workgroup to take a ticket sees every tile's final count: the
             // counts and the max are only ever changed by atomics, which execute at
             // the memory side, and every one of this workgroup's has completed before
@@ -1227,7 +1291,10 @@ __global__ __launch_bounds__(kSetupThreads) void k_setup_bin(DrawParams P) {
                 s_misc[5] = __hip_atomic_fetch_add(&P.counters[kCtSchedTicket], 1u, __ATOMIC_RELAXED,
                                                    __HIP_MEMORY_SCOPE_AGENT);
             __syncthreads();
-            if (s_misc[5] == G - 1u) build_tile_schedule(P, nt, s_sched);
+            if (s_misc[5] == G - 1u) {
+                if (P.job_entries) build_job_schedule(P, nt, s_sched);
+                if (P.tile_sched) build_tile_schedule(P, nt, s_sched, P.tile_order + (P.job_entries ? P.job_pad : 0u));
+            }
         }
     }
     ZR_STAMP(2);
@@ -2262,8 +2329,12 @@ __global__ __launch_bounds__(NT, kTileWgs * kTileThreads / 256) void k_tile(Draw
     uint32_t& s_bclaim = s_misc[2];
     uint32_t* s_dbg = s_misc + 3;    // [2] kDebugStamps: lane-walk steps of the chunks, wave-path sweeps
     uint32_t* s_nwin = s_misc + 5;   // resolve: distinct winners of the tile
-    const uint32_t b = (tile_debug(P) & kDebugReverseTiles) ? P.ntiles - 1u - blockIdx.x : blockIdx.x;
-    const uint32_t t = P.tile_order ? P.tile_order[b] : xcd_tile(b, P.ntiles);
+    const uint32_t b = (tile_debug(P) & kDebugReverseTiles) ? gridDim.x - 1u - blockIdx.x : blockIdx.x;
+    // a tile_order item: tile | job part << kJobTileBits, or a job grid's spare block
+    const uint32_t jp = P.job_entries ? P.job_pad : 0u;  // (tile jobs: part blocks first)
+    const uint32_t item = (b < jp || P.tile_sched) ? P.tile_order[b] : xcd_tile(b - jp, P.ntiles);
+    if (item == kJobNone) return;
+    const uint32_t t = item & kJobTileMask, part = item >> kJobTileBits;
     uint32_t tx, ty;
     shard_tile_xy(shard_geom(P), t, tx, ty);
     const int x0 = (int)tx * kTile, y0 = (int)ty * kTile;
@@ -2347,7 +2418,7 @@ __global__ __launch_bounds__(NT, kTileWgs * kTileThreads / 256) void k_tile(Draw
             ent[k] = i < n ? s_sorted[i] : 0u;
         }
     };
-    if (!(tile_debug(P) & kDebugSkipRaster)) load_segment(0, min(kSortCap, slab));
+    if (!(tile_debug(P) & kDebugSkipRaster) && part == 0) load_segment(0, min(kSortCap, slab));
     const uint32_t count_v = P.tile_counts[t];
     const uint32_t count = count_v & ~kCountRuns;
     // The list: the slab's first slab_len entries, then the tile's pool runs
@@ -2368,12 +2439,12 @@ __global__ __launch_bounds__(NT, kTileWgs * kTileThreads / 256) void k_tile(Draw
     if (tab)
         for (uint32_t i = threadIdx.x; i < kRecHashSlots; i += NT) s_thash[i] = 0u;
     if (threadIdx.x < 2) s_dbg[threadIdx.x] = 0u;
-    // The first block dispatched reports the draw's setup and binning stats
+    // The first tile block dispatched reports the draw's setup and binning stats
     // (k_setup_bin's counters, complete before this launch) to the runtime's status
     // words: plain stores, no read of host memory unless a run was dropped
     // (volatile accesses wait for each one to cross the bus).  Draws run in stream
     // order; the host reads the words after a stream sync.
-    if (blockIdx.x == 0 && threadIdx.x == 0) {
+    if (blockIdx.x == jp && threadIdx.x == 0) {  // (jp: the first tile block; part blocks before it may be spare)
         uint32_t* st = P.status;
         const unsigned long long pairs = *reinterpret_cast<const unsigned long long*>(&P.counters[kCtPairs]);
         const unsigned long long pool = *reinterpret_cast<const unsigned long long*>(&P.counters[kCtPoolTop]);
@@ -2383,6 +2454,11 @@ __global__ __launch_bounds__(NT, kTileWgs * kTileThreads / 256) void k_tile(Draw
         st[kStTotalPairs] = pairs > 0xFFFFFFFFull ? 0xFFFFFFFFu : (uint32_t)pairs;
         st[kStPoolPairs] = pool > 0xFFFFFFFFull ? 0xFFFFFFFFu : (uint32_t)pool;
         st[kStPoolRuns] = P.counters[kCtPoolRuns];
+        st[kStJobs] = P.counters[kCtJobs];
+        if (P.counters[kCtJobsDenied]) {
+            const uint32_t jd = st[kStJobsDenied];
+            st[kStJobsDenied] = jd + 1u;
+        }
         const uint32_t target = bin_slab_target(pairs, P.ntiles);
         if (pool > P.pool_cap) {  // a dropped run: the buffer this draw asks for (read-modify-write only here)
             const unsigned long long need = (unsigned long long)P.ntiles * target + pool;
@@ -2394,26 +2470,33 @@ __global__ __launch_bounds__(NT, kTileWgs * kTileThreads / 256) void k_tile(Draw
         if (P.stat_slot < kSlabSlots) {  // (the runtime derives the buffer the draw asks for from these)
             st[kStSlabSlot0 + P.stat_slot] = target;
             st[kStPoolSlot0 + P.stat_slot] = pool > 0xFFFFFFFFull ? 0xFFFFFFFFu : (uint32_t)pool;
+            st[kStMaxSlot0 + P.stat_slot] = P.counters[kCtMaxTile];
         }
     }
     __syncthreads();
     const bool has_runs = (__builtin_amdgcn_readfirstlane((int)count_v) & (int)kCountRuns) != 0;
     const uint32_t rcw = has_runs ? (uint32_t)__builtin_amdgcn_readfirstlane((int)P.run_counts[t]) : 0u;
     const bool spill = (rcw & kRunDropped) != 0u;
-    const uint32_t cnt = spill ? 0u : count;
+    // this block's part of the list: all of it, or job `part` of K (build_job_schedule)
+    const uint32_t J = P.job_entries ? (uint32_t)__builtin_amdgcn_readfirstlane((int)P.draw_info[kInfoJobEntries]) : 0u;
+    const uint32_t K = tile_jobs(count, rcw, J);
+    const uint32_t seg_lo = K > 1u ? part * J : 0u;
+    const uint32_t cnt = spill ? 0u : K > 1u ? min(count, seg_lo + J) : count;
     // (the segment loop reads slab_len and the run count back from LDS, each wave
     // its own leader's copy: held in registers across the pass they cost the C2
-    // instance VGPR spills)
+    // instance VGPR spills; likewise the job count and key slot after it)
     if ((threadIdx.x & 63u) == 0) {
         s_misc[8] = (rcw & kRunFill) ? (rcw & ~(kRunFill | kRunDropped)) >> kRunFillShift : min(count, slab);
         s_misc[9] = min(rcw & kRunCountMask, P.run_cap);
+        s_misc[10] = K;
+        s_misc[11] = K > 1u ? P.job_slot[t] : 0u;
     }
     // k_setup_bin's counters back to zero for the next draw on this scratch set:
     // each tile its own count (every wave has read it: the barrier above) and, at
     // the end of the tile, its run word (read after that barrier), block 0 the draw
     // counters
-    if (threadIdx.x == 0) P.tile_counts[t] = 0u;
-    if (blockIdx.x == 0)
+    if (threadIdx.x == 0 && K == 1u) P.tile_counts[t] = 0u;  // (a split tile: its resolving job)
+    if (blockIdx.x == jp)
         for (uint32_t i = threadIdx.x; i < kCtWords; i += NT) P.counters[i] = 0u;
 
     const uint32_t wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
@@ -2425,7 +2508,7 @@ __global__ __launch_bounds__(NT, kTileWgs * kTileThreads / 256) void k_tile(Draw
         // so that a 64-lane chunk holds primitives of similar cost (the lane loop runs
         // as long as its largest member).  Then each wave takes every 4th chunk: one
         // lane per entry loads the 64-B record, and the wave walks the chunk.
-        for (uint32_t seg = 0; seg < cnt; seg += kSortCap) {
+        for (uint32_t seg = seg_lo; seg < cnt; seg += kSortCap) {
             const uint32_t n = min(kSortCap, cnt - seg);
             // a list with pool runs loads its segments past the slab part through
             // the run table (s_misc[9]: runs, s_misc[8]: the slab part's length)
@@ -2657,6 +2740,41 @@ __global__ __launch_bounds__(NT, kTileWgs * kTileThreads / 256) void k_tile(Draw
         }
     }
     __syncthreads();
+    // A split tile (tile jobs): every job stores its keys to a buffer of its own
+    // (job_keys[job_slot[t] + part]) and takes a ticket; the last job to arrive
+    // folds the others' keys into its own with a min (every job started from the
+    // same initial keys) and resolves the tile, the others end here.  (Plain
+    // system-coherent stores and loads: merging with 64-bit atomic mins at device
+    // scope ran c2x's tile pass at 281 us with jobs of 2048 entries, 639 with 512;
+    // their blocks are not reliably on one XCD, so L2-local atomics lost keys.)
+    if ((uint32_t)__builtin_amdgcn_readfirstlane((int)s_misc[10]) > 1u) {
+        const uint32_t Kj = (uint32_t)__builtin_amdgcn_readfirstlane((int)s_misc[10]);
+        const uint32_t buf0 = (uint32_t)__builtin_amdgcn_readfirstlane((int)s_misc[11]);
+        unsigned long long* mine = P.job_keys + (size_t)(buf0 + part) * kTilePixels;
+        int i0 = threadIdx.x;  // (opaque: the key addresses of the init loop, held across the pass, spilled)
+        asm volatile("" : "+v"(i0));
+        for (int i = i0; i < kTilePixels; i += NT)
+            __hip_atomic_store(&mine[i], s_key[i], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // (each thread's stores done before the ticket)
+        __syncthreads();
+        if (threadIdx.x == 0)
+            s_misc[12] = __hip_atomic_fetch_add(&P.job_tickets[buf0], 1u, __ATOMIC_ACQ_REL, __HIP_MEMORY_SCOPE_AGENT);
+        __syncthreads();
+        if ((uint32_t)__builtin_amdgcn_readfirstlane((int)s_misc[12]) != Kj - 1u) return;
+        for (uint32_t j = 0; j < Kj; ++j) {
+            if (j == part) continue;
+            const unsigned long long* other = P.job_keys + (size_t)(buf0 + j) * kTilePixels;
+            for (int i = i0; i < kTilePixels; i += NT) {
+                const unsigned long long k = __hip_atomic_load(&other[i], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                if (k < s_key[i]) s_key[i] = k;
+            }
+        }
+        if (threadIdx.x == 0) {
+            __hip_atomic_store(&P.job_tickets[buf0], 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            P.tile_counts[t] = 0u;  // (every job of the tile read it before its ticket)
+        }
+        __syncthreads();
+    }
     if (stamp) ts[3] = __builtin_amdgcn_s_memrealtime();
 
     // Resolve (the index width is a template parameter so a winner's record and
@@ -2739,10 +2857,11 @@ void launch_setup_bin(const DrawParams& p, void* stream) {
 
 template <int PROG, int MODE, int NT>
 static void launch_tile_pmt(const DrawParams& p, hipStream_t s, bool initd) {
+    const uint32_t blocks = p.ntiles + (p.job_entries ? p.job_pad : 0u);  // (tile jobs: part blocks first)
     if (initd)
-        hipLaunchKernelGGL((k_tile<PROG, MODE, true, NT>), dim3(p.ntiles), dim3(NT), 0, s, p);
+        hipLaunchKernelGGL((k_tile<PROG, MODE, true, NT>), dim3(blocks), dim3(NT), 0, s, p);
     else
-        hipLaunchKernelGGL((k_tile<PROG, MODE, false, NT>), dim3(p.ntiles), dim3(NT), 0, s, p);
+        hipLaunchKernelGGL((k_tile<PROG, MODE, false, NT>), dim3(blocks), dim3(NT), 0, s, p);
 }
 
 template <int PROG, int MODE>

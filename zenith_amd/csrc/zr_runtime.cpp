@@ -214,6 +214,12 @@ struct ScratchSet {
     uint32_t* run_counts = nullptr;  // [ntiles] (zero between draws: k_tile resets it)
     uint64_t run_counts_cap = 0;
     uint32_t* tile_order = nullptr;  // k_tile's block -> tile schedule (k_setup_bin's last workgroup writes it)
+    uint32_t* job_slot = nullptr;    // tile jobs (DrawParams::job_entries): key slot per split tile
+    uint64_t job_slot_cap = 0;
+    unsigned long long* job_keys = nullptr;  // [slots][kTilePixels] per-job key buffers
+    uint64_t job_keys_cap = 0;
+    uint32_t* job_tickets = nullptr;  // [slots], zero between draws
+    uint64_t job_tickets_cap = 0;
     uint64_t tile_order_cap = 0;
     uint8_t* xsend = nullptr;   // partitioned setup: exchange blocks (bytes)
     uint64_t xsend_cap = 0;
@@ -276,9 +282,12 @@ struct zr_device_t {
     // slab targets (bin_slab_target) measured per draw shape, (tiles << 32) | primitives;
     // the draws since the last sync, in status-slot order (DrawParams::stat_slot)
     struct BinShape {
-        uint32_t target = 0;  // bin_slab_target
-        uint32_t pool = 0;    // pool entries its runs asked for (at the slab it had)
+        uint32_t target = 0;    // bin_slab_target
+        uint32_t pool = 0;      // pool entries its runs asked for (at the slab it had)
+        uint32_t max_tile = 0;  // its longest tile list
     };
+    int jobs = -1;              // ZR_JOBS: tile jobs of N entries (tests), 0 off; -1: use_tile_jobs
+    uint32_t job_boost = 1;     // job_pad multiplier, doubled after a draw whose jobs did not fit
     std::unordered_map<uint64_t, BinShape> bin_shapes;
     std::vector<uint64_t> slab_keys;
     uint32_t forced_slab = ~0u; // ZR_BIN_SLAB: every draw's slab (tests: pool runs everywhere)
@@ -493,6 +502,11 @@ zr_result device_sync(zr_device* d) {
     d->last.micro_fragments = st[kStMicro];
     d->last.bin_pool_pairs = st[kStPoolPairs];
     d->last.bin_pool_runs = st[kStPoolRuns];
+    d->last.tile_jobs = st[kStJobs];
+    if (st[kStJobsDenied]) {
+        d->job_boost = std::min<uint32_t>(d->job_boost * 2u, 1u << 12);
+        st[kStJobsDenied] = 0;
+    }
     // partitioned draws since the previous sync point
     if (st[kStRouteMax]) {  // kept from the last interval with partitioned draws
         d->last.route_max_entries = st[kStRouteMax];
@@ -514,16 +528,19 @@ zr_result device_sync(zr_device* d) {
     uint64_t need = st[kStBinNeed];  // (draws with a dropped run; the others from their slots)
     st[kStBinNeed] = 0;
     for (size_t i = 0; i < d->slab_keys.size(); ++i) {
-        const uint32_t target = st[kStSlabSlot0 + i], pool = st[kStPoolSlot0 + i];
+        const uint32_t target = st[kStSlabSlot0 + i], pool = st[kStPoolSlot0 + i], max_tile = st[kStMaxSlot0 + i];
         if (!target) continue;
         need = std::max<uint64_t>(need, (d->slab_keys[i] >> 32) * target + pool);
         st[kStSlabSlot0 + i] = 0;
         st[kStPoolSlot0 + i] = 0;
+        st[kStMaxSlot0 + i] = 0;
         if (d->bin_shapes.size() >= 1024) d->bin_shapes.clear();  // (shapes that come and go)
         zr_device_t::BinShape& v = d->bin_shapes[d->slab_keys[i]];
         if (v.target != target || v.pool != pool) d->scratch_gen++;  // recorded graphs bake the slab in
+        if (use_tile_jobs(v.max_tile) != use_tile_jobs(max_tile)) d->scratch_gen++;
         v.target = target;
         v.pool = pool;
+        v.max_tile = max_tile;
     }
     d->slab_keys.clear();
     if (st[kStOverflow]) {
@@ -729,6 +746,35 @@ zr_result ensure_scratch(zr_device* d, ScratchSet& S, DrawParams& P) {
     P.slab = (uint32_t)slab;
     P.pool_off = (uint32_t)(slab * P.ntiles);
     P.pool_cap = (uint32_t)(S.bins_cap - slab * P.ntiles);
+    // Tile jobs (DrawParams::job_entries): for a shape whose longest list was long
+    // (use_tile_jobs), or forced (ZR_JOBS).  The grid's spare blocks bound the jobs
+    // beyond one per tile by the shape's pairs / J (pairs < tiles x target).
+    P.job_entries = 0;
+    P.job_pad = P.job_slots = 0;
+    if (!(d->debug & kDebugPhase1Only)) {
+        const bool known = shape != d->bin_shapes.end();
+        if (d->jobs > 0)
+            P.job_entries = (uint32_t)d->jobs;
+        else if (d->jobs < 0 && known && use_tile_jobs(shape->second.max_tile))
+            P.job_entries = kTileJobEntries;
+    }
+    if (P.job_entries) {
+        const uint64_t pairs = shape != d->bin_shapes.end()
+                                   ? (uint64_t)P.ntiles * shape->second.target + shape->second.pool
+                                   : std::max<uint64_t>((uint64_t)P.prims * 4u, (uint64_t)P.ntiles * P.job_entries);
+        // (parts go to their tile's XCD: room for twice an even share on each)
+        const uint64_t cap = std::min<uint64_t>((pairs / P.job_entries + 64) * 2 * d->job_boost, 1u << 20);
+        P.job_pad = (uint32_t)((cap + 7) / 8 * 8);
+        P.job_slots = P.job_pad + std::min<uint32_t>(P.job_pad, P.ntiles);  // (key buffers: parts + the split tiles' part 0)
+        const uint64_t tc = S.job_tickets_cap;
+        if ((rc = grow(d, S.job_slot, S.job_slot_cap, P.ntiles, 4))) return rc;
+        if ((rc = grow(d, S.job_keys, S.job_keys_cap, (uint64_t)P.job_slots * kTilePixels, 8))) return rc;
+        if ((rc = grow(d, S.job_tickets, S.job_tickets_cap, P.job_slots, 4))) return rc;
+        if (S.job_tickets_cap != tc) ZR_HIP(hipMemset(S.job_tickets, 0, S.job_tickets_cap * 4));
+        P.job_slot = S.job_slot;
+        P.job_keys = S.job_keys;
+        P.job_tickets = S.job_tickets;
+    }
     P.stat_slot = ~0u;
     if (!d->capturing && d->slab_keys.size() < kSlabSlots) {
         P.stat_slot = (uint32_t)d->slab_keys.size();
@@ -993,8 +1039,9 @@ zr_result exec_draw(zr_device* d, ExecState& s, const Cmd& c, bool indexed) {
     // (a phase-1-only timing run never reaches the last workgroup's ticket, so it
     // writes no schedule: k_tile then keeps xcd_tile order instead of reading an
     // unwritten one)
-    if (sched && !(d->debug & kDebugPhase1Only)) {
-        if ((rc = grow(d, S.tile_order, S.tile_order_cap, P.ntiles, 4))) return rc;
+    P.tile_sched = sched && !(d->debug & kDebugPhase1Only) ? 1u : 0u;
+    if ((sched || P.job_entries) && !(d->debug & kDebugPhase1Only)) {
+        if ((rc = grow(d, S.tile_order, S.tile_order_cap, (uint64_t)P.ntiles + P.job_pad, 4))) return rc;
         P.tile_order = S.tile_order;
     }
     d->last_prims = prims;
@@ -1227,6 +1274,7 @@ ZR_API zr_result zr_device_create(int32_t hip_device, zr_device** out) {
     if (const char* rw = getenv("ZR_REC_WGS")) d->rec_wgs = (uint32_t)strtoul(rw, nullptr, 0);
     if (const char* bs = getenv("ZR_BIN_STAGE")) d->bin_stage = atoi(bs);
     if (const char* mi = getenv("ZR_MICRO")) d->micro = atoi(mi) != 0 ? 1 : 0;
+    if (const char* jb = getenv("ZR_JOBS")) d->jobs = atoi(jb) > 0 ? std::max(atoi(jb), 256) : 0;
     if (const char* nt = getenv("ZR_TILE_NT")) {
         const unsigned long v = strtoul(nt, nullptr, 0);
         d->tile_threads = v >= 512 ? 512u : v ? 256u : 0u;
@@ -1264,7 +1312,7 @@ ZR_API void zr_device_destroy(zr_device* d) {
     if (d->dbg_ts) (void)hipFree(d->dbg_ts);
     if (d->win_bits) (void)hipFree(d->win_bits);
     for (ScratchSet& S : d->sets) {
-        for (void* p : {(void*)S.runs, (void*)S.run_counts, (void*)S.records, (void*)S.records_big, (void*)S.mesh_edges, (void*)S.bboxes, (void*)S.tile_counts,
+        for (void* p : {(void*)S.job_slot, (void*)S.job_keys, (void*)S.job_tickets, (void*)S.runs, (void*)S.run_counts, (void*)S.records, (void*)S.records_big, (void*)S.mesh_edges, (void*)S.bboxes, (void*)S.tile_counts,
                         (void*)S.draw_info, (void*)S.counters, (void*)S.bins, (void*)S.xsend, (void*)S.xrecv,
                         (void*)S.gids, (void*)S.tile_order})
             if (p) (void)hipFree(p);

@@ -86,7 +86,8 @@ class zr_draw_stats(C.Structure):
                 ("triangles_dropped_clip", C.c_uint64), ("bin_pairs", C.c_uint64),
                 ("bin_capacity", C.c_uint64), ("overflowed_draws", C.c_uint64),
                 ("route_max_entries", C.c_uint64), ("route_fallback_draws", C.c_uint64), ("winners", C.c_uint64),
-                ("micro_fragments", C.c_uint64), ("bin_pool_pairs", C.c_uint64), ("bin_pool_runs", C.c_uint64)]
+                ("micro_fragments", C.c_uint64), ("bin_pool_pairs", C.c_uint64), ("bin_pool_runs", C.c_uint64),
+                ("tile_jobs", C.c_uint64)]
 
 
 class zr_buffer_desc(C.Structure):
