@@ -727,8 +727,8 @@ zr_result ensure_scratch(zr_device* d, ScratchSet& S, DrawParams& P) {
     P.run_counts = S.run_counts;
     // tile t's slab is bins[t * slab, (t + 1) * slab), the pool the rest.  Before
     // any measurement of the draw's shape: slabs of a third of the buffer.  After:
-    // the buffer less the pool the shape's runs asked for (+10 %, and at least an
-    // eighth of the buffer) over the tiles, but no less than the shape's target --
+    // the buffer less the pool the shape's runs asked for (+25 %, and at least a
+    // 64th of the buffer) over the tiles, but no less than the shape's target --
     // a buffer larger than the pairs need (the 2^20-entry floor; C2's 2 x prims)
     // goes to the slabs, where no run is needed (cerberus: the target slab put its
     // crowded tiles' excess in runs, setup +8 us).
@@ -739,7 +739,7 @@ zr_result ensure_scratch(zr_device* d, ScratchSet& S, DrawParams& P) {
     if (d->forced_slab != ~0u) {
         slab = d->forced_slab;
     } else if (shape != d->bin_shapes.end()) {
-        const uint64_t pool = std::max<uint64_t>((uint64_t)shape->second.pool * 11 / 10 + 4096, cap / 8);
+        const uint64_t pool = std::max<uint64_t>((uint64_t)shape->second.pool * 5 / 4 + 4096, cap / 64);
         slab = std::max<uint64_t>(shape->second.target, cap > pool ? (cap - pool) / nt : 0);
     }
     slab = std::min<uint64_t>({slab, cap / nt, (uint64_t)kMaxSlab});
