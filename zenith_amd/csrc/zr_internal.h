@@ -91,9 +91,9 @@ constexpr uint32_t kBinPrimMask = (1u << kBinPrimBits) - 1u;
 // (phase 4 stores only below 2^31; bin buffers stay under 2^30 entries) and the
 // tile takes k_tile's record scan.
 constexpr uint32_t kDropCursor = 0xC0000000u;
-// run_counts[t] (DrawParams::runs): pool runs of tile t in bits [0, 9), the slab
-// fill in bits [9, 30) with kRunFill when a run straddled the slab end, kRunDropped
-// when a run was dropped.  Slabs are capped at kMaxSlab entries so the fill fits.
+// run_counts[t] (DrawParams::runs): the slab fill in bits [9, 30) with kRunFill
+// when a run straddled the slab end, kRunDropped when a run was dropped (bits
+// [0, 9) unused).  Slabs are capped at kMaxSlab entries so the fill fits.
 constexpr uint32_t kRunCountMask = 0x1FFu;
 constexpr uint32_t kRunFillShift = 9;
 constexpr uint32_t kMaxSlab = (1u << 21) - 1u;
@@ -345,15 +345,15 @@ struct DrawParams {
     // Overflow runs: a workgroup whose run of pairs for tile t does
     // not fit what is left of t's slab stores it in the pool instead,
     // bins[pool_off + base, + its pairs) from a bump allocator (kCtPoolTop), and
-    // registers (pool_off + base, pairs) in runs[t * run_cap + d], d from
-    // run_counts[t] (one run per setup workgroup and tile).  The run that
+    // registers (pool_off + base, pairs) in runs[t * run_cap + w], w its
+    // workgroup index (slots of other workgroups hold length 0).  The run that
     // straddles the slab end records its offset, the slab's fill (kRunFill); a run
     // the pool cannot hold is dropped (kRunDropped) and k_tile takes that tile by
     // its record scan.
     uint32_t pool_off, pool_cap, run_cap;
     uint32_t stat_slot;       // status slot for this draw's slab target (kStSlabSlot0 + i), or >= kSlabSlots: none
-    uint2* runs;              // [ntiles * run_cap] (bins index, pairs)
-    uint32_t* run_counts;     // [ntiles] (kRunCountMask etc.; zero between draws: k_tile resets it)
+    uint2* runs;              // [ntiles * run_cap] (bins index, pairs), zero between draws (k_tile clears a used table)
+    uint32_t* run_counts;     // [ntiles] run word (kRunFill, kRunDropped; zero between draws: k_tile resets it)
     // Tile jobs: a list longer than job_entries is split into
     // jobs of job_entries entries, each its own k_tile block (tile_order items
     // t | part << kJobTileBits, built by k_setup_bin's last workgroup), which
@@ -432,6 +432,15 @@ __host__ __device__ inline uint32_t bin_slab_target(uint64_t pairs, uint32_t nti
     const float mean = (float)pairs / (float)ntiles;
     const float t = mean + 3.0f * sqrtf(mean) + 64.0f;
     return t >= (float)kMaxSlab ? kMaxSlab : (uint32_t)t;
+}
+
+// A slab of the longest list when that costs at most twice the target plus 1024
+// entries per tile (the bin memory bound; 0 otherwise): a mildly
+// skewed draw then keeps every list whole, no pool runs.  cerberus' ~80 runs a
+// frame on its few crowded tiles -- the pass's critical path -- cost its tile
+// pass ~1.8 us.
+inline uint32_t bin_slab_whole(uint32_t target, uint32_t max_tile) {
+    return (uint64_t)max_tile <= 2ull * target + 1024u ? max_tile : 0u;
 }
 
 // The bin buffer (entries) of a scratch set's first draw, before any draw has

@@ -1064,32 +1064,34 @@ __device__ void build_job_schedule(const DrawParams& P, uint32_t nt, uint32_t* s
 
 // Phase 2's overflow run (DrawParams::runs): this workgroup's c pairs for tile t,
 // reserved at offset o (ov: the count the atomic returned) of the tile's list, do not fit the rest of its slab; they
-// go to the pool.  The run takes a slot in t's run table and an offset inside the
-// workgroup's pool allocation (an LDS counter, s_pool[0]); the allocation itself
-// is one atomic per workgroup after the tile loop (pool_commit), which turns the
-// returned kPoolPending | slot into the run's bin position.  (One pool atomic per
-// run: the clustered c2x scene's ~31k runs queued on that address, setup
-// 772 us.)  Returns kDropCursor when t's run table is full.
+// go to the pool.  The run takes slot w (this workgroup) of t's run table and an
+// offset inside the workgroup's pool allocation (an LDS counter, s_pool[0]); the
+// allocation itself is one atomic per workgroup after the tile loop
+// (pool_commit), which turns the returned kPoolPending | offset into the run's
+// bin position.  No returning global atomic per run: one per run on the pool
+// counter queued the clustered c2x scene's ~31k runs on that address (setup
+// 772 us), and a slot counter per tile cost cerberus' ~100 runs ~4 us of setup.
+// Returns kDropCursor for a workgroup beyond the run table (run_cap).
 constexpr uint32_t kPoolPending = 0x40000000u;
-__device__ __noinline__ uint32_t pool_run(const DrawParams& P, uint32_t t, uint32_t ov, uint32_t c, uint32_t* s_pool) {
-    uint32_t* rc = &P.run_counts[t];
+__device__ __noinline__ uint32_t pool_run(const DrawParams& P, uint32_t t, uint32_t ov, uint32_t c, uint32_t* s_pool,
+                                          uint32_t w) {
     if (!(ov & kCountRuns)) atomicOr(&P.tile_counts[t], kCountRuns);  // (the first run of the tile, as far as this workgroup saw)
     const uint32_t o = ov & ~kCountRuns;
-    if (o < P.slab) atomicOr(rc, kRunFill | (o << kRunFillShift));  // the slab holds [0, o) of the list
-    const uint32_t d = atomicAdd(rc, 1u) & kRunCountMask;
-    if (d >= P.run_cap) {
-        atomicOr(rc, kRunDropped);
+    if (o < P.slab) atomicOr(&P.run_counts[t], kRunFill | (o << kRunFillShift));  // the slab holds [0, o) of the list
+    if (w >= P.run_cap) {
+        atomicOr(&P.run_counts[t], kRunDropped);
         return kDropCursor;
     }
-    P.runs[(size_t)t * P.run_cap + d] = make_uint2(atomicAdd(&s_pool[0], c), c);
+    P.runs[(size_t)t * P.run_cap + w].y = c;  // (the position once the workgroup's allocation is known)
     atomicAdd(&s_pool[1], 1u);
-    return kPoolPending | d;
+    return kPoolPending | atomicAdd(&s_pool[0], c);
 }
 
 // After phase 2's tile loop (same thread -> tile mapping): the workgroup's pool
 // runs take one allocation of s_pool[0] entries; each pending cursor becomes its
 // run's position, or kDropCursor (and the tile's kRunDropped) when the pool is full.
-__device__ __noinline__ void pool_commit(const DrawParams& P, uint32_t* s_hist, uint32_t* s_pool, uint32_t rot) {
+__device__ __noinline__ void pool_commit(const DrawParams& P, uint32_t* s_hist, uint32_t* s_pool, uint32_t rot,
+                                         uint32_t w) {
     const uint32_t nt = P.ntiles, tid = threadIdx.x;
     if (tid == 0) {
         const unsigned long long base =
@@ -1103,10 +1105,9 @@ __device__ __noinline__ void pool_commit(const DrawParams& P, uint32_t* s_hist, 
         const uint32_t t = i + rot < nt ? i + rot : i + rot - nt;
         const uint32_t v = s_hist[t];
         if ((v >> 30) != 1u) continue;  // not pending
-        uint2* e = &P.runs[(size_t)t * P.run_cap + (v & kRunCountMask)];
         if (pb != kDropCursor) {
-            const uint32_t x = pb + e->x;
-            e->x = x;
+            const uint32_t x = pb + (v & ~kPoolPending);
+            P.runs[(size_t)t * P.run_cap + w].x = x;
             s_hist[t] = x;
         } else {
             atomicOr(&P.run_counts[t], kRunDropped);
@@ -1253,7 +1254,7 @@ __global__ __launch_bounds__(kSetupThreads) void k_setup_bin(DrawParams P) {
             const uint32_t c = s_hist[t];
             const uint32_t ov = c ? __hip_atomic_fetch_add(&P.tile_counts[t], c, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) : 0u;
             const uint32_t o = ov & ~kCountRuns;
-            s_hist[t] = o + c <= P.slab ? t * P.slab + o : pool_run(P, t, ov, c, s_misc + 8);
+            s_hist[t] = o + c <= P.slab ? t * P.slab + o : pool_run(P, t, ov, c, s_misc + 8, w);
             if (P.bin_stage) s_lcur[t] = c;
             top = max(top, o + c);
             sum += c;
@@ -1276,7 +1277,7 @@ __global__ __launch_bounds__(kSetupThreads) void k_setup_bin(DrawParams P) {
             if (s_misc[3]) atomicAdd(reinterpret_cast<unsigned long long*>(&P.counters[kCtPairs]), (unsigned long long)s_misc[3]);
         }
         if (s_misc[8]) {  // (the barrier above: every pool_run of this workgroup is done)
-            pool_commit(P, s_hist, s_misc + 8, rot);
+            pool_commit(P, s_hist, s_misc + 8, rot, w);
             __syncthreads();
         }
         if (P.tile_order) {  // (the tile schedule and / or tile jobs)
@@ -2487,7 +2488,7 @@ __global__ __launch_bounds__(NT, kTileWgs * kTileThreads / 256) void k_tile(Draw
     // instance VGPR spills; likewise the job count and key slot after it)
     if ((threadIdx.x & 63u) == 0) {
         s_misc[8] = (rcw & kRunFill) ? (rcw & ~(kRunFill | kRunDropped)) >> kRunFillShift : min(count, slab);
-        s_misc[9] = min(rcw & kRunCountMask, P.run_cap);
+        s_misc[9] = has_runs ? P.run_cap : 0u;  // (one run slot per setup workgroup, empty ones of length 0)
         s_misc[10] = K;
         s_misc[11] = K > 1u ? P.job_slot[t] : 0u;
     }
@@ -2791,9 +2792,15 @@ __global__ __launch_bounds__(NT, kTileWgs * kTileThreads / 256) void k_tile(Draw
         resolve_tile<PROG, MODE, false, NT>(kernarg_params(), x0, y0, s_key, s_u, kUnionWords, s_nwin, s_srgb,
                                            stamp ? ts : nullptr);
     }
-    // (s_misc[9]: the run count, >= 1 for a tile with kCountRuns; every wave read
-    // the run word before the segment loop)
-    if (threadIdx.x == 0 && s_misc[9]) P.run_counts[t] = 0u;
+    // A tile with pool runs (s_misc[9]: its run slots) clears its run table and run
+    // word for the next draw (every wave read them before the segment loop; a
+    // split tile: its resolving job, after every job's loop)
+    if ((uint32_t)__builtin_amdgcn_readfirstlane((int)s_misc[9])) {
+        const DrawParams& Q = kernarg_params();  // (loaded here, not held across the pass)
+        uint2* rt = Q.runs + (size_t)t * Q.run_cap;
+        for (uint32_t i = threadIdx.x; i < Q.run_cap; i += NT) rt[i] = make_uint2(0u, 0u);
+        if (threadIdx.x == 0) Q.run_counts[t] = 0u;
+    }
     if (stamp) {
         ts[4] = __builtin_amdgcn_s_memrealtime();
         ts[7] = ((unsigned long long)s_dbg[1] << 32) | s_dbg[0];

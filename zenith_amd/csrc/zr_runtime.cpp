@@ -530,7 +530,8 @@ zr_result device_sync(zr_device* d) {
     for (size_t i = 0; i < d->slab_keys.size(); ++i) {
         const uint32_t target = st[kStSlabSlot0 + i], pool = st[kStPoolSlot0 + i], max_tile = st[kStMaxSlot0 + i];
         if (!target) continue;
-        need = std::max<uint64_t>(need, (d->slab_keys[i] >> 32) * target + pool);
+        need = std::max<uint64_t>({need, (d->slab_keys[i] >> 32) * target + pool,
+                                   (d->slab_keys[i] >> 32) * bin_slab_whole(target, max_tile) + 4096});
         st[kStSlabSlot0 + i] = 0;
         st[kStPoolSlot0 + i] = 0;
         st[kStMaxSlot0 + i] = 0;
@@ -705,7 +706,11 @@ zr_result ensure_scratch(zr_device* d, ScratchSet& S, DrawParams& P) {
         if (S.run_counts_cap != cap) ZR_HIP(hipMemset(S.run_counts, 0, S.run_counts_cap * 4));
     }
     P.run_cap = std::min<uint32_t>(P.setup_wgs, kMaxRunsPerTile);
-    if ((rc = grow(d, S.runs, S.runs_cap, (uint64_t)P.ntiles * P.run_cap, sizeof(uint2)))) return rc;
+    {  // run tables start empty (length 0); k_tile clears the ones it used
+        const uint64_t cap = S.runs_cap;
+        if ((rc = grow(d, S.runs, S.runs_cap, (uint64_t)P.ntiles * P.run_cap, sizeof(uint2)))) return rc;
+        if (S.runs_cap != cap) ZR_HIP(hipMemset(S.runs, 0, S.runs_cap * sizeof(uint2)));
+    }
     if (!S.bins) {
         const uint64_t want = std::max(d->bins_want, d->initial_bins ? d->initial_bins : bin_default_capacity(prims, P.ntiles));
         if ((rc = grow(d, S.bins, S.bins_cap, want, 4))) return rc;
@@ -740,7 +745,8 @@ zr_result ensure_scratch(zr_device* d, ScratchSet& S, DrawParams& P) {
         slab = d->forced_slab;
     } else if (shape != d->bin_shapes.end()) {
         const uint64_t pool = std::max<uint64_t>((uint64_t)shape->second.pool * 5 / 4 + 4096, cap / 64);
-        slab = std::max<uint64_t>(shape->second.target, cap > pool ? (cap - pool) / nt : 0);
+        slab = std::max<uint64_t>({shape->second.target, bin_slab_whole(shape->second.target, shape->second.max_tile),
+                                   cap > pool ? (cap - pool) / nt : 0});
     }
     slab = std::min<uint64_t>({slab, cap / nt, (uint64_t)kMaxSlab});
     P.slab = (uint32_t)slab;
