@@ -279,6 +279,7 @@ struct zr_device_t {
     uint64_t bins_want = 0;     // bin buffer the last sync's draws asked for (+10 %; 0: none measured yet)
     uint64_t bins_want_max = 0; // ... the most any sync asked for since the last shrink check
     uint32_t bins_syncs = 0;    // syncs with draws since the last shrink check
+    uint32_t shrink_syncs = kBinShrinkSyncs;  // ZR_BIN_SHRINK_SYNCS (0: never shrink)
     // slab targets (bin_slab_target) measured per draw shape, (tiles << 32) | primitives;
     // the draws since the last sync, in status-slot order (DrawParams::stat_slot)
     struct BinShape {
@@ -488,8 +489,6 @@ void dump_stamps(zr_device* d) {
     fclose(f);
 }
 
-constexpr uint32_t kBinShrinkSyncs = 16;
-
 zr_result device_sync(zr_device* d) {
     zr_result rc = set_device(d);
     if (rc) return rc;
@@ -551,7 +550,7 @@ zr_result device_sync(zr_device* d) {
     if (need) {
         d->bins_want = std::min<uint64_t>(std::max<uint64_t>(need + need / 10 + 4096, 1ull << 20), 1ull << 30);
         d->bins_want_max = std::max(d->bins_want_max, d->bins_want);
-        const bool check = ++d->bins_syncs >= kBinShrinkSyncs;
+        const bool check = d->shrink_syncs && ++d->bins_syncs >= d->shrink_syncs;
         for (ScratchSet& S : d->sets) {
             if (!S.bins || (S.bins_cap >= need && (!check || S.bins_cap * 2 <= d->bins_want_max * 3))) continue;
             ZR_HIP(hipFree(S.bins));
@@ -1280,6 +1279,7 @@ ZR_API zr_result zr_device_create(int32_t hip_device, zr_device** out) {
     if (const char* rw = getenv("ZR_REC_WGS")) d->rec_wgs = (uint32_t)strtoul(rw, nullptr, 0);
     if (const char* bs = getenv("ZR_BIN_STAGE")) d->bin_stage = atoi(bs);
     if (const char* mi = getenv("ZR_MICRO")) d->micro = atoi(mi) != 0 ? 1 : 0;
+    if (const char* ss = getenv("ZR_BIN_SHRINK_SYNCS")) d->shrink_syncs = (uint32_t)strtoul(ss, nullptr, 0);
     if (const char* jb = getenv("ZR_JOBS")) d->jobs = atoi(jb) > 0 ? std::max(atoi(jb), 256) : 0;
     if (const char* nt = getenv("ZR_TILE_NT")) {
         const unsigned long v = strtoul(nt, nullptr, 0);
