@@ -448,6 +448,7 @@ inline uint32_t bin_slab_whole(uint32_t target, uint32_t max_tile) {
 // a third of it (zr_runtime ensure_scratch) and the pool the rest, which holds
 // the Gaussian-clustered c2x / c3x scenes' first frames without a dropped run.
 constexpr uint32_t kBinShrinkSyncs = 16;  // the runtime's bin-buffer shrink check interval (sync points)
+constexpr uint64_t kBinShrinkMin = 1ull << 24;  // ... and the least it frees (entries: 64 MiB)
 
 inline uint64_t bin_default_capacity(uint64_t prims, uint32_t ntiles) {
     return std::max<uint64_t>(1ull << 20, 2 * prims + 256ull * ntiles);

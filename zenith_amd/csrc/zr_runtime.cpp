@@ -521,8 +521,10 @@ zr_result device_sync(zr_device* d) {
     // for -- slabs plus the pool their runs needed -- when it is smaller (a draw with
     // a dropped run rasterized that tile by k_tile's record scan).  Every
     // kBinShrinkSyncs syncs it shrinks to the most any of them asked for when it is
-    // more than 1.5x that (not per sync: a device alternating between a light and a
-    // heavy scene would reallocate, and drop runs, every time).  (Capped at 2^30
+    // more than twice that and the difference is worth it (kBinShrinkMin): not
+    // per sync (a device alternating between a light and a heavy scene would
+    // reallocate, and drop runs, every time), and not for a few MB (a shrink of
+    // the 8-way shard emulation's small buffers cost one rank 7 us per frame).  (Capped at 2^30
     // entries, 4 GiB: a larger draw keeps using the exact spill path.)
     uint64_t need = st[kStBinNeed];  // (draws with a dropped run; the others from their slots)
     st[kStBinNeed] = 0;
@@ -552,7 +554,8 @@ zr_result device_sync(zr_device* d) {
         d->bins_want_max = std::max(d->bins_want_max, d->bins_want);
         const bool check = d->shrink_syncs && ++d->bins_syncs >= d->shrink_syncs;
         for (ScratchSet& S : d->sets) {
-            if (!S.bins || (S.bins_cap >= need && (!check || S.bins_cap * 2 <= d->bins_want_max * 3))) continue;
+            const bool shrink = check && S.bins_cap > 2 * d->bins_want_max && S.bins_cap - d->bins_want_max >= kBinShrinkMin;
+            if (!S.bins || (S.bins_cap >= need && !shrink)) continue;
             ZR_HIP(hipFree(S.bins));
             S.bins = nullptr;
             void* p = nullptr;
