@@ -983,7 +983,7 @@ __device__ uint32_t tile_jobs(uint32_t count, uint32_t run_word, uint32_t J) {
     return (J && !(run_word & kRunDropped) && count > J) ? (count + J - 1u) / J : 1u;
 }
 
-__device__ void build_job_schedule(const DrawParams& P, uint32_t nt, uint32_t* s_buf) {
+__device__ __noinline__ void build_job_schedule(const DrawParams& P, uint32_t nt, uint32_t* s_buf) {
     const uint32_t tid = threadIdx.x, J = P.job_entries, per_xcd = P.job_pad / 8u;
     uint32_t* s_cnt = s_buf;       // [8] parts per XCD, then their cursors
     uint32_t* s_tot = s_buf + 8;   // [0] key buffers (jobs of split tiles), [1] buffer cursor, [2] denied
@@ -991,14 +991,31 @@ __device__ void build_job_schedule(const DrawParams& P, uint32_t nt, uint32_t* s
     __syncthreads();
     // pass 1: every tile's job count, parked in job_slot[t] (this thread reads it
     // back in pass 2), and the parts each XCD gets
-    for (uint32_t t = tid; t < nt; t += kSetupThreads) {
-        const uint32_t c = __hip_atomic_load(&P.tile_counts[t], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-        const uint32_t w = (c & kCountRuns) ? __hip_atomic_load(&P.run_counts[t], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) : 0u;
-        const uint32_t K = tile_jobs(c & ~kCountRuns, w, J);
-        P.job_slot[t] = K;
-        if (K > 1u) {
-            atomicAdd(&s_cnt[xcd_block(t, nt) & 7u], K - 1u);
-            atomicAdd(&s_tot[0], K);
+    // (batches of 4 tiles per thread, their loads in flight together: one at a
+    // time, c3x's 8160 tiles kept this last workgroup ~10 us)
+    constexpr uint32_t kB = 4;
+    for (uint32_t t0 = tid; t0 < nt; t0 += kB * kSetupThreads) {
+        uint32_t c[kB], w[kB];
+#pragma unroll
+        for (uint32_t k = 0; k < kB; ++k) {
+            const uint32_t t = t0 + k * kSetupThreads;
+            c[k] = t < nt ? __hip_atomic_load(&P.tile_counts[t], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) : 0u;
+        }
+#pragma unroll
+        for (uint32_t k = 0; k < kB; ++k) {
+            const uint32_t t = t0 + k * kSetupThreads;
+            w[k] = (c[k] & kCountRuns) ? __hip_atomic_load(&P.run_counts[t], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) : 0u;
+        }
+#pragma unroll
+        for (uint32_t k = 0; k < kB; ++k) {
+            const uint32_t t = t0 + k * kSetupThreads;
+            if (t >= nt) continue;
+            const uint32_t K = tile_jobs(c[k] & ~kCountRuns, w[k], J);
+            P.job_slot[t] = K;
+            if (K > 1u) {
+                atomicAdd(&s_cnt[xcd_block(t, nt) & 7u], K - 1u);
+                atomicAdd(&s_tot[0], K);
+            }
         }
     }
     __syncthreads();
