@@ -308,8 +308,9 @@ def test_clustered_first_frame(cfg):
             st = dev.last_draw_stats()
             assert st["overflowed_draws"] == 0, (frame, st)
             assert st["bin_pool_runs"] > 0, (frame, st)
-            # (from the second frame its crowded tiles are split into tile jobs)
-            assert (st["tile_jobs"] > 0) == (frame > 0), (frame, st)
+            # (its crowded tiles are split into tile jobs, the first frame included:
+            # a shape not measured yet builds jobs for whatever lists turn out long)
+            assert st["tile_jobs"] > 0, (frame, st)
             assert np.array_equal(gc, oc), frame
             assert np.array_equal(gd.view(np.uint32), od.view(np.uint32)), frame
         assert st["bin_capacity"] <= 2 * st["bin_pairs"] + 512 * ntiles, st

@@ -761,15 +761,20 @@ zr_result ensure_scratch(zr_device* d, ScratchSet& S, DrawParams& P) {
     P.job_pad = P.job_slots = 0;
     if (!(d->debug & kDebugPhase1Only)) {
         const bool known = shape != d->bin_shapes.end();
+        // (a shape not measured yet may be skewed: its first draw builds jobs for
+        // whatever lists turn out long -- the clustered c2x scene's first frame
+        // walked its 30-segment tile in one workgroup -- at the cost of the job
+        // builder and the spare blocks once)
         if (d->jobs > 0)
             P.job_entries = (uint32_t)d->jobs;
-        else if (d->jobs < 0 && known && use_tile_jobs(shape->second.max_tile))
+        else if (d->jobs < 0 && (!known || use_tile_jobs(shape->second.max_tile)))
             P.job_entries = kTileJobEntries;
     }
     if (P.job_entries) {
+        // (pairs: the shape's, or for one not measured yet what the bin buffer holds)
         const uint64_t pairs = shape != d->bin_shapes.end()
                                    ? (uint64_t)P.ntiles * shape->second.target + shape->second.pool
-                                   : std::max<uint64_t>((uint64_t)P.prims * 4u, (uint64_t)P.ntiles * P.job_entries);
+                                   : std::max<uint64_t>(cap, (uint64_t)P.ntiles * P.job_entries);
         // (parts go to their tile's XCD: room for twice an even share on each)
         const uint64_t cap = std::min<uint64_t>((pairs / P.job_entries + 64) * 2 * d->job_boost, 1u << 20);
         P.job_pad = (uint32_t)((cap + 7) / 8 * 8);
