@@ -69,7 +69,7 @@ def parse():
     p.add_argument("--no-census", action="store_true",
                    help="skip the untimed winner-census frame (its instrumented k_tile would enter a rocprofv3 "
                         "kernel trace beside the timed launches; roofline.design then counts no winners)")
-    p.add_argument("--pmc", default=os.path.join(ROOT, "profiles", "r05_v1_pmc_c2.json"),
+    p.add_argument("--pmc", default=os.path.join(ROOT, "profiles", "r05_v4_pmc_c2.json"),
                    help="rocprofv3 PMC summary for roofline.traffic (tools/pmc_summary.py)")
     return p.parse_args()
 
