@@ -2779,13 +2779,24 @@ __global__ __launch_bounds__(NT, kTileWgs * kTileThreads / 256) void k_tile(Draw
             s_misc[12] = __hip_atomic_fetch_add(&P.job_tickets[buf0], 1u, __ATOMIC_ACQ_REL, __HIP_MEMORY_SCOPE_AGENT);
         __syncthreads();
         if ((uint32_t)__builtin_amdgcn_readfirstlane((int)s_misc[12]) != Kj - 1u) return;
-        for (uint32_t j = 0; j < Kj; ++j) {
-            if (j == part) continue;
-            const unsigned long long* other = P.job_keys + (size_t)(buf0 + j) * kTilePixels;
-            for (int i = i0; i < kTilePixels; i += NT) {
-                const unsigned long long k = __hip_atomic_load(&other[i], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-                if (k < s_key[i]) s_key[i] = k;
+        // (eight buffers' loads in flight per pixel: one buffer at a time, the fold
+        // of a 15-job tile was ~15 memory round trips on the pass's critical path)
+        const unsigned long long* keys0 = P.job_keys + (size_t)buf0 * kTilePixels;
+        for (int i = i0; i < kTilePixels; i += NT) {
+            unsigned long long m = s_key[i];
+            for (uint32_t j0 = 0; j0 < Kj; j0 += 8u) {
+                unsigned long long v[8];
+#pragma unroll
+                for (uint32_t k = 0; k < 8u; ++k) {
+                    const uint32_t j = j0 + k;
+                    v[k] = (j < Kj && j != part)
+                               ? __hip_atomic_load(&keys0[(size_t)j * kTilePixels + i], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT)
+                               : ~0ull;
+                }
+#pragma unroll
+                for (uint32_t k = 0; k < 8u; ++k) m = v[k] < m ? v[k] : m;
             }
+            s_key[i] = m;
         }
         if (threadIdx.x == 0) {
             __hip_atomic_store(&P.job_tickets[buf0], 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
