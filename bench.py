@@ -28,7 +28,9 @@ import torch.distributed as dist
 ROOT = os.path.dirname(os.path.abspath(__file__))
 sys.path.insert(0, ROOT)
 
-from zenith_amd import renderer, rhi, scenes, shard, zr  # noqa: E402
+from zenith_amd import buildinfo, renderer, rhi, scenes, shard, zr  # noqa: E402
+
+PROFILE_TAG = "r06_final"        # profiles/<tag>_{pmc,kt}_c2.json: the round's profiles of the final tree
 
 HBM_PEAK_GBPS = 6290.0           # MI355X_MICROARCH.md: HBM3E measured (float4 copy), the peak SURVEY.md §8d fixes
 HBM_SPEC_GBPS = 8000.0           # same table: 8.0 TB/s spec
@@ -69,9 +71,26 @@ def parse():
     p.add_argument("--no-census", action="store_true",
                    help="skip the untimed winner-census frame (its instrumented k_tile would enter a rocprofv3 "
                         "kernel trace beside the timed launches; roofline.design then counts no winners)")
-    p.add_argument("--pmc", default=os.path.join(ROOT, "profiles", "r05_v4_pmc_c2.json"),
-                   help="rocprofv3 PMC summary for roofline.traffic (tools/pmc_summary.py)")
+    p.add_argument("--pmc", default=os.path.join(ROOT, "profiles", PROFILE_TAG + "_pmc_c2.json"),
+                   help="rocprofv3 PMC summary for roofline.traffic (tools/pmc_summary.py); quoted only when it "
+                        "profiled this build (zenith_amd/buildinfo.py)")
+    p.add_argument("--rocprof", default=os.path.join(ROOT, "profiles", PROFILE_TAG + "_kt_c2.json"),
+                   help="rocprofv3 kernel-trace summary for kernels_rocprof (tools/kt_summary.py); same rule")
     return p.parse_args()
+
+
+def build_profile(path, config):
+    """A profile summary (PMC or kernel trace) of this build and config, or None
+    with the reason (a profile of another build is stale: never quoted)."""
+    if not os.path.exists(path):
+        return None, f"{os.path.basename(path)}: missing"
+    with open(path) as fh:
+        prof = json.load(fh)
+    if prof.get("config") != config:
+        return None, f"{os.path.basename(path)}: config {prof.get('config')}"
+    if prof.get("build") != buildinfo.source_hash():
+        return None, f"{os.path.basename(path)}: build {prof.get('build')} is not this tree's {buildinfo.source_hash()}"
+    return prof, os.path.basename(path)
 
 
 SETUP_IN_BYTES = 12 + 3 * 12    # what k_setup_bin loads per triangle: 3 u32 indices + 3 float3 positions
@@ -89,7 +108,8 @@ def setup_mode(requested, world, triangles, width, height):
     if requested != "auto":
         return requested
     tiles = ((width + shard.TILE - 1) // shard.TILE) * ((height + shard.TILE - 1) // shard.TILE)
-    return "partitioned" if world >= 8 and triangles >= 256 * tiles else "replicated"
+    # (a quarter triangle per pixel of the tiled target)
+    return "partitioned" if world >= 8 and 4 * triangles >= tiles * shard.TILE ** 2 else "replicated"
 
 
 def winner_bytes(program, index_size=4):
@@ -601,12 +621,13 @@ def main():
     dk = kernels.get(dom, {})
     traffic = None
     traffic_classes = None
-    if os.path.exists(a.pmc):  # measured on the warm pass's single copy, like `achieved`
-        with open(a.pmc) as fh:
-            pmc = json.load(fh)
-        if pmc.get("config") == a.config and dom in pmc.get("kernels", {}):
-            traffic = pmc["kernels"][dom]["hbm_bytes_per_launch"]
-            traffic_classes = pmc["kernels"][dom].get("classes")
+    pmc, pmc_src = build_profile(a.pmc, a.config)  # measured on the warm pass's single copy, like `achieved`
+    if pmc and dom in pmc.get("kernels", {}):
+        traffic = pmc["kernels"][dom]["hbm_bytes_per_launch"]
+        traffic_classes = pmc["kernels"][dom].get("classes")
+    kt_prof, kt_src = build_profile(a.rocprof, a.config)
+    kernels_rocprof = ({k: {"avg_us": v["avg_us"], "calls": v["calls"]} for k, v in kt_prof["kernels"].items()}
+                       if kt_prof else None)
     achieved = dk.get("gbps") or 0.0
     # SURVEY.md §8d's own fragment-pass figure (64-B records: 68 B per pair) beside
     # this design's minimum (32-B compact records: 36 B per pair)
@@ -660,8 +681,12 @@ def main():
                      "design": {"bytes": design_total, "classes": design, "winners": winners,
                                 "bytes_per_winner": per_winner, "achieved": achieved_design,
                                 "frac": round(achieved_design / HBM_PEAK_GBPS, 4) if achieved_design else None},
-                     "traffic_classes": traffic_classes},
+                     "traffic_classes": traffic_classes, "traffic_source": pmc_src},
         "kernels": kernels,
+        # the same kernels' rocprofv3 kernel-trace averages for this build (no events
+        # between launches), beside the event-timed `kernels` above
+        "kernels_rocprof": kernels_rocprof, "kernels_rocprof_source": kt_src,
+        "build": buildinfo.source_hash(),
         "bin_pairs": pairs,
         "triangles_setup": stats["triangles_setup"],
     }

@@ -25,7 +25,7 @@ def owned(scene, shard_):
 
 def assert_parity(device, scene, shard=None, **kw):
     gc, gd = renderer.render_scene(device, scene, shard=shard, **kw)
-    oc, od = oracle.render(scene, shard=shard or (0, 1), **kw)
+    oc, od = oracle.render(scene, shard=shard or (0, 1), tile_size=zr.tile_size(), **kw)
     rows = owned(scene, shard)
     full_c, full_d = gc, gd
     gc, oc = gc[rows], oc.reshape(scene.height, scene.width, -1)[rows]
@@ -247,8 +247,10 @@ def test_pool_runs(monkeypatch, slab):
 
 @pytest.mark.parametrize("jobs", ["256", "1000"])
 def test_tile_jobs(monkeypatch, jobs):
-    """Tile lists split into jobs of ZR_JOBS entries, each its own k_tile block,
-    merging keys with 64-bit atomic mins; the last job of a tile resolves it.
+    """Tile lists split into jobs of ZR_JOBS entries, each its own k_tile block
+    that stores its LDS keys to a key buffer of its own; the last job of a tile
+    (a ticket) folds the other jobs' buffers into its keys with a min and
+    resolves it.
     Exact on 256- and 512-thread tiles with the record table on and off, a
     tile-row shard, the camera program's fans, the wave path, a crowded tile
     (~35 jobs), depth ops without writes (initial-depth tiles), jobs over pool
@@ -513,9 +515,10 @@ def test_c4_micro_triangles(device):
 
 
 def mixed_micro_scene(seed, n, width, height, program, flat_z=None):
-    """Micro primitives (bbox < 1 px: resolved by k_setup_bin, DrawParams::
-    micro_keys) interleaved in API order with ordinary 6-px ones (binned and
-    walked by k_tile): every third primitive is ordinary.  flat_z: every vertex
+    """Micro primitives (a clipped bbox of one pixel: k_setup_bin tests the one
+    sample and drops those that miss it, DrawParams::micro; the covered ones are
+    binned and resolved by k_tile like any other) interleaved in API order with
+    ordinary 6-px ones: every third primitive is ordinary.  flat_z: every vertex
     at that depth, so every fragment of a pixel ties and only API order decides."""
     normals = program == scenes.PROGRAM_BLINN_PHONG
     micro = scenes.soup_arrays(seed, n, width, height, 0.45, normals).reshape(n, 3, -1)

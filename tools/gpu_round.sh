@@ -21,6 +21,7 @@ timeout -k 10 200 python bench.py --config c3 --emulate-shard 8 --no-cpu-baselin
 [ "$2" = quick ] && { echo done; exit 0; }
 fi
 timeout -k 10 200 rocprofv3 --kernel-trace --stats -d $O/kt -o run --output-format csv -- python3 bench.py --steps 50 --warmup 5 --no-cpu-baseline --no-census > $O/kt.log 2>&1 || exit 4
+python3 tools/kt_summary.py $O/kt/run_kernel_stats.csv --config c2 -o $O/kt_c2.json > /dev/null || exit 4
 timeout -k 10 200 rocprofv3 --pmc FETCH_SIZE -d $O/pf -o run --output-format csv -- python3 bench.py --steps 5 --warmup 2 --no-cpu-baseline --no-census > $O/pf.log 2>&1 || exit 5
 timeout -k 10 200 rocprofv3 --pmc WRITE_SIZE -d $O/pw -o run --output-format csv -- python3 bench.py --steps 5 --warmup 2 --no-cpu-baseline --no-census > $O/pw.log 2>&1 || exit 6
 timeout -k 10 120 rocprofv3 --pmc FETCH_SIZE -d $O/cf -o run --output-format csv -- tools/build/pmc_calib > $O/calib_known.txt 2>&1 || exit 7

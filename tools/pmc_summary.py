@@ -18,6 +18,11 @@ import argparse
 import collections
 import csv
 import json
+import os
+import sys
+
+sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+from zenith_amd.buildinfo import source_hash  # noqa: E402  (the build the passes profiled)
 
 KERNELS = {"k_setup_bin": "setup_bin", "k_tile": "tile", "k_clear": "clear"}
 # setup_bin reads indices and positions of consecutive vertices: dense, coalesced
@@ -97,7 +102,8 @@ def main():
         known = json.loads(open(a.calib_known).read().strip().splitlines()[-1])
         rf = calib(a.calib[0], "FETCH_SIZE", known)
         wf = calib(a.calib[1], "WRITE_SIZE", known)
-    out = {"config": a.config, "source": "rocprofv3 --pmc FETCH_SIZE / --pmc WRITE_SIZE (separate passes)",
+    out = {"config": a.config, "build": source_hash(),
+           "source": "rocprofv3 --pmc FETCH_SIZE / --pmc WRITE_SIZE (separate passes)",
            "calibration": {"fetch_factor": rf, "write_factor": wf,
                            "note": "bytes moved / (counter KiB * 1024) on 1 GiB buffers (tools/pmc_calib.hip)"},
            "kernels": {}}

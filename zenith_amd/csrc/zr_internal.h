@@ -7,8 +7,15 @@
 
 namespace zr {
 
-constexpr int kTile = 32;          // screen-tile edge in pixels (one workgroup per tile)
-constexpr int kTileShift = 5;
+// Screen-tile edge in pixels (one k_tile workgroup per tile).  A build choice of
+// 16, 32 or 64 (tools/build_variant.sh -DZR_TILE=...; docs/EXPERIMENTS.md round 6
+// has the A/B); zr_tile_size() reports it, and zenith_amd/shard.py reads it there.
+#ifndef ZR_TILE
+#define ZR_TILE 32
+#endif
+constexpr int kTile = ZR_TILE;
+static_assert(kTile == 16 || kTile == 32 || kTile == 64, "tile edge: 16, 32 or 64 pixels");
+constexpr int kTileShift = kTile == 16 ? 4 : kTile == 32 ? 5 : 6;
 constexpr int kTilePixels = kTile * kTile;
 constexpr int kTileThreads = 256;  // k_tile workgroup: 4 waves of 64 (512 for some passes: tile_threads_for)
 constexpr uint32_t kSortCap = 1024;     // tile-list segment sorted by area in LDS
@@ -107,8 +114,10 @@ constexpr uint32_t kMaxRunsPerTile = 256;  // k_tile keeps a tile's run table in
 struct alignas(8) BBox {
     uint32_t bb0, bb1;  // as TriRecord::bb0/bb1
 };
-constexpr uint32_t kMaxTilesPerPass = 16384;  // LDS histogram of the setup pass (64 KB)
-constexpr uint32_t kJobTileBits = 14;          // tile_order item: tile | part << kJobTileBits (tiles < kMaxTilesPerPass)
+// LDS histogram of the setup pass (64 KB; 128 KB with 16-px tiles, whose 4K
+// target has 32,400 tiles)
+constexpr uint32_t kMaxTilesPerPass = kTile == 16 ? 32768u : 16384u;
+constexpr uint32_t kJobTileBits = kTile == 16 ? 15u : 14u;  // tile_order item: tile | part << kJobTileBits (tiles < kMaxTilesPerPass)
 constexpr uint32_t kJobTileMask = (1u << kJobTileBits) - 1u;
 constexpr uint32_t kJobNone = 0xFFFFFFFFu;     // tile_order item of a spare block (job grids)
 static_assert((1u << kJobTileBits) == kMaxTilesPerPass, "job items hold any tile index");
@@ -227,7 +236,9 @@ enum StatusWord : uint32_t {
     kStSlabSlot0 = 16,      // [kSlabSlots]: the slab target (bin_slab_target) of the draw given slot i (DrawParams::stat_slot)
     kStPoolSlot0 = 64,      // [kSlabSlots]: the pool entries that draw's runs asked for (saturating)
     kStMaxSlot0 = 112,      // [kSlabSlots]: that draw's longest tile list
-    kStWords = 160,
+    kStJobBufSlot0 = 160,   // [kSlabSlots]: the tile-job key buffers that draw's split tiles needed (0: no jobs built)
+    kStJobPartSlot0 = 208,  // [kSlabSlots]: ... and the most parts (jobs past the first) it put on one XCD
+    kStWords = 256,
 };
 // Device counters of k_setup_bin, read by the draw's k_tile (tile 0 reports them
 // and resets them, as every tile resets its count, so a draw needs no memset).
@@ -241,6 +252,8 @@ enum CounterWord : uint32_t {
     kCtPoolRuns = 10,    // pool runs the draw registered
     kCtJobsDenied = 11,  // 1: the draw's tile jobs did not fit (build_job_schedule)
     kCtJobs = 12,        // tile jobs of the draw beyond one per tile
+    kCtJobBufs = 13,     // key buffers the draw's split tiles needed (build_job_schedule; fitting or not)
+    kCtJobXcdMax = 14,   // the most parts of the draw on one XCD (build_job_schedule)
     kCtWords = 32,
 };
 // draw_info words (written by k_setup_bin for k_tile)
@@ -402,7 +415,12 @@ constexpr uint32_t kSetupMiscWords = 96 + 8 * kSchedBuckets;
 // partitioned shard whose tiles fit one round of 512-thread workgroups (4 per CU)
 // takes 8 waves per tile -- C3 rank of 8 (1020 tiles), with the records-mode grid
 // below: 4.47x vs 4.12x at 4 waves -- and 4 waves only past one round.
+// Other tile edges have one workgroup size each: 64-px tiles (4096 pixels, 32 KiB
+// of keys) take 1024 threads, two workgroups per CU; 16-px tiles (256 pixels)
+// take 256.
 inline uint32_t tile_threads_for(uint32_t ntiles, uint32_t cus, uint64_t prims, bool partitioned) {
+    if (kTile == 64) return 1024u;
+    if (kTile == 16) return (uint32_t)kTileThreads;
     const uint32_t c = cus ? cus : 1u;
     const uint32_t per_cu = ntiles / c;
     if (partitioned) return ntiles > 4ull * c ? (uint32_t)kTileThreads : 512u;
@@ -460,6 +478,9 @@ inline uint64_t bin_default_capacity(uint64_t prims, uint32_t ntiles) {
 // scene's tile pass.
 constexpr uint32_t kTileJobEntries = 2048;
 inline bool use_tile_jobs(uint32_t max_tile) { return max_tile > 4u * kTileJobEntries; }
+// Key buffers a draw shape not measured yet may get for its tile jobs (64 MiB;
+// zr_runtime ensure_scratch): afterwards a shape gets what its split needed.
+constexpr uint64_t kJobKeyBytesFirst = 64ull << 20;
 
 inline uint32_t records_setup_wgs(uint64_t entries, uint32_t cus) {
     const uint64_t w = (entries + 2047u) / 2048u;
@@ -473,8 +494,10 @@ inline uint32_t records_setup_wgs(uint64_t entries, uint32_t cus) {
 // us); with fewer, larger primitives per tile their pixels' record requests
 // already merge and the inserts and lookups cost more than they save (C3, 122
 // per tile: 174.6 -> 181.8 us).
+// (Stated per pixel -- a quarter primitive per pixel -- so it carries over to
+// other tile edges.)
 inline bool use_record_table(uint64_t prims, uint32_t tiles_x, uint32_t tiles_y) {
-    return prims >= 256ull * tiles_x * tiles_y;
+    return 4ull * prims >= (uint64_t)kTilePixels * tiles_x * tiles_y;
 }
 
 // Whether k_setup_bin builds a heaviest-first tile schedule for k_tile
@@ -486,8 +509,8 @@ inline bool use_record_table(uint64_t prims, uint32_t tiles_x, uint32_t tiles_y)
 // (round 4, ZR_TILE_SCHED A/B, 2 runs: cerberus frame 53.8 -> 51.0 us; C2 108.4
 // -> 113.7, C3 238.9 -> 245.0, C1 and C4 equal within 0.5 %).
 inline bool use_tile_schedule(uint32_t ntiles, uint32_t cus, uint32_t tile_threads, uint64_t prims) {
-    const uint64_t slots = (uint64_t)cus * (tile_threads >= 512u ? 4u : 8u);
-    return ntiles > slots && prims < 32ull * ntiles;
+    const uint64_t slots = (uint64_t)cus * (8u * kTileThreads / tile_threads);
+    return ntiles > slots && 32ull * prims < (uint64_t)ntiles * kTilePixels;  // (< 1/32 primitive per pixel)
 }
 
 __host__ __device__ inline ShardGeom shard_geom(const DrawParams& P) {

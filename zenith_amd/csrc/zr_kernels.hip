@@ -1021,7 +1021,15 @@ __device__ __noinline__ void build_job_schedule(const DrawParams& P, uint32_t nt
     __syncthreads();
     if (tid == 0) {
         bool ok = s_tot[0] <= P.job_slots;
-        for (uint32_t x = 0; x < 8u; ++x) ok = ok && s_cnt[x] <= per_xcd;
+        uint32_t xmax = 0;
+        for (uint32_t x = 0; x < 8u; ++x) {
+            ok = ok && s_cnt[x] <= per_xcd;
+            xmax = max(xmax, s_cnt[x]);
+        }
+        // what the split needs, fitting or not (the runtime sizes the shape's next
+        // draws from it: key buffers and spare blocks per XCD)
+        P.counters[kCtJobBufs] = s_tot[0];
+        P.counters[kCtJobXcdMax] = xmax;
         s_tot[2] = ok ? 0u : 1u;
         P.draw_info[kInfoJobEntries] = ok ? J : 0u;
         if (!ok) atomicAdd(&P.counters[kCtJobsDenied], 1u);
@@ -1846,10 +1854,15 @@ __device__ __forceinline__ void resolve_vids(const DrawParams& P, uint32_t prim,
 constexpr uint32_t kRecHashSlots = 2048;
 constexpr uint32_t kRecTabProbes = 8;
 __device__ __forceinline__ uint32_t rec_hash(uint32_t rec) { return (rec * 0x9E3779B1u) >> 21; }  // 11 bits
+// Vertex 0 of a small primitive (extents <= 64 px) whose bbox meets the tile lies
+// within [-64 px, kTile + 64 px) of the tile origin: stored as u16 offsets (24.8
+// fixed point) from 64 px above-left of the origin.
+constexpr int kRelBias = 64 * 256;
+static_assert((kTile + 128) * 256 <= 65536, "tile-relative vertex 0 fits u16");
 
 __device__ __forceinline__ void rec_table_insert(uint32_t* s_thash, int4* s_trec, uint32_t rec, uint32_t j,
                                                  const int4 q0, const int4 q1, int x0, int y0) {
-    const uint32_t rel = ((uint32_t)(q0.x - x0 * 256) & 0xFFFFu) | ((uint32_t)(q0.y - y0 * 256) << 16);
+    const uint32_t rel = ((uint32_t)(q0.x - x0 * 256 + kRelBias) & 0xFFFFu) | ((uint32_t)(q0.y - y0 * 256 + kRelBias) << 16);
     s_trec[j] = make_int4((int)rel, q0.z, q0.w, q1.w);
     uint32_t h = rec_hash(rec);
     for (uint32_t p = 0; p < kRecTabProbes; ++p) {
@@ -1867,7 +1880,8 @@ __device__ __forceinline__ bool rec_table_find(const uint32_t* s_thash, const in
         if (v == 0u) return false;
         if (s_sorted[v - 1u] == rec) {
             const int4 e = s_trec[v - 1u];
-            q0 = make_int4(x0 * 256 + (int)(int16_t)(e.x & 0xFFFF), y0 * 256 + (e.x >> 16), e.y, e.z);
+            q0 = make_int4(x0 * 256 - kRelBias + (int)((uint32_t)e.x & 0xFFFFu), y0 * 256 - kRelBias + (int)((uint32_t)e.x >> 16),
+                           e.y, e.z);
             q1 = make_int4(0, 0, 0, e.w);
             return true;
         }
@@ -2034,7 +2048,7 @@ struct WinLayout {
 // dense winner list (kWinSlots record ids); both live where the keys were.
 constexpr uint32_t kWinSlots = kTilePixels;
 constexpr uint32_t kWinEmpty = 0xFFFFFFFFu;
-__device__ __forceinline__ uint32_t win_hash(uint32_t rec) { return (rec * 0x9E3779B1u) >> 22; }  // 10 bits
+__device__ __forceinline__ uint32_t win_hash(uint32_t rec) { return (rec * 0x9E3779B1u) >> (32 - 2 * kTileShift); }  // log2(kWinSlots) bits
 
 __device__ __forceinline__ void copy3(float* dst, const float* src) {
     dst[0] = src[0]; dst[1] = src[1]; dst[2] = src[2];
@@ -2347,9 +2361,12 @@ __global__ __launch_bounds__(NT, kTileWgs * kTileThreads / 256) void k_tile(Draw
     uint32_t& s_bclaim = s_misc[2];
     uint32_t* s_dbg = s_misc + 3;    // [2] kDebugStamps: lane-walk steps of the chunks, wave-path sweeps
     uint32_t* s_nwin = s_misc + 5;   // resolve: distinct winners of the tile
-    const uint32_t b = (tile_debug(P) & kDebugReverseTiles) ? gridDim.x - 1u - blockIdx.x : blockIdx.x;
     // a tile_order item: tile | job part << kJobTileBits, or a job grid's spare block
     const uint32_t jp = P.job_entries ? P.job_pad : 0u;  // (tile jobs: part blocks first)
+    // (reversed timing runs reverse the tile blocks only, so block jp -- the
+    // reporter below -- still holds a tile, never a spare part block)
+    const uint32_t b = ((tile_debug(P) & kDebugReverseTiles) && blockIdx.x >= jp) ? jp + (gridDim.x - 1u - blockIdx.x)
+                                                                                   : blockIdx.x;
     const uint32_t item = (b < jp || P.tile_sched) ? P.tile_order[b] : xcd_tile(b - jp, P.ntiles);
     if (item == kJobNone) return;
     const uint32_t t = item & kJobTileMask, part = item >> kJobTileBits;
@@ -2489,6 +2506,8 @@ __global__ __launch_bounds__(NT, kTileWgs * kTileThreads / 256) void k_tile(Draw
             st[kStSlabSlot0 + P.stat_slot] = target;
             st[kStPoolSlot0 + P.stat_slot] = pool > 0xFFFFFFFFull ? 0xFFFFFFFFu : (uint32_t)pool;
             st[kStMaxSlot0 + P.stat_slot] = P.counters[kCtMaxTile];
+            st[kStJobBufSlot0 + P.stat_slot] = P.counters[kCtJobBufs];
+            st[kStJobPartSlot0 + P.stat_slot] = P.counters[kCtJobXcdMax];
         }
     }
     __syncthreads();
@@ -2808,7 +2827,7 @@ __global__ __launch_bounds__(NT, kTileWgs * kTileThreads / 256) void k_tile(Draw
 
     // Resolve (the index width is a template parameter so a winner's record and
     // index loads are issued back to back).
-    if (NT >= 512 && !ZR_RESOLVE_DEDUP512) {
+    if constexpr (NT >= 512 && !ZR_RESOLVE_DEDUP512) {
         if (P.index_size == 4)
             resolve_pixels<PROG, MODE, true, NT, kTab>(kernarg_params(), x0, y0, s_key, s_srgb, s_thash, s_trec, s_sorted);
         else
@@ -2899,11 +2918,18 @@ static void launch_tile_pmt(const DrawParams& p, hipStream_t s, bool initd) {
         hipLaunchKernelGGL((k_tile<PROG, MODE, false, NT>), dim3(blocks), dim3(NT), 0, s, p);
 }
 
+// (workgroup sizes per tile edge: tile_threads_for)
 template <int PROG, int MODE>
 static void launch_tile_pm(const DrawParams& p, hipStream_t s, bool initd) {
-    switch (p.tile_threads) {
-    case 512: launch_tile_pmt<PROG, MODE, 512>(p, s, initd); break;
-    default: launch_tile_pmt<PROG, MODE, kTileThreads>(p, s, initd); break;
+    if constexpr (kTile == 64) {
+        launch_tile_pmt<PROG, MODE, 1024>(p, s, initd);
+    } else if constexpr (kTile == 16) {
+        launch_tile_pmt<PROG, MODE, kTileThreads>(p, s, initd);
+    } else {
+        switch (p.tile_threads) {
+        case 512: launch_tile_pmt<PROG, MODE, 512>(p, s, initd); break;
+        default: launch_tile_pmt<PROG, MODE, kTileThreads>(p, s, initd); break;
+        }
     }
 }
 

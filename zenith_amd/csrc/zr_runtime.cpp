@@ -286,9 +286,11 @@ struct zr_device_t {
         uint32_t target = 0;    // bin_slab_target
         uint32_t pool = 0;      // pool entries its runs asked for (at the slab it had)
         uint32_t max_tile = 0;  // its longest tile list
+        uint32_t job_bufs = 0;  // tile-job key buffers its split tiles needed (0: none built)
+        uint32_t job_parts = 0; // ... and the most parts it put on one XCD
     };
     int jobs = -1;              // ZR_JOBS: tile jobs of N entries (tests), 0 off; -1: use_tile_jobs
-    uint32_t job_boost = 1;     // job_pad multiplier, doubled after a draw whose jobs did not fit
+    uint64_t job_want_max = 0;  // the most key buffers a draw asked for since the last shrink check
     std::unordered_map<uint64_t, BinShape> bin_shapes;
     std::vector<uint64_t> slab_keys;
     uint32_t forced_slab = ~0u; // ZR_BIN_SLAB: every draw's slab (tests: pool runs everywhere)
@@ -502,10 +504,7 @@ zr_result device_sync(zr_device* d) {
     d->last.bin_pool_pairs = st[kStPoolPairs];
     d->last.bin_pool_runs = st[kStPoolRuns];
     d->last.tile_jobs = st[kStJobs];
-    if (st[kStJobsDenied]) {
-        d->job_boost = std::min<uint32_t>(d->job_boost * 2u, 1u << 12);
-        st[kStJobsDenied] = 0;
-    }
+    st[kStJobsDenied] = 0;  // (a denied split is sized from its shape's kStJobBufSlot0 below)
     // partitioned draws since the previous sync point
     if (st[kStRouteMax]) {  // kept from the last interval with partitioned draws
         d->last.route_max_entries = st[kStRouteMax];
@@ -530,6 +529,10 @@ zr_result device_sync(zr_device* d) {
     st[kStBinNeed] = 0;
     for (size_t i = 0; i < d->slab_keys.size(); ++i) {
         const uint32_t target = st[kStSlabSlot0 + i], pool = st[kStPoolSlot0 + i], max_tile = st[kStMaxSlot0 + i];
+        const uint32_t job_bufs = st[kStJobBufSlot0 + i], job_parts = st[kStJobPartSlot0 + i];
+        st[kStJobBufSlot0 + i] = 0;
+        st[kStJobPartSlot0 + i] = 0;
+        d->job_want_max = std::max<uint64_t>(d->job_want_max, job_bufs);
         if (!target) continue;
         need = std::max<uint64_t>({need, (d->slab_keys[i] >> 32) * target + pool,
                                    (d->slab_keys[i] >> 32) * bin_slab_whole(target, max_tile) + 4096});
@@ -540,9 +543,12 @@ zr_result device_sync(zr_device* d) {
         zr_device_t::BinShape& v = d->bin_shapes[d->slab_keys[i]];
         if (v.target != target || v.pool != pool) d->scratch_gen++;  // recorded graphs bake the slab in
         if (use_tile_jobs(v.max_tile) != use_tile_jobs(max_tile)) d->scratch_gen++;
+        if (v.job_bufs != job_bufs || v.job_parts != job_parts) d->scratch_gen++;
         v.target = target;
         v.pool = pool;
         v.max_tile = max_tile;
+        v.job_bufs = job_bufs;
+        v.job_parts = job_parts;
     }
     d->slab_keys.clear();
     if (st[kStOverflow]) {
@@ -566,10 +572,25 @@ zr_result device_sync(zr_device* d) {
             d->scratch_gen++;
         }
         if (check) {
+            // tile-job key buffers (8 B per pixel of a tile each) follow the most
+            // any draw of the interval asked for, the same way
+            const uint64_t keep = (d->job_want_max ? d->job_want_max * 5 / 4 + 16 : 0) * (uint64_t)kTilePixels;
+            for (ScratchSet& S : d->sets) {
+                if (!S.job_keys || S.job_keys_cap <= 2 * keep + (1u << 16)) continue;
+                (void)hipFree(S.job_keys);
+                (void)hipFree(S.job_tickets);
+                S.job_keys = nullptr;
+                S.job_tickets = nullptr;
+                S.job_keys_cap = S.job_tickets_cap = 0;
+                d->scratch_gen++;
+            }
+            d->job_want_max = 0;
             d->bins_want_max = 0;
             d->bins_syncs = 0;
         }
     }
+    d->last.job_key_bytes = 0;
+    for (const ScratchSet& S : d->sets) d->last.job_key_bytes += S.job_keys ? S.job_keys_cap * 8 : 0;
     d->last.overflowed_draws = d->overflowed_draws;
     d->last.bin_capacity = d->sets[0].bins_cap;
     for (const ScratchSet& S : d->sets)
@@ -759,8 +780,8 @@ zr_result ensure_scratch(zr_device* d, ScratchSet& S, DrawParams& P) {
     // beyond one per tile by the shape's pairs / J (pairs < tiles x target).
     P.job_entries = 0;
     P.job_pad = P.job_slots = 0;
+    const bool known = shape != d->bin_shapes.end();
     if (!(d->debug & kDebugPhase1Only)) {
-        const bool known = shape != d->bin_shapes.end();
         // (a shape not measured yet may be skewed: its first draw builds jobs for
         // whatever lists turn out long -- the clustered c2x scene's first frame
         // walked its 30-segment tile in one workgroup -- at the cost of the job
@@ -771,14 +792,25 @@ zr_result ensure_scratch(zr_device* d, ScratchSet& S, DrawParams& P) {
             P.job_entries = kTileJobEntries;
     }
     if (P.job_entries) {
-        // (pairs: the shape's, or for one not measured yet what the bin buffer holds)
-        const uint64_t pairs = shape != d->bin_shapes.end()
-                                   ? (uint64_t)P.ntiles * shape->second.target + shape->second.pool
-                                   : std::max<uint64_t>(cap, (uint64_t)P.ntiles * P.job_entries);
-        // (parts go to their tile's XCD: room for twice an even share on each)
-        const uint64_t cap = std::min<uint64_t>((pairs / P.job_entries + 64) * 2 * d->job_boost, 1u << 20);
-        P.job_pad = (uint32_t)((cap + 7) / 8 * 8);
-        P.job_slots = P.job_pad + std::min<uint32_t>(P.job_pad, P.ntiles);  // (key buffers: parts + the split tiles' part 0)
+        // Key buffers (one per job of a split tile, kTilePixels x 8 B each) and the
+        // grid's spare part blocks (job_pad / 8 per XCD: a tile's parts go to its
+        // XCD).  A shape whose split was measured gets what it needed (+25 %): a draw
+        // that did not fit is counted and rasterized unsplit, and the next draw of
+        // its shape is sized from what it asked for.  A shape not measured yet gets
+        // what the bin buffer's pairs can need at most -- each part past the first
+        // holds job_entries pairs, each split tile more than job_entries -- within a
+        // fixed memory bound (kJobKeyBytesFirst).
+        uint64_t bufs, parts;
+        if (known && shape->second.job_bufs) {
+            bufs = (uint64_t)shape->second.job_bufs * 5 / 4 + 16;
+            parts = (uint64_t)shape->second.job_parts * 5 / 4 + 8;
+        } else {
+            const uint64_t pairs = known ? (uint64_t)P.ntiles * shape->second.target + shape->second.pool : cap;
+            bufs = std::min<uint64_t>(2 * (pairs / P.job_entries) + 64, kJobKeyBytesFirst / (8ull * kTilePixels));
+            parts = pairs / P.job_entries / 4 + 64;  // (a few crowded tiles: parts spread over several XCDs)
+        }
+        P.job_pad = (uint32_t)std::min<uint64_t>(8 * parts, 1u << 20);
+        P.job_slots = (uint32_t)std::min<uint64_t>(bufs, 1u << 20);
         const uint64_t tc = S.job_tickets_cap;
         if ((rc = grow(d, S.job_slot, S.job_slot_cap, P.ntiles, 4))) return rc;
         if ((rc = grow(d, S.job_keys, S.job_keys_cap, (uint64_t)P.job_slots * kTilePixels, 8))) return rc;
@@ -966,7 +998,7 @@ zr_result exec_draw(zr_device* d, ExecState& s, const Cmd& c, bool indexed) {
     // binning geometry: k_setup_bin runs one kSetupThreads workgroup per CU at most
     // (its LDS histogram of all tiles; workgroups never wait for each other)
     if (P.ntiles > kMaxTilesPerPass)
-        return fail(ZR_ERROR_FEATURE_NOT_PRESENT, "more than 16384 owned 32x32 tiles in one pass");
+        return fail(ZR_ERROR_FEATURE_NOT_PRESENT, "more owned tiles in one pass than the setup pass histogram holds (kMaxTilesPerPass)");
     P.setup_batch = mesh ? 1u : 2u;  // k_setup_bin<2> (the mesh instance: <1, true>)
     if (d->occupancy_checked_tiles != P.ntiles || d->occupancy_checked_mesh != mesh) {
         int nb = 0;
@@ -980,7 +1012,9 @@ zr_result exec_draw(zr_device* d, ExecState& s, const Cmd& c, bool indexed) {
     {
         // one workgroup per CU (fewer for small draws); a wave processes units of
         // 64 * batch * 2^k primitives, at most ~64 units per workgroup on average
-        const uint64_t cus = (uint64_t)std::max(d->cu_count, 1);
+        // (at most kMaxRunsPerTile workgroups: a pool run takes its workgroup's slot
+        // of the tile's run table)
+        const uint64_t cus = std::min<uint64_t>((uint64_t)std::max(d->cu_count, 1), kMaxRunsPerTile);
         const uint64_t per_wg = (uint64_t)kSetupThreads * P.setup_batch;
         P.setup_wgs = (uint32_t)std::max<uint64_t>(1, std::min<uint64_t>(cus, (positions + per_wg - 1) / per_wg));
         if (partitioned)  // records mode: sized to the expected received entries (ZR_REC_WGS: A/B)
@@ -1021,7 +1055,7 @@ zr_result exec_draw(zr_device* d, ExecState& s, const Cmd& c, bool indexed) {
     // (records mode never runs setup_finish: no effect there)
     P.micro = (d->micro < 0 ? use_micro_test(prims, (uint64_t)(P.ra_x1 - P.ra_x0 + 1) * (uint64_t)(P.ra_y1 - P.ra_y0 + 1))
                             : d->micro != 0) ? 1u : 0u;
-    P.tile_threads = d->tile_threads ? d->tile_threads
+    P.tile_threads = (d->tile_threads && kTile == 32) ? d->tile_threads
                                      : tile_threads_for(P.ntiles, (uint32_t)std::max(d->cu_count, 1), prims, partitioned);
     P.rec_table = (d->rec_table < 0 ? use_record_table(prims, P.tiles_x, P.tiles_y) : d->rec_table != 0) ? 1u : 0u;
     const bool sched = d->tile_sched < 0 ? use_tile_schedule(P.ntiles, (uint32_t)std::max(d->cu_count, 1), P.tile_threads, prims)
@@ -1278,7 +1312,9 @@ ZR_API zr_result zr_device_create(int32_t hip_device, zr_device** out) {
     d->hip_device = hip_device;
     if (const char* dbg = getenv("ZR_DEBUG")) d->debug = (uint32_t)strtoul(dbg, nullptr, 0);
     if (const char* p = getenv("ZR_DEBUG_TS")) d->dbg_ts_path = p;
-    if (const char* cap = getenv("ZR_BIN_CAPACITY")) d->initial_bins = std::max<uint64_t>(64, strtoull(cap, nullptr, 0));
+    // (at most 2^30 entries: k_setup_bin's cursors tag pending and dropped runs in bits 30-31)
+    if (const char* cap = getenv("ZR_BIN_CAPACITY"))
+        d->initial_bins = std::min<uint64_t>(std::max<uint64_t>(64, strtoull(cap, nullptr, 0)), 1ull << 30);
     if (const char* sl = getenv("ZR_BIN_SLAB")) d->forced_slab = (uint32_t)std::min<uint64_t>(strtoull(sl, nullptr, 0), kMaxSlab);
     if (const char* g = getenv("ZR_GRAPH")) d->use_graphs = strtoul(g, nullptr, 0) != 0;
     if (const char* o = getenv("ZR_SETUP_OVERLAP")) d->setup_overlap = strtoul(o, nullptr, 0) != 0 ? 1 : 0;
@@ -2095,6 +2131,8 @@ zr_result rccl_exchange(void* user, void* stream, const void* send, void* recv, 
 // and unpacks it on the root.  One op per (tile row, owner), none for the root's
 // own tiles.  `offset` is the byte offset in the image (the same on both sides);
 // the last tile row may be partial.
+ZR_API uint32_t zr_tile_size(void) { return (uint32_t)kTile; }
+
 ZR_API int32_t zr_gather_plan(uint32_t width, uint32_t height, uint32_t bytes_per_pixel, int32_t nranks, int32_t rank,
                               int32_t root, zr_transfer_op* out, int32_t capacity) {
     if (nranks < 1 || nranks > (int32_t)kMaxShards || rank < 0 || rank >= nranks || root < 0 || root >= nranks ||

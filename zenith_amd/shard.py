@@ -17,7 +17,9 @@ import numpy as np
 import torch
 import torch.distributed as dist
 
-TILE = 32  # must match zr::kTile (zenith_amd/csrc/zr_internal.h)
+from . import zr
+
+TILE = zr.tile_size()  # the library's tile edge (zr::kTile, zr_tile_size): the unit of ownership
 
 
 def tile_owner(tiles_x: int, tiles_y: int, world: int) -> np.ndarray:

@@ -87,7 +87,7 @@ class zr_draw_stats(C.Structure):
                 ("bin_capacity", C.c_uint64), ("overflowed_draws", C.c_uint64),
                 ("route_max_entries", C.c_uint64), ("route_fallback_draws", C.c_uint64), ("winners", C.c_uint64),
                 ("micro_fragments", C.c_uint64), ("bin_pool_pairs", C.c_uint64), ("bin_pool_runs", C.c_uint64),
-                ("tile_jobs", C.c_uint64)]
+                ("tile_jobs", C.c_uint64), ("job_key_bytes", C.c_uint64)]
 
 
 class zr_buffer_desc(C.Structure):
@@ -245,6 +245,7 @@ _SIGS = {
     "zr_gather_plan": (C.c_int32, [C.c_uint32, C.c_uint32, C.c_uint32, C.c_int32, C.c_int32, C.c_int32,
                                    C.POINTER(zr_transfer_op), C.c_int32]),
     "zr_exchange_plan": (C.c_int32, [C.c_int32, C.c_int32, C.c_uint64, C.POINTER(zr_transfer_op), C.c_int32]),
+    "zr_tile_size": (C.c_uint32, []),
     "zr_device_set_stream": (_R, [_P, _P]),
     "zr_device_stream": (_P, [_P]),
     "zr_rccl_available": (C.c_int32, []),
@@ -282,6 +283,13 @@ def lib():
 
 def exported_symbols():
     return sorted(_SIGS)
+
+
+def tile_size() -> int:
+    """The loaded library's screen-tile edge (zr_tile_size; 32 for a build that
+    predates it, under A/B)."""
+    L = lib()
+    return int(L.zr_tile_size()) if hasattr(L, "zr_tile_size") else 32
 
 
 def check(rc: int, what: str) -> int:
