@@ -261,7 +261,7 @@ def emulate(a, scene, cuda):
     def timed(enc):
         for _ in range(a.warmup):
             dev.submit(enc)
-        dev.wait_idle()
+            dev.wait_idle()  # (a sync per warm-up frame, as in the bench's timed_pass)
         torch.cuda.synchronize()
         t0 = time.perf_counter()
         for _ in range(a.steps):
@@ -541,7 +541,11 @@ def main():
         frame[0] = 0
         for _ in range(a.warmup):
             step(copies)
-        dev.wait_idle()
+            # each warm-up frame ends at a sync point, as a presented frame does: the
+            # runtime sizes bins and jobs, and picks the tile edge, from what the
+            # draws it has seen measured (a shape that changes its tile edge is
+            # measured again at the next sync)
+            dev.wait_idle()
         torch.cuda.synchronize()
         if distributed:
             dist.barrier()

@@ -153,6 +153,9 @@ typedef struct zr_draw_stats {
     /* device memory held for tile-job key buffers (all scratch sets), sized per
      * draw shape from what its split needed and shrunk with the bin buffer */
     uint64_t job_key_bytes;
+    /* the tile edge (pixels) of the last draw recorded: 16, 32 or 64, chosen per
+     * draw; tile-row shards always 32 (zr_tile_size) */
+    uint64_t tile_size;
 } zr_draw_stats;
 ZR_API zr_result zr_device_last_draw_stats(zr_device *dev, zr_draw_stats *out);
 /* Last error message recorded on this thread (for logging; never NULL). */
@@ -478,8 +481,9 @@ ZR_API int32_t zr_gather_plan(uint32_t width, uint32_t height, uint32_t bytes_pe
                               int32_t root, zr_transfer_op *out, int32_t capacity);
 ZR_API int32_t zr_exchange_plan(int32_t nranks, int32_t rank, uint64_t bytes_per_rank, zr_transfer_op *out,
                                 int32_t capacity);
-/* The screen-tile edge in pixels (16, 32 or 64; a build choice):
- * the unit of tile-row shard ownership above (zenith_amd/shard.py owned_mask). */
+/* The screen-tile edge of tile-row shards in pixels (32): the unit of shard
+ * ownership above (zenith_amd/shard.py owned_mask).  Unsharded draws pick 16,
+ * 32 or 64 per draw (zr_draw_stats.tile_size). */
 ZR_API uint32_t zr_tile_size(void);
 
 /* -------------------------------------------------------------- submission */

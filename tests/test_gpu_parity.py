@@ -299,15 +299,20 @@ def test_clustered_first_frame(cfg):
     frame already holds every pair (the crowded tiles' excess in pool runs, no
     tile takes the record scan), the second frame too (slabs of the measured
     target), both exact; the bin buffer then holds at most 2x the pairs plus 512
-    entries per tile."""
+    entries per tile.  The tile edge (tile_shift_for): the first
+    frame takes the edge by size (c2x 32 px, c3x at 4K 64 px), whose measured
+    shape is crowded, so the later frames take 16 px (c2x) or, where 16-px tiles
+    would be too many, 32 (c3x)."""
     s = scenes.config_scene(cfg)
     oc, od = oracle.render(s, nthreads=16)
-    ntiles = -(-s.width // 32) * -(-s.height // 32)
+    edges = {"c2x": [32, 16, 16], "c3x": [64, 32, 32]}[cfg]
     dev = rhi.RenderDevice(0)
     try:
         for frame in range(3):
             gc, gd = renderer.render_scene(dev, s)
             st = dev.last_draw_stats()
+            assert st["tile_size"] == edges[frame], (frame, st)
+            ntiles = -(-s.width // st["tile_size"]) * -(-s.height // st["tile_size"])
             assert st["overflowed_draws"] == 0, (frame, st)
             assert st["bin_pool_runs"] > 0, (frame, st)
             # (its crowded tiles are split into tile jobs, the first frame included:
@@ -414,6 +419,73 @@ def test_tile_workgroup_sizes(monkeypatch, nt):
         dev.close()
 
 
+@pytest.mark.parametrize("edge", [16, 32, 64])
+def test_tile_edges(monkeypatch, edge):
+    """Every path of k_tile at each tile edge (ZR_TILE forces it; the runtime
+    picks per draw, tile_shift_for): the flat and Blinn-Phong programs under the
+    depth-writing modes take 16- and 64-px tiles (256 / 1024 threads), the other
+    draws (triangle and camera programs, last-wins modes) and tile-row shards stay
+    on 32.  Exact on soups, large primitives (wave path and lane walk), lists of
+    several segments with the record table on and off, a crowded tile in pool
+    runs, tile jobs, the record-scan spill, and frames back to back."""
+    monkeypatch.setenv("ZR_TILE", str(edge))
+    dev = rhi.RenderDevice(0)
+    try:
+        def check(scene, want, shard=None):
+            assert_parity(dev, scene, shard=shard)
+            assert dev.last_draw_stats()["tile_size"] == want, (scene.name, dev.last_draw_stats())
+        for prog in (scenes.PROGRAM_FLAT_COLOR, scenes.PROGRAM_BLINN_PHONG):
+            check(scenes.soup_scene(160 + prog, 5000, 330, 250, 9.0, prog), edge)
+        check(scenes.soup_scene(163, 400, 512, 384, 150.0, scenes.PROGRAM_BLINN_PHONG), edge)
+        for op, clear in ((scenes.OP_LEQUAL, 1.0), (scenes.OP_GREATER, 0.0), (scenes.OP_GEQUAL, 0.0)):
+            s = scenes.soup_scene(164, 3000, 256, 192, 10.0, scenes.PROGRAM_FLAT_COLOR)
+            s.depth_op, s.depth_clear = op, clear
+            check(s, edge)
+        s.depth_write = False  # last-wins keys: 32-px tiles
+        check(s, 32)
+        check(scenes.soup_scene(165, 2000, 256, 192, 10.0, scenes.PROGRAM_TRIANGLE), 32)
+        check(scenes.cerberus_scene(640, 480), 32)
+        check(scenes.soup_scene(166, 3000, 320, 240, 10.0, scenes.PROGRAM_BLINN_PHONG), 32, shard=(1, 3))
+        check(scenes.soup_scene(66, 3000, 320, 240, 10.0, scenes.PROGRAM_BLINN_PHONG), edge)
+        for table in ("0", "1"):  # several 1024-entry segments per tile (the record table's reuse)
+            monkeypatch.setenv("ZR_REC_TABLE", table)
+            d2 = rhi.RenderDevice(0)
+            try:
+                assert_parity(d2, scenes.soup_scene(87, 40000, 96, 96, 5.0, scenes.PROGRAM_BLINN_PHONG))
+                assert d2.last_draw_stats()["tile_size"] == edge
+            finally:
+                d2.close()
+        monkeypatch.delenv("ZR_REC_TABLE")
+        check(crowded_tile_scene(), edge)
+        for _ in range(2):  # the shape measured: later draws take its slab / pool / jobs sizing
+            s = scenes.config_scene("c2", n=200_000)
+            gc, gd = renderer.render_scene(dev, s, frames=3)
+            oc, od = oracle.render(s, nthreads=16)
+            assert np.array_equal(gc, oc) and np.array_equal(gd.view(np.uint32), od.view(np.uint32))
+            assert dev.last_draw_stats()["tile_size"] == edge
+    finally:
+        dev.close()
+    monkeypatch.setenv("ZR_JOBS", "256")  # tile jobs (key buffers of the edge's pixels)
+    dev = rhi.RenderDevice(0)
+    try:
+        check_jobs = scenes.soup_scene(167, 20000, 160, 128, 10.0, scenes.PROGRAM_BLINN_PHONG)
+        for _ in range(2):
+            assert_parity(dev, check_jobs)
+            st = dev.last_draw_stats()
+            assert st["tile_size"] == edge and st["tile_jobs"] > 0, st
+    finally:
+        dev.close()
+    monkeypatch.delenv("ZR_JOBS")
+    monkeypatch.setenv("ZR_BIN_CAPACITY", "1024")  # the record-scan spill
+    dev = rhi.RenderDevice(0)
+    try:
+        assert_parity(dev, scenes.soup_scene(16, 3000, 640, 480, 40.0, scenes.PROGRAM_FLAT_COLOR))
+        st = dev.last_draw_stats()
+        assert st["overflowed_draws"] == 1 and st["tile_size"] == edge, st
+    finally:
+        dev.close()
+
+
 @pytest.mark.parametrize("fmt", [zr.FORMAT_R8G8B8A8_UNORM, zr.FORMAT_B8G8R8A8_UNORM, zr.FORMAT_R8G8B8A8_SRGB,
                                  zr.FORMAT_R32G32B32A32_SFLOAT])
 def test_color_formats(device, fmt):
@@ -475,10 +547,12 @@ def test_tile_row_shards(device, world):
 # ------------------------------------------------------- full benchmark sizes
 @pytest.mark.parametrize("cfg", ["c1", "c2"])
 def test_full_config_parity(device, cfg):
-    """C1 (100k tris) and C2 (1M tris) at 1920x1080, bit-exact vs the oracle."""
+    """C1 (100k tris) and C2 (1M tris) at 1920x1080, bit-exact vs the oracle (both
+    on 32-px tiles: tile_shift_for)."""
     s = scenes.config_scene(cfg)
     gc, gd = renderer.render_scene(device, s)
     st = device.last_draw_stats()
+    assert st["tile_size"] == 32, st
     oc, od, ost = oracle.render(s, nthreads=16, with_stats=True)
     assert np.array_equal(gc, oc)
     assert np.array_equal(gd.view(np.uint32), od.view(np.uint32))
@@ -488,18 +562,25 @@ def test_full_config_parity(device, cfg):
 def test_c3_4k_shards_union(device):
     """C3 geometry (1M tris, 3840x2160): the union of 8 shards rendered separately
     equals the oracle frame, colour and depth bits (the multi-GPU partition, on
-    one GPU; 1020 tiles per rank: 8 round-robin rows of 120 + a run of 60)."""
+    one GPU; 1020 tiles per rank: 8 round-robin rows of 120 + a run of 60; shards
+    bin 32-px tiles), and the unsharded frame, which tile_shift_for puts on 64-px
+    tiles (a 4K target with 122 primitives per 32-px tile)."""
     s = scenes.config_scene("c3")
     oc, od = oracle.render(s, nthreads=16)
     acc = np.zeros_like(oc)
     accd = np.full_like(od, np.nan)
     for r in range(8):
         gc, gd = renderer.render_scene(device, s, shard=(r, 8))
+        assert device.last_draw_stats()["tile_size"] == 32
         rows = owned(s, (r, 8))
         acc[rows] = gc[rows]
         accd[rows] = gd[rows]
     assert np.array_equal(acc, oc)
     assert np.array_equal(accd.view(np.uint32), od.view(np.uint32))
+    gc, gd = renderer.render_scene(device, s)
+    assert device.last_draw_stats()["tile_size"] == 64
+    assert np.array_equal(gc, oc)
+    assert np.array_equal(gd.view(np.uint32), od.view(np.uint32))
 
 
 def test_c4_micro_triangles(device):
@@ -509,6 +590,7 @@ def test_c4_micro_triangles(device):
     s = scenes.config_scene("c4")
     gc, gd = renderer.render_scene(device, s)
     assert device.last_draw_stats()["micro_fragments"] > 100_000
+    assert device.last_draw_stats()["tile_size"] == 64  # (>= 1 primitive per pixel: tile_shift_for)
     oc, od = oracle.render(s, nthreads=16)
     assert np.array_equal(gc, oc)
     assert np.array_equal(gd.view(np.uint32), od.view(np.uint32))

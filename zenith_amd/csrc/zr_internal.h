@@ -7,16 +7,14 @@
 
 namespace zr {
 
-// Screen-tile edge in pixels (one k_tile workgroup per tile).  A build choice of
-// 16, 32 or 64 (tools/build_variant.sh -DZR_TILE=...; docs/EXPERIMENTS.md round 6
-// has the A/B); zr_tile_size() reports it, and zenith_amd/shard.py reads it there.
-#ifndef ZR_TILE
-#define ZR_TILE 32
-#endif
-constexpr int kTile = ZR_TILE;
-static_assert(kTile == 16 || kTile == 32 || kTile == 64, "tile edge: 16, 32 or 64 pixels");
-constexpr int kTileShift = kTile == 16 ? 4 : kTile == 32 ? 5 : 6;
+// Screen tiles (one k_tile workgroup per tile) are 16, 32 or 64 pixels on a side,
+// chosen per draw (DrawParams::tile_shift, tile_shift_for below).
+// 32 is the default and the unit of tile-row shard ownership, of the row gather
+// and of k_clear; zr_tile_size() reports it and zenith_amd/shard.py reads it there.
+constexpr int kTile = 32;
+constexpr int kTileShift = 5;
 constexpr int kTilePixels = kTile * kTile;
+constexpr uint32_t kTileShiftMin = 4, kTileShiftMax = 6;
 constexpr int kTileThreads = 256;  // k_tile workgroup: 4 waves of 64 (512 for some passes: tile_threads_for)
 constexpr uint32_t kSortCap = 1024;     // tile-list segment sorted by area in LDS
 constexpr uint32_t kBigQueue = 512;     // k_tile: queued wave-path primitives per segment
@@ -114,12 +112,17 @@ constexpr uint32_t kMaxRunsPerTile = 256;  // k_tile keeps a tile's run table in
 struct alignas(8) BBox {
     uint32_t bb0, bb1;  // as TriRecord::bb0/bb1
 };
-// LDS histogram of the setup pass (64 KB; 128 KB with 16-px tiles, whose 4K
-// target has 32,400 tiles)
-constexpr uint32_t kMaxTilesPerPass = kTile == 16 ? 32768u : 16384u;
-constexpr uint32_t kJobTileBits = kTile == 16 ? 15u : 14u;  // tile_order item: tile | part << kJobTileBits (tiles < kMaxTilesPerPass)
+constexpr uint32_t kMaxTilesPerPass = 16384;  // LDS histogram of the setup pass (64 KB)
+constexpr uint32_t kJobTileBits = 14;          // tile_order item: tile | part << kJobTileBits (tiles < kMaxTilesPerPass)
 constexpr uint32_t kJobTileMask = (1u << kJobTileBits) - 1u;
 constexpr uint32_t kJobNone = 0xFFFFFFFFu;     // tile_order item of a spare block (job grids)
+// tile_order item flag: part 0 of a split tile, placed among the part blocks
+// (parts < 2^17: a list of at most 2^26 entries in jobs of at least 256)
+constexpr uint32_t kJobFront = 1u << 31;
+#ifndef ZR_JOBS_FRONT
+#define ZR_JOBS_FRONT 1
+#endif
+constexpr bool kJobsFront = ZR_JOBS_FRONT;  // every job of a split tile among the first blocks (A/B: 0)
 static_assert((1u << kJobTileBits) == kMaxTilesPerPass, "job items hold any tile index");
 constexpr uint32_t kMaxPushBytes = 128;       // ZR_MAX_PUSH_CONSTANTS_SIZE (Vulkan's guaranteed minimum)
 constexpr uint32_t kMaxPushWords = kMaxPushBytes / 4;
@@ -379,6 +382,12 @@ struct DrawParams {
     uint32_t* job_slot;              // [ntiles] first key buffer of a split tile (one per job)
     unsigned long long* job_keys;    // [job_slots][kTilePixels] key buffers
     uint32_t* job_tickets;           // [job_slots] per split tile, at its first buffer (zero between draws)
+    // log2 of the draw's tile edge (kTileShiftMin..kTileShiftMax; tile_shift_for):
+    // k_setup_bin bins and k_tile rasterizes tiles of 1 << tile_shift pixels a side
+    uint32_t tile_shift;
+    // k_tile's max-key test between a tile's segments (crowded lists; zr_runtime
+    // exec_draw): 1 for draws with tile jobs, ZR_HIZ forces it
+    uint32_t hiz;
     // push-constant state at the draw (zr_cmd_push_constants): the bytes ride in
     // the launch's kernel arguments, as Vulkan push constants ride in user SGPRs
     // (last, so the fields above keep their kernarg offsets; fields added later
@@ -415,12 +424,15 @@ constexpr uint32_t kSetupMiscWords = 96 + 8 * kSchedBuckets;
 // partitioned shard whose tiles fit one round of 512-thread workgroups (4 per CU)
 // takes 8 waves per tile -- C3 rank of 8 (1020 tiles), with the records-mode grid
 // below: 4.47x vs 4.12x at 4 waves -- and 4 waves only past one round.
-// Other tile edges have one workgroup size each: 64-px tiles (4096 pixels, 32 KiB
-// of keys) take 1024 threads, two workgroups per CU; 16-px tiles (256 pixels)
-// take 256.
-inline uint32_t tile_threads_for(uint32_t ntiles, uint32_t cus, uint64_t prims, bool partitioned) {
-    if (kTile == 64) return 1024u;
-    if (kTile == 16) return (uint32_t)kTileThreads;
+// 64-px tiles (4096 pixels, 32 KiB of keys) take 512 threads (4 workgroups per
+// CU), or 1024 (2 per CU, LDS for the record table) for draws of at least one
+// primitive per pixel -- round 6, 2 interleaved runs: C3 frame 230.2 us at 1024 vs
+// 208.8 at 512 (tile pass 180.9 vs 156.3), C4 317.6 vs 322.1; 16-px tiles (256
+// pixels) take 256.
+inline uint32_t tile_threads_for(uint32_t ntiles, uint32_t cus, uint64_t prims, bool partitioned,
+                                 uint32_t tile_shift = kTileShift) {
+    if (tile_shift == 6u) return prims >= ((uint64_t)ntiles << 12) ? 1024u : 512u;
+    if (tile_shift == 4u) return (uint32_t)kTileThreads;
     const uint32_t c = cus ? cus : 1u;
     const uint32_t per_cu = ntiles / c;
     if (partitioned) return ntiles > 4ull * c ? (uint32_t)kTileThreads : 512u;
@@ -496,8 +508,8 @@ inline uint32_t records_setup_wgs(uint64_t entries, uint32_t cus) {
 // per tile: 174.6 -> 181.8 us).
 // (Stated per pixel -- a quarter primitive per pixel -- so it carries over to
 // other tile edges.)
-inline bool use_record_table(uint64_t prims, uint32_t tiles_x, uint32_t tiles_y) {
-    return 4ull * prims >= (uint64_t)kTilePixels * tiles_x * tiles_y;
+inline bool use_record_table(uint64_t prims, uint32_t tiles_x, uint32_t tiles_y, uint32_t tile_shift = kTileShift) {
+    return 4ull * prims >= ((uint64_t)tiles_x * tiles_y << (2u * tile_shift));
 }
 
 // Whether k_setup_bin builds a heaviest-first tile schedule for k_tile
@@ -508,9 +520,48 @@ inline bool use_record_table(uint64_t prims, uint32_t tiles_x, uint32_t tiles_y)
 // uniform soups the order gains nothing and the schedule costs setup its ticket
 // (round 4, ZR_TILE_SCHED A/B, 2 runs: cerberus frame 53.8 -> 51.0 us; C2 108.4
 // -> 113.7, C3 238.9 -> 245.0, C1 and C4 equal within 0.5 %).
-inline bool use_tile_schedule(uint32_t ntiles, uint32_t cus, uint32_t tile_threads, uint64_t prims) {
+inline bool use_tile_schedule(uint32_t ntiles, uint32_t cus, uint32_t tile_threads, uint64_t prims,
+                              uint32_t tile_shift = kTileShift) {
     const uint64_t slots = (uint64_t)cus * (8u * kTileThreads / tile_threads);
-    return ntiles > slots && 32ull * prims < (uint64_t)ntiles * kTilePixels;  // (< 1/32 primitive per pixel)
+    return ntiles > slots && 32ull * prims < ((uint64_t)ntiles << (2u * tile_shift));  // (< 1/32 primitive per pixel)
+}
+
+// A measured draw shape is crowded when its longest list needed tile jobs and is
+// more than eight times its slab target (a skewed scene, not a dense uniform one:
+// c2x 29.7k vs 785; C4's longest list is within 10 % of its mean).
+inline bool crowded_shape(uint32_t max_tile, uint32_t target) {
+    return use_tile_jobs(max_tile) && (uint64_t)max_tile > 8ull * target;
+}
+
+// k_tile instances exist for 16- and 64-px tiles only for these (program, depth
+// mode) pairs (zr_kernels.hip launch_tile_pm); other draws keep 32-px tiles.
+constexpr bool tile_variant_built(int program, int depth_mode) {
+    return (program == kProgFlat || program == kProgBlinn) && depth_mode != kDepthLastWins;
+}
+
+// The tile edge of a draw (DrawParams::tile_shift), from the 16 / 32 / 64-px A/B of
+// round 6 (docs/EXPERIMENTS.md; 2 interleaved runs, frame time):
+//   - 64 px for a large target with a dense draw -- at least 4096 tiles of 32 px
+//     and 64 primitives per such tile (C3, 1M at 4K: 239.9 -> 229.6 us, its setup
+//     bins a quarter of the tiles: 59.3 -> 44.1 us, the tile pass equal) -- and for
+//     draws of at least one primitive per pixel (C4: 321.8 -> 316.8 us);
+//   - 16 px for a draw shape whose longest list needed tile jobs (a crowded
+//     region: the clustered c2x, 219.1 -> 166.8 us, its crowded tiles' lists and
+//     overdraw split four ways), when the target has at most kMaxTilesPerPass of
+//     them;
+//   - 32 px otherwise (C1 44.4 us vs 62.9 / 52.9 at 16 / 64, C2 108.9 vs 140.8 /
+//     120.8, cerberus 34.5 vs 61.9 / 60.8), and always for tile-row shards, whose
+//     ownership, row gather and exchange are in 32-px tiles (at 64 a C3 rank of 8
+//     has one tile per CU: slowest rank 58.7-63.0 vs 54.7-58.9 us).
+// `crowded`: the shape at the edge picked by size was measured and is skewed
+// (crowded_shape).
+inline uint32_t tile_shift_for(uint64_t prims, uint32_t width, uint32_t height, uint32_t shard_count, bool crowded) {
+    if (shard_count > 1) return kTileShift;
+    const uint64_t t32 = (uint64_t)((width + 31u) / 32u) * ((height + 31u) / 32u);
+    const uint64_t t16 = (uint64_t)((width + 15u) / 16u) * ((height + 15u) / 16u);
+    if (crowded) return t16 <= kMaxTilesPerPass ? 4u : kTileShift;
+    if ((t32 >= 4096u && prims >= 64u * t32) || prims >= (uint64_t)width * height) return 6u;
+    return kTileShift;
 }
 
 __host__ __device__ inline ShardGeom shard_geom(const DrawParams& P) {

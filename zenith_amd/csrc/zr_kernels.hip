@@ -583,8 +583,9 @@ __device__ __forceinline__ void for_owned_tiles(uint32_t G, uint32_t rank, uint3
 
 __device__ __forceinline__ uint32_t count_owned_box(const DrawParams& P, int px0, int py0, int px1, int py1,
                                                     uint32_t* s_hist) {
-    const int tx0 = px0 >> kTileShift, tx1 = px1 >> kTileShift;
-    const int ty0 = py0 >> kTileShift, ty1 = py1 >> kTileShift;
+    const uint32_t tsh = P.tile_shift;
+    const int tx0 = px0 >> tsh, tx1 = px1 >> tsh;
+    const int ty0 = py0 >> tsh, ty1 = py1 >> tsh;
     uint32_t owned = 0;
     for_owned_tiles(P.shard_count, P.shard_rank, P.tiles_x, P.full_rows, P.own_rows, P.left_lo, P.left_hi, tx0, ty0,
                     tx1, ty1, [&](uint32_t t, int, int) {
@@ -833,8 +834,9 @@ __device__ __forceinline__ BBox receive_entry(const DrawParams& P, const uint32_
 // dropped; the receiver reads count = min(total, capacity) and sees the overflow.
 __device__ __forceinline__ uint32_t dest_mask(const DrawParams& P, const PrimGeom& g) {
     const uint32_t G = P.shard_count;
-    const int ty0 = g.py0 >> kTileShift, ty1 = g.py1 >> kTileShift;
-    const int tx0 = g.px0 >> kTileShift, tx1 = g.px1 >> kTileShift;
+    const uint32_t tsh = P.tile_shift;  // (kTileShift: shards bin 32-px tiles)
+    const int ty0 = g.py0 >> tsh, ty1 = g.py1 >> tsh;
+    const int tx0 = g.px0 >> tsh, tx1 = g.px1 >> tsh;
     const uint32_t all = G >= 32u ? 0xFFFFFFFFu : (1u << G) - 1u;
     const int tyf = min(ty1, (int)P.full_rows - 1);  // round-robin rows: owner ty % G
     uint32_t m = 0;
@@ -972,10 +974,13 @@ __device__ void build_tile_schedule(const DrawParams& P, uint32_t nt, uint32_t* 
 // Tile jobs (DrawParams::job_entries), built by the same last workgroup.  A
 // tile whose list is longer than J (and takes no record scan) becomes
 // K = ceil(count / J) jobs, part p covering list entries [p J, (p + 1) J), with
-// K key buffers from job_slot[t].  Part 0 keeps the tile's block in the usual
-// order (blocks [job_pad, job_pad + nt)); parts 1.. take blocks of [0, job_pad)
-// spread like their tile (block b % 8 = the tile's XCD in that order, for L2
-// locality only); the blocks of [0, job_pad) left over get kJobNone.  When the
+// K key buffers from job_slot[t].  Every part takes a block of [0, job_pad), the
+// blocks dispatched first (round 6: part 0 kept the tile's own block in the usual
+// order and c2x's crowded tiles resolved late, their last jobs starting 92 us into
+// a 163-us pass), spread like its tile (block b % 8 = the tile's XCD in that
+// order, for L2 locality only); part 0's item carries kJobFront, and the tile's
+// own block (blocks [job_pad, job_pad + nt)) then exits after the block-level
+// duties; the blocks of [0, job_pad) left over get kJobNone.  When the
 // parts do not fit (an XCD's share of job_pad, or the key buffers) no tile is
 // split and the draw is counted (kCtJobsDenied) for the runtime to size them up.  k_tile derives K from the
 // same count and run word.
@@ -986,7 +991,7 @@ __device__ uint32_t tile_jobs(uint32_t count, uint32_t run_word, uint32_t J) {
 __device__ __noinline__ void build_job_schedule(const DrawParams& P, uint32_t nt, uint32_t* s_buf) {
     const uint32_t tid = threadIdx.x, J = P.job_entries, per_xcd = P.job_pad / 8u;
     uint32_t* s_cnt = s_buf;       // [8] parts per XCD, then their cursors
-    uint32_t* s_tot = s_buf + 8;   // [0] key buffers (jobs of split tiles), [1] buffer cursor, [2] denied
+    uint32_t* s_tot = s_buf + 8;   // [0] key buffers (jobs of split tiles), [1] buffer cursor, [2] denied, [3] split tiles
     if (tid < 16u) s_buf[tid] = 0u;
     __syncthreads();
     // pass 1: every tile's job count, parked in job_slot[t] (this thread reads it
@@ -1013,8 +1018,9 @@ __device__ __noinline__ void build_job_schedule(const DrawParams& P, uint32_t nt
             const uint32_t K = tile_jobs(c[k] & ~kCountRuns, w[k], J);
             P.job_slot[t] = K;
             if (K > 1u) {
-                atomicAdd(&s_cnt[xcd_block(t, nt) & 7u], K - 1u);
+                atomicAdd(&s_cnt[xcd_block(t, nt) & 7u], kJobsFront ? K : K - 1u);
                 atomicAdd(&s_tot[0], K);
+                atomicAdd(&s_tot[3], 1u);
             }
         }
     }
@@ -1037,11 +1043,10 @@ __device__ __noinline__ void build_job_schedule(const DrawParams& P, uint32_t nt
     __syncthreads();
     const bool ok = s_tot[2] == 0u;
     if (tid < 8u) {
-        const uint32_t extra = ok ? s_cnt[tid] : 0u;
-        s_cnt[16 + tid] = extra;  // (parts per XCD; s_cnt[0, 8) become the cursors)
+        s_cnt[16 + tid] = ok ? s_cnt[tid] : 0u;  // (parts per XCD; s_cnt[0, 8) become the cursors)
         s_cnt[tid] = 0u;
-        if (extra) atomicAdd(&P.counters[kCtJobs], extra);
     }
+    if (tid == 0 && ok && s_tot[0]) atomicAdd(&P.counters[kCtJobs], s_tot[0] - s_tot[3]);  // (jobs beyond one per tile)
     __syncthreads();
     // pass 2: key slots and part items (same thread -> tile mapping as pass 1)
     for (uint32_t t = tid; ok && t < nt; t += kSetupThreads) {
@@ -1049,8 +1054,10 @@ __device__ __noinline__ void build_job_schedule(const DrawParams& P, uint32_t nt
         if (K <= 1u) continue;
         const uint32_t x = xcd_block(t, nt) & 7u;
         P.job_slot[t] = atomicAdd(&s_tot[1], K);  // (K key buffers, one per job)
-        const uint32_t l0 = atomicAdd(&s_cnt[x], K - 1u);
-        for (uint32_t p = 1; p < K; ++p) P.tile_order[(l0 + p - 1u) * 8u + x] = t | (p << kJobTileBits);
+        const uint32_t p0 = kJobsFront ? 0u : 1u;
+        const uint32_t l0 = atomicAdd(&s_cnt[x], K - p0);
+        for (uint32_t p = p0; p < K; ++p)
+            P.tile_order[(l0 + p - p0) * 8u + x] = t | (p << kJobTileBits) | (p ? 0u : kJobFront);
     }
     for (uint32_t i = tid; i < P.job_pad; i += kSetupThreads)  // the spare part blocks
         if ((i >> 3) >= s_cnt[16 + (i & 7u)]) P.tile_order[i] = kJobNone;
@@ -1338,16 +1345,18 @@ __global__ __launch_bounds__(kSetupThreads) void k_setup_bin(DrawParams P) {
         uint32_t* const bins = P.bins;
         const uint32_t sG = P.shard_count, srank = P.shard_rank, tiles_x = P.tiles_x;
         const uint32_t full_rows = P.full_rows, own_rows = P.own_rows, left_lo = P.left_lo, left_hi = P.left_hi;
+        const uint32_t tsh = P.tile_shift;
+        const int tl = 1 << tsh;
         auto scatter = [&](uint32_t rec, const BBox bb) {
             if (bb.bb0 == kEmptyBox) return;
-            const int tx0 = (int)(bb.bb0 & 0xFFFFu) >> kTileShift, tx1 = (int)(bb.bb1 & 0xFFFFu) >> kTileShift;
-            const int ty0 = (int)(bb.bb0 >> 16) >> kTileShift, ty1 = (int)(bb.bb1 >> 16) >> kTileShift;
+            const int tx0 = (int)(bb.bb0 & 0xFFFFu) >> tsh, tx1 = (int)(bb.bb1 & 0xFFFFu) >> tsh;
+            const int ty0 = (int)(bb.bb0 >> 16) >> tsh, ty1 = (int)(bb.bb1 >> 16) >> tsh;
             for_owned_tiles(sG, srank, tiles_x, full_rows, own_rows, left_lo, left_hi, tx0, ty0, tx1, ty1,
                             [&](uint32_t t, int tx, int ty) {
-                const int cy0 = max((int)(bb.bb0 >> 16), ty << kTileShift);
-                const int cy1 = min((int)(bb.bb1 >> 16), (ty << kTileShift) + kTile - 1);
-                const int cx0 = max((int)(bb.bb0 & 0xFFFFu), tx << kTileShift);
-                const int cx1 = min((int)(bb.bb1 & 0xFFFFu), (tx << kTileShift) + kTile - 1);
+                const int cy0 = max((int)(bb.bb0 >> 16), ty << tsh);
+                const int cy1 = min((int)(bb.bb1 >> 16), (ty << tsh) + tl - 1);
+                const int cx0 = max((int)(bb.bb0 & 0xFFFFu), tx << tsh);
+                const int cx1 = min((int)(bb.bb1 & 0xFFFFu), (tx << tsh) + tl - 1);
                 // cost class: the lane walk's pair steps over bbox ∩ tile, ceil(w / 2)
                 // per row (sorting by steps instead of area: C3 tile pass -1 %, C2 -0.8 %)
                 const uint32_t steps = (uint32_t)(((cx1 - cx0 + 2) >> 1) * (cy1 - cy0 + 1));
@@ -1391,14 +1400,14 @@ __global__ __launch_bounds__(kSetupThreads) void k_setup_bin(DrawParams P) {
         }
         auto scatter_staged = [&](uint32_t rec, const BBox bb) {
             if (bb.bb0 == kEmptyBox) return;
-            const int tx0 = (int)(bb.bb0 & 0xFFFFu) >> kTileShift, tx1 = (int)(bb.bb1 & 0xFFFFu) >> kTileShift;
-            const int ty0 = (int)(bb.bb0 >> 16) >> kTileShift, ty1 = (int)(bb.bb1 >> 16) >> kTileShift;
+            const int tx0 = (int)(bb.bb0 & 0xFFFFu) >> tsh, tx1 = (int)(bb.bb1 & 0xFFFFu) >> tsh;
+            const int ty0 = (int)(bb.bb0 >> 16) >> tsh, ty1 = (int)(bb.bb1 >> 16) >> tsh;
             for_owned_tiles(sG, srank, tiles_x, full_rows, own_rows, left_lo, left_hi, tx0, ty0, tx1, ty1,
                             [&](uint32_t t, int tx, int ty) {
-                const int cy0 = max((int)(bb.bb0 >> 16), ty << kTileShift);
-                const int cy1 = min((int)(bb.bb1 >> 16), (ty << kTileShift) + kTile - 1);
-                const int cx0 = max((int)(bb.bb0 & 0xFFFFu), tx << kTileShift);
-                const int cx1 = min((int)(bb.bb1 & 0xFFFFu), (tx << kTileShift) + kTile - 1);
+                const int cy0 = max((int)(bb.bb0 >> 16), ty << tsh);
+                const int cy1 = min((int)(bb.bb1 >> 16), (ty << tsh) + tl - 1);
+                const int cx0 = max((int)(bb.bb0 & 0xFFFFu), tx << tsh);
+                const int cx1 = min((int)(bb.bb1 & 0xFFFFu), (tx << tsh) + tl - 1);
                 const uint32_t steps = (uint32_t)(((cx1 - cx0 + 2) >> 1) * (cy1 - cy0 + 1));
                 const uint32_t bucket = min((steps - 1u) >> 1, kSortBuckets - 1u);
                 const uint32_t l = atomicAdd(&s_lcur[t], 1u);
@@ -1535,10 +1544,12 @@ __device__ __forceinline__ TriRecord decode_large(const DrawParams& P, const int
 // kLaneStep - 1 columns on either side, must fit int32.  The edge functions are linear, so
 // their extremes are at the rectangle's corners: |w| <= |w(corner)| + |dy| 256 W
 // + |dx| 256 H, bounded in int64 against 2^31 - 1.
+template <int TS>
 __device__ __forceinline__ bool lane_walk_fits(const TriRecord& r, int x0, int y0) {
+    constexpr int T = 1 << TS;
     const int bx0 = max((int)(r.bb0 & 0xFFFFu), x0) - (kLaneStep - 1), by0 = max((int)(r.bb0 >> 16), y0);
-    const int bx1 = min((int)(r.bb1 & 0xFFFFu), x0 + kTile - 1) + (kLaneStep - 1);
-    const int by1 = min((int)(r.bb1 >> 16), y0 + kTile - 1);
+    const int bx1 = min((int)(r.bb1 & 0xFFFFu), x0 + T - 1) + (kLaneStep - 1);
+    const int by1 = min((int)(r.bb1 >> 16), y0 + T - 1);
     const long long Sx = (long long)bx0 * 256 + 128, Sy = (long long)by0 * 256 + 128;
     const long long Wd = (long long)(bx1 - bx0) * 256, Hd = (long long)max(by1 - by0, 0) * 256;
     auto edge = [&](int Xa, int Ya, int Xb, int Yb) {
@@ -1571,20 +1582,23 @@ __device__ __forceinline__ TriRecord load_uniform_record(const TriRecord* p) {
 
 
 // Row sweeps raster_prim makes over a record's bbox ∩ tile (kDebugStamps).
+template <int TS>
 __device__ __forceinline__ uint32_t prim_sweeps(const TriRecord& r, int x0, int y0) {
-    const int bw = min((int)(r.bb1 & 0xFFFFu), x0 + kTile - 1) - max((int)(r.bb0 & 0xFFFFu), x0) + 1;
-    const int bh = min((int)(r.bb1 >> 16), y0 + kTile - 1) - max((int)(r.bb0 >> 16), y0) + 1;
+    constexpr int T = 1 << TS;
+    const int bw = min((int)(r.bb1 & 0xFFFFu), x0 + T - 1) - max((int)(r.bb0 & 0xFFFFu), x0) + 1;
+    const int bh = min((int)(r.bb1 >> 16), y0 + T - 1) - max((int)(r.bb0 >> 16), y0) + 1;
     if (bw <= 0 || bh <= 0) return 0u;
     const int sh = bw <= 1 ? 0 : 32 - __clz(bw - 1);
     const int rows = 64 >> sh;
     return (uint32_t)((bh + rows - 1) / rows);
 }
 
-template <int MODE, bool INITD>
+template <int MODE, bool INITD, int TS>
 __device__ __forceinline__ void raster_prim(const DrawParams& P, const TriRecord& r, uint32_t seq, int x0, int y0,
                                             int lane, unsigned long long* s_key, const float* s_initd) {
+    constexpr int T = 1 << TS;
     const int bx0 = max((int)(r.bb0 & 0xFFFFu), x0), by0 = max((int)(r.bb0 >> 16), y0);
-    const int bx1 = min((int)(r.bb1 & 0xFFFFu), x0 + kTile - 1), by1 = min((int)(r.bb1 >> 16), y0 + kTile - 1);
+    const int bx1 = min((int)(r.bb1 & 0xFFFFu), x0 + T - 1), by1 = min((int)(r.bb1 >> 16), y0 + T - 1);
     const int bw = bx1 - bx0 + 1, bh = by1 - by0 + 1;
     if (bw <= 0 || bh <= 0) return;
     const int sh = bw <= 1 ? 0 : 32 - __clz(bw - 1);
@@ -1605,7 +1619,7 @@ __device__ __forceinline__ void raster_prim(const DrawParams& P, const TriRecord
         if (lx < bw && ly < bh && (w0 | w1 | w2) >= 0) {
             const float z = plane_z(dp, (float)w1, (float)w2);
             if (z >= dlo && z <= dhi) {
-                const int li = (by0 + ly - y0) * kTile + (bx0 + lx - x0);
+                const int li = (by0 + ly - y0) * T + (bx0 + lx - x0);
                 if (!INITD || depth_pass(P.depth_op, z, s_initd[li])) atomicMin(&s_key[li], frag_key<MODE>(z, seq));
             }
         }
@@ -1620,16 +1634,17 @@ __device__ __forceinline__ void raster_prim(const DrawParams& P, const TriRecord
 // incrementally in int32 (exact: |w| <= 2^29 inside a small primitive's bbox).
 // With k = 2^ksh lanes per primitive (sparse tiles), lane `sub` of the
 // primitive's group takes the bbox rows sub, sub + k, ...
-template <int MODE, bool INITD>
+template <int MODE, bool INITD, int TS>
 __device__ __forceinline__ void raster_lane(const DrawParams& P, const TriRecord& r, uint32_t seq, int x0, int y0,
                                             unsigned long long* s_key, const float* s_initd, int sub, int ksh) {
+    constexpr int T = 1 << TS;
     const int k = 1 << ksh;
     const int X0 = r.X0, Y0 = r.Y0, X1 = r.X1, Y1 = r.Y1, X2 = r.X2, Y2 = r.Y2;
     const float z0 = r.z0, dz1 = r.dz1, dz2 = r.dz2, invA2 = r.invA2;
     const uint32_t bb0 = r.bb0, bb1 = r.bb1, flags = r.flags;
     int bx0 = max((int)(bb0 & 0xFFFFu), x0);
     const int by0 = max((int)(bb0 >> 16), y0);
-    const int bx1 = min((int)(bb1 & 0xFFFFu), x0 + kTile - 1), by1 = min((int)(bb1 >> 16), y0 + kTile - 1);
+    const int bx1 = min((int)(bb1 & 0xFFFFu), x0 + T - 1), by1 = min((int)(bb1 >> 16), y0 + T - 1);
     int bw = bx1 - bx0 + 1;
     const int bh = by1 - by0 + 1;
     if (bw <= 0 || bh <= sub) return;
@@ -1682,8 +1697,8 @@ __device__ __forceinline__ void raster_lane(const DrawParams& P, const TriRecord
     const int rows = (bh - sub + k - 1) >> ksh;
     int w0 = wr((uint32_t)r0 - b0), w1 = wr((uint32_t)r1 - b1), w2 = wr((uint32_t)r2 - b2);
     int ex = 0;
-    uint32_t la = (uint32_t)(((by0 + sub - y0) * kTile + (bx0 - x0)) * 8);  // byte offset of the key
-    const uint32_t la_end = la + (uint32_t)(rows * k * kTile * 8);
+    uint32_t la = (uint32_t)(((by0 + sub - y0) * T + (bx0 - x0)) * 8);  // byte offset of the key
+    const uint32_t la_end = la + (uint32_t)(rows * k * T * 8);
     // The depth-range test (fragments outside [dlo, dhi] are discarded, §3) is
     // dropped from the loop when every lane's vertex depths lie inside the range
     // by a margin far above the interpolation's rounding (a few ulp of 1): then
@@ -1706,7 +1721,7 @@ __device__ __forceinline__ void raster_lane(const DrawParams& P, const TriRecord
     const int t0 = wr((uint32_t)S * sx0), t1 = wr((uint32_t)S * sx1), t2 = wr((uint32_t)S * sx2);
     const uint32_t kk = (uint32_t)k, hh = (uint32_t)S * (uint32_t)(hw - 1);
     const int q0 = wr(kk * sy0 - hh * sx0), q1 = wr(kk * sy1 - hh * sx1), q2 = wr(kk * sy2 - hh * sx2);
-    const uint32_t lq = (uint32_t)((k * kTile - S * (hw - 1)) * 8);
+    const uint32_t lq = (uint32_t)((k * T - S * (hw - 1)) * 8);
     auto sweep = [&](auto ztest, auto wchk) {
         do {
             int a0 = w0, a1 = w1, a2 = w2;
@@ -1739,6 +1754,14 @@ __device__ __forceinline__ void raster_lane(const DrawParams& P, const TriRecord
     else
         sweep(std::true_type{}, std::true_type{});
 }
+
+// The tile's max-key test (k_tile, DrawParams::hiz): depth-writing modes only; the
+// margin on a primitive's best vertex depth bounds the depth plane's rounding
+// (a few ulp of the depths' magnitude, which lie in [0, 1]) with room to spare.
+#ifndef ZR_HIZ_BUILD
+#define ZR_HIZ_BUILD 1
+#endif
+constexpr float kHizMargin = 1e-5f;
 
 // Visibility sequence of setup record e (API order): e + 1, or for the mesh
 // program 4p + k + 1 for fan k of primitive p (zr_internal.h kMeshFans).
@@ -1855,10 +1878,10 @@ constexpr uint32_t kRecHashSlots = 2048;
 constexpr uint32_t kRecTabProbes = 8;
 __device__ __forceinline__ uint32_t rec_hash(uint32_t rec) { return (rec * 0x9E3779B1u) >> 21; }  // 11 bits
 // Vertex 0 of a small primitive (extents <= 64 px) whose bbox meets the tile lies
-// within [-64 px, kTile + 64 px) of the tile origin: stored as u16 offsets (24.8
+// within [-64 px, tile edge + 64 px) of the tile origin: stored as u16 offsets (24.8
 // fixed point) from 64 px above-left of the origin.
 constexpr int kRelBias = 64 * 256;
-static_assert((kTile + 128) * 256 <= 65536, "tile-relative vertex 0 fits u16");
+static_assert((64 + 128) * 256 <= 65536, "tile-relative vertex 0 fits u16 (tiles up to 64 px)");
 
 __device__ __forceinline__ void rec_table_insert(uint32_t* s_thash, int4* s_trec, uint32_t rec, uint32_t j,
                                                  const int4 q0, const int4 q1, int x0, int y0) {
@@ -1900,11 +1923,12 @@ __device__ __forceinline__ bool rec_table_find(const uint32_t* s_thash, const in
 // thread in two batches; C1 49 vs 44 us, C3 223 vs 204 us).  A wave with no
 // winner skips the gathers; other pixels without a winner load the wave's first
 // winner (in-bounds addresses) and discard it.
-template <int PROG, int MODE, bool IDX32, int NT, bool TAB>
+template <int PROG, int MODE, bool IDX32, int NT, bool TAB, int TS>
 __device__ __forceinline__ void resolve_pixels(const DrawParams& P, int x0, int y0, const unsigned long long* s_key,
                                                const float* s_srgb, const uint32_t* s_thash, const int4* s_trec,
                                                const uint32_t* s_sorted) {
-    constexpr int kPer = kTilePixels / NT;
+    constexpr int T = 1 << TS, TP = T * T;
+    constexpr int kPer = TP / NT;
     constexpr int kB = kPer < (int)kResolveBatch ? kPer : (int)kResolveBatch;
     // recomputed here, not reused from the tile's init: a pixel coordinate kept
     // live across the raster loop spills at 64 VGPRs
@@ -1920,8 +1944,8 @@ __device__ __forceinline__ void resolve_pixels(const DrawParams& P, int x0, int 
 #pragma unroll
         for (int b = 0; b < kB; ++b) {
             const int i = tid + (k0 + b) * NT;
-            px[b] = x0 + (i & (kTile - 1));
-            py[b] = y0 + (i >> kTileShift);
+            px[b] = x0 + (i & (T - 1));
+            py[b] = y0 + (i >> TS);
             inside[b] = !(px[b] < P.ra_x0 || px[b] > P.ra_x1 || py[b] < P.ra_y0 || py[b] > P.ra_y1);
             key[b] = s_key[i];
             const uint32_t seq = inside[b] ? winner_seq<MODE>(key[b]) : 0u;
@@ -2044,11 +2068,12 @@ struct WinLayout {
     static constexpr int kWords = (kAttrOff + kAttrW + 3) & ~3;
 };
 
-// Resolve hash table: kWinSlots setup-record ids (kWinEmpty = free), then the
-// dense winner list (kWinSlots record ids); both live where the keys were.
-constexpr uint32_t kWinSlots = kTilePixels;
+// Resolve hash table: TP setup-record ids (kWinEmpty = free), then the
+// dense winner list (TP record ids); both live where the keys were.
+// (TP = the tile's pixels, 1 << 2 TS)
 constexpr uint32_t kWinEmpty = 0xFFFFFFFFu;
-__device__ __forceinline__ uint32_t win_hash(uint32_t rec) { return (rec * 0x9E3779B1u) >> (32 - 2 * kTileShift); }  // log2(kWinSlots) bits
+template <int TS>
+__device__ __forceinline__ uint32_t win_hash(uint32_t rec) { return (rec * 0x9E3779B1u) >> (32 - 2 * TS); }  // log2(TP) bits
 
 __device__ __forceinline__ void copy3(float* dst, const float* src) {
     dst[0] = src[0]; dst[1] = src[1]; dst[2] = src[2];
@@ -2199,19 +2224,20 @@ __device__ __forceinline__ void shade_from_lds(const DrawParams& P, const float*
 //      whose winner is in the batch shades from LDS and stores its colour
 // Three barriers in all.  s_u: the dense-id map (u16 per slot), then (kPer > 2)
 // each pixel's dense id (u16), then the per-winner words (cap * kWords floats).
-template <int PROG, int MODE, bool IDX32, int NT>
+template <int PROG, int MODE, bool IDX32, int NT, int TS>
 __device__ __forceinline__ void resolve_tile(const DrawParams& P, int x0, int y0, unsigned long long* s_key,
                                              uint32_t* s_u, uint32_t u_words, uint32_t* s_nwin,
                                              const float* s_srgb, unsigned long long* ts = nullptr) {
+    constexpr int T = 1 << TS, TP = T * T;
     using L = WinLayout<PROG, MODE>;
-    constexpr int kPer = kTilePixels / NT;
+    constexpr int kPer = TP / NT;
     constexpr bool kPixLds = kPer > 2;  // per-pixel ids in LDS (registers at 512 threads)
-    uint32_t* s_list = reinterpret_cast<uint32_t*>(s_key);              // [kWinSlots] over keys 0..511
-    uint32_t* s_tab = s_list + kWinSlots;                               // [kWinSlots] over keys 512..1023
-    uint16_t* s_dmap = reinterpret_cast<uint16_t*>(s_u);                // [kWinSlots]
-    uint32_t* s_pix = s_tab;  // [kTilePixels] (kPixLds): the table is free once every dense id is known
-    float* s_win = reinterpret_cast<float*>(s_u + kWinSlots / 2u);
-    const uint32_t cap = min((u_words - kWinSlots / 2u) / (uint32_t)L::kWords, kWinSlots);
+    uint32_t* s_list = reinterpret_cast<uint32_t*>(s_key);              // [TP] over keys 0..511
+    uint32_t* s_tab = s_list + TP;                               // [TP] over keys 512..1023
+    uint16_t* s_dmap = reinterpret_cast<uint16_t*>(s_u);                // [TP]
+    uint32_t* s_pix = s_tab;  // [TP] (kPixLds): the table is free once every dense id is known
+    float* s_win = reinterpret_cast<float*>(s_u + TP / 2u);
+    const uint32_t cap = min((u_words - TP / 2u) / (uint32_t)L::kWords, TP);
     // recomputed here, not reused from the tile's init: a pixel coordinate kept
     // live across the raster loop spills at 64 VGPRs
     int tid = (int)threadIdx.x;
@@ -2220,12 +2246,12 @@ __device__ __forceinline__ void resolve_tile(const DrawParams& P, int x0, int y0
 #pragma unroll
     for (int k = 0; k < kPer; ++k) {
         const int i = tid + k * NT;
-        const int px = x0 + (i & (kTile - 1)), py = y0 + (i >> kTileShift);
+        const int px = x0 + (i & (T - 1)), py = y0 + (i >> TS);
         const bool inside = !(px < P.ra_x0 || px > P.ra_x1 || py < P.ra_y0 || py > P.ra_y1);
         const unsigned long long key = s_key[i];
-        if (i >= (int)(kTilePixels / 2)) {  // this key's bytes hold hash slots 2(i - 512) and 2(i - 512) + 1
-            s_tab[2 * (i - kTilePixels / 2)] = kWinEmpty;
-            s_tab[2 * (i - kTilePixels / 2) + 1] = kWinEmpty;
+        if (i >= (int)(TP / 2)) {  // this key's bytes hold hash slots 2(i - 512) and 2(i - 512) + 1
+            s_tab[2 * (i - TP / 2)] = kWinEmpty;
+            s_tab[2 * (i - TP / 2) + 1] = kWinEmpty;
         }
         const uint32_t seq = inside ? winner_seq<MODE>(key) : 0u;
         rec[k] = seq ? seq_record<PROG>(P, seq - 1u) : kWinEmpty;
@@ -2250,13 +2276,13 @@ __device__ __forceinline__ void resolve_tile(const DrawParams& P, int x0, int y0
 #pragma unroll
     for (int k = 0; k < kPer; ++k) {
         bool fresh = false;
-        uint32_t h = win_hash(rec[k]);
+        uint32_t h = win_hash<TS>(rec[k]);
         if (rec[k] != kWinEmpty) {
-            for (;;) {  // linear probing; at most kTilePixels distinct records, so it ends
+            for (;;) {  // linear probing; at most TP distinct records, so it ends
                 const uint32_t old = atomicCAS(&s_tab[h], kWinEmpty, rec[k]);
                 if (old == kWinEmpty) { fresh = true; break; }
                 if (old == rec[k]) break;
-                h = (h + 1u) & (kWinSlots - 1u);
+                h = (h + 1u) & (TP - 1u);
             }
         }
         hs[k] = h;
@@ -2300,7 +2326,7 @@ __device__ __forceinline__ void resolve_tile(const DrawParams& P, int x0, int y0
             const uint32_t j = dk - base;
             if (dk == kWinEmpty || j >= nb) return;
             const int i = tid + k * NT;
-            const int px = x0 + (i & (kTile - 1)), py = y0 + (i >> kTileShift);
+            const int px = x0 + (i & (T - 1)), py = y0 + (i >> TS);
             float col[4] = {0.f, 0.f, 0.f, 0.f};
             float zw = 0.0f;
             if (!(tile_debug(P) & kDebugSkipShade))
@@ -2321,10 +2347,11 @@ __device__ __forceinline__ void resolve_tile(const DrawParams& P, int x0, int y0
 // NT threads per tile: 256 when the pass has several tiles per CU, 512 when it
 // has few (tile-row shards, small attachments), so a tile's primitives spread
 // over more waves (P.tile_threads, tile_threads_for).
-template <int PROG, int MODE, bool INITD, int NT>
+template <int PROG, int MODE, bool INITD, int NT, int TS>
 // (launch bounds: the second argument is the minimum waves per SIMD -- 8, i.e.
 // 64 VGPRs, for both sizes; 8 x 256 or 4 x 512 threads per CU)
 __global__ __launch_bounds__(NT, kTileWgs * kTileThreads / 256) void k_tile(DrawParams P) {
+    constexpr int T = 1 << TS, TP = T * T;
     // LDS: a workgroup's share of the CU's 160 KiB at the occupancy the launch
     // bounds ask for (8 x 256 or 4 x 512 threads: 20 or 40 KiB).  The keys (8 KiB)
     // become the resolve's hash table; one union holds the raster scratch (sorted
@@ -2333,27 +2360,32 @@ __global__ __launch_bounds__(NT, kTileWgs * kTileThreads / 256) void k_tile(Draw
     constexpr uint32_t kWgsPerCu = kTileWgs * (uint32_t)kTileThreads / (uint32_t)NT;
     constexpr uint32_t kBudget = 160u * 1024u / kWgsPerCu;
     constexpr uint32_t kMiscWords = 16;
-    constexpr uint32_t kUnionWords = (kBudget - kTilePixels * 8u - 256u * 4u - kMiscWords * 4u) / 4u;
-    static_assert(kSortCap + kBigQueue + kSortBuckets + (INITD ? kTilePixels : 0u) +
-                          ((NT >= 512 && MODE != kDepthLastWins && PROG != kProgMesh && !INITD)
+    constexpr uint32_t kWaves = (uint32_t)NT / 64u;
+    constexpr uint32_t kUnionWords = (kBudget - TP * 8u - 256u * 4u - kMiscWords * 4u - kWaves * 8u) / 4u;
+    static_assert(kSortCap + kBigQueue + kSortBuckets + (INITD ? TP : 0u) +
+                          ((NT >= 512 && MODE != kDepthLastWins && PROG != kProgMesh && !INITD && (TS <= 5 || NT >= 1024))
                                ? 4u * kSortCap + kRecHashSlots
                                : 0u) <=
                       kUnionWords,
                   "k_tile raster scratch exceeds the workgroup's LDS share");
-    __shared__ unsigned long long s_key[kTilePixels];
+    __shared__ unsigned long long s_key[TP];
     __shared__ float s_srgb[256];
     __shared__ __attribute__((aligned(16))) uint32_t s_u[kUnionWords];
     __shared__ uint32_t s_misc[kMiscWords];
+    __shared__ unsigned long long s_wmax[kWaves];  // per wave: the worst key of its pixels (the tile's max-key test)
     uint32_t* s_sorted = s_u;                       // [kSortCap]
     // wave-path (large) primitives of the segment, rasterized after its
     // chunks by whichever wave claims them next: the area sort groups them, so the
     // wave owning their chunk would otherwise sweep them all alone
     uint32_t* s_big = s_u + kSortCap;               // [kBigQueue]
     uint32_t* s_bucket = s_big + kBigQueue;         // [kSortBuckets]
-    float* s_initd = reinterpret_cast<float*>(s_bucket + kSortBuckets);  // [kTilePixels] (INITD)
+    float* s_initd = reinterpret_cast<float*>(s_bucket + kSortBuckets);  // [TP] (INITD)
     // 512-thread tiles: the record table of the resolve (rec_table_insert); last-wins
     // modes need the records' depth terms, which it does not hold
-    constexpr bool kTab = ZR_TAB && !ZR_RESOLVE_DEDUP512 && NT >= 512 && MODE != kDepthLastWins && PROG != kProgMesh && !INITD;
+    // (64-px tiles: only 1024-thread workgroups have the LDS for it beside 32 KiB of keys)
+    constexpr bool kHiz = ZR_HIZ_BUILD && MODE != kDepthLastWins && !INITD;
+    constexpr bool kTab = ZR_TAB && !ZR_RESOLVE_DEDUP512 && NT >= 512 && MODE != kDepthLastWins && PROG != kProgMesh &&
+                          !INITD && (TS <= 5 || NT >= 1024);
     int4* s_trec = reinterpret_cast<int4*>(s_bucket + kSortBuckets);        // [kSortCap]
     uint32_t* s_thash = reinterpret_cast<uint32_t*>(s_trec + kSortCap);      // [kRecHashSlots]
     uint32_t& s_claim = s_misc[0];   // next 64-entry chunk of the segment to rasterize
@@ -2369,10 +2401,11 @@ __global__ __launch_bounds__(NT, kTileWgs * kTileThreads / 256) void k_tile(Draw
                                                                                    : blockIdx.x;
     const uint32_t item = (b < jp || P.tile_sched) ? P.tile_order[b] : xcd_tile(b - jp, P.ntiles);
     if (item == kJobNone) return;
-    const uint32_t t = item & kJobTileMask, part = item >> kJobTileBits;
+    const bool front = (item & kJobFront) != 0u;  // part 0 of a split tile among the part blocks
+    const uint32_t t = item & kJobTileMask, part = (item & ~kJobFront) >> kJobTileBits;
     uint32_t tx, ty;
     shard_tile_xy(shard_geom(P), t, tx, ty);
-    const int x0 = (int)tx * kTile, y0 = (int)ty * kTile;
+    const int x0 = (int)tx * T, y0 = (int)ty * T;
     const bool stamp = (tile_debug(P) & kDebugStamps) && threadIdx.x == 0 && t < kMaxTilesPerPass;
     unsigned long long* ts = P.dbg_ts + 8192 * 8 + (size_t)t * 8;
     if (stamp) ts[0] = __builtin_amdgcn_s_memrealtime();
@@ -2462,8 +2495,8 @@ __global__ __launch_bounds__(NT, kTileWgs * kTileThreads / 256) void k_tile(Draw
     // rasterized exactly but slowly: it scans every record's bbox (k_setup_bin
     // stored them all) instead.  Only a tile with kCountRuns reads its run word.
 
-    for (int i = threadIdx.x; i < kTilePixels; i += NT) {
-        const int px = x0 + (i & (kTile - 1)), py = y0 + (i >> kTileShift);
+    for (int i = threadIdx.x; i < TP; i += NT) {
+        const int px = x0 + (i & (T - 1)), py = y0 + (i >> TS);
         float d = P.clear_depth;
         if (P.load_depth && px < (int)P.fb_w && py < (int)P.fb_h) d = P.depth[(size_t)py * P.fb_w + px];
         s_key[i] = init_key<MODE>(d);
@@ -2535,6 +2568,8 @@ __global__ __launch_bounds__(NT, kTileWgs * kTileThreads / 256) void k_tile(Draw
     if (threadIdx.x == 0 && K == 1u) P.tile_counts[t] = 0u;  // (a split tile: its resolving job)
     if (blockIdx.x == jp)
         for (uint32_t i = threadIdx.x; i < kCtWords; i += NT) P.counters[i] = 0u;
+    // a split tile's own block: its part 0 runs among the part blocks (build_job_schedule)
+    if (kJobsFront && K > 1u && part == 0u && !front) return;
 
     const uint32_t wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
     const int lane = threadIdx.x & 63;
@@ -2545,8 +2580,24 @@ __global__ __launch_bounds__(NT, kTileWgs * kTileThreads / 256) void k_tile(Draw
         // so that a 64-lane chunk holds primitives of similar cost (the lane loop runs
         // as long as its largest member).  Then each wave takes every 4th chunk: one
         // lane per entry loads the 64-B record, and the wave walks the chunk.
+        bool hiz_on = false;  // s_wmax holds the keys of the segments so far (kHiz)
         for (uint32_t seg = seg_lo; seg < cnt; seg += kSortCap) {
             const uint32_t n = min(kSortCap, cnt - seg);
+            // The tile's max-key test (crowded lists, DrawParams::hiz): after a segment, the
+            // worst (largest) key of any pixel of the tile; a primitive whose every
+            // fragment's key would exceed it -- its best vertex depth, less a margin
+            // far above the depth plane's rounding, is strictly worse than that pixel
+            // depth -- cannot win a pixel and is skipped before its walk.  Ties are not
+            // skipped (the sequence decides them), nor is anything in last-wins modes.
+            // (the depth half of the key decides: a bound key's sequence half is 0;
+            // wave-uniform, in an SGPR)
+            uint32_t kmax_hi = ~0u;
+            if (kHiz && hiz_on) {
+                uint32_t m = 0;
+#pragma unroll
+                for (uint32_t w = 0; w < kWaves; ++w) m = max(m, (uint32_t)(s_wmax[w] >> 32));
+                kmax_hi = (uint32_t)__builtin_amdgcn_readfirstlane((int)m);
+            }
             // a list with pool runs loads its segments past the slab part through
             // the run table (s_misc[9]: runs, s_misc[8]: the slab part's length)
             const uint32_t nr = (uint32_t)__builtin_amdgcn_readfirstlane((int)s_misc[9]);
@@ -2641,7 +2692,14 @@ __global__ __launch_bounds__(NT, kTileWgs * kTileThreads / 256) void k_tile(Draw
                     q0 = rp[0];
                     q1 = rp[1];
                 }
-                const bool valid = j < n && !(tile_debug(P) & kDebugLoadOnly);
+                bool valid = j < n && !(tile_debug(P) & kDebugLoadOnly);
+                if (kHiz && kmax_hi != ~0u && valid) {
+                    const float z0 = __int_as_float(q1.x), z1 = z0 + __int_as_float(q1.y), z2 = z0 + __int_as_float(q1.z);
+                    const bool lt = MODE == kDepthMinStrict || MODE == kDepthMinNonStrict;
+                    const float zb = lt ? fmaxf(fminf(z0, fminf(z1, z2)) - kHizMargin, 0.0f)
+                                        : fmaxf(z0, fmaxf(z1, z2)) + kHizMargin;
+                    valid = (uint32_t)(frag_key<MODE>(zb, 0u) >> 32) <= kmax_hi;
+                }
                 if (tile_debug(P) & kDebugLoadOnly) asm volatile("" ::"v"(q0.x), "v"(q1.x), "v"(my_prim));
                 const bool large = compact_is_large(q0);
                 // A large primitive below the last cost bucket (bbox ∩ tile under ~253
@@ -2658,7 +2716,7 @@ __global__ __launch_bounds__(NT, kTileWgs * kTileThreads / 256) void k_tile(Draw
                     const int2* vp = reinterpret_cast<const int2*>(P.records_big + my_prim) + 1;
                     v1 = vp[0];
                     v2 = vp[1];
-                    walk = lane_walk_fits(decode_large(P, q0, q1, true, v1, v2), x0, y0);
+                    walk = lane_walk_fits<TS>(decode_large(P, q0, q1, true, v1, v2), x0, y0);
                 }
                 if (tab && valid && sub == 0) {
                     if (!large) {
@@ -2673,14 +2731,14 @@ __global__ __launch_bounds__(NT, kTileWgs * kTileThreads / 256) void k_tile(Draw
                     }
                 }
                 if (walk && !(tile_debug(P) & kDebugSkipLanePath))
-                    raster_lane<MODE, INITD>(P, decode_large(P, q0, q1, large, v1, v2), entry_seq<PROG>(P, my_prim), x0, y0,
+                    raster_lane<MODE, INITD, TS>(P, decode_large(P, q0, q1, large, v1, v2), entry_seq<PROG>(P, my_prim), x0, y0,
                                              s_key, s_initd, sub, (int)ksh);
                 if (ZR_TILE_WORK_STATS && (tile_debug(P) & kDebugStamps)) {  // work of the chunk: its longest lane walk
                     int steps = 0;
                     if (valid && !large) {
                         const TriRecord r = decode_compact(P, q0, q1, true);
-                        const int bw = min((int)(r.bb1 & 0xFFFFu), x0 + kTile - 1) - max((int)(r.bb0 & 0xFFFFu), x0) + 1;
-                        const int bh = min((int)(r.bb1 >> 16), y0 + kTile - 1) - max((int)(r.bb0 >> 16), y0) + 1;
+                        const int bw = min((int)(r.bb1 & 0xFFFFu), x0 + T - 1) - max((int)(r.bb0 & 0xFFFFu), x0) + 1;
+                        const int bh = min((int)(r.bb1 >> 16), y0 + T - 1) - max((int)(r.bb0 >> 16), y0) + 1;
                         steps = (bw > 0 && bh > sub) ? bw * ((bh - sub + (1 << ksh) - 1) >> ksh) : 0;
                     }
 #pragma unroll
@@ -2710,8 +2768,8 @@ __global__ __launch_bounds__(NT, kTileWgs * kTileThreads / 256) void k_tile(Draw
                     big &= big - 1ull;
                     const uint32_t prim = (uint32_t)rl((int)my_prim, i);
                     const TriRecord r = load_uniform_record(P.records_big + prim);
-                    raster_prim<MODE, INITD>(P, r, entry_seq<PROG>(P, prim), x0, y0, lane, s_key, s_initd);
-                    if (ZR_TILE_WORK_STATS && (tile_debug(P) & kDebugStamps) && lane == 0) atomicAdd(&s_dbg[1], prim_sweeps(r, x0, y0));
+                    raster_prim<MODE, INITD, TS>(P, r, entry_seq<PROG>(P, prim), x0, y0, lane, s_key, s_initd);
+                    if (ZR_TILE_WORK_STATS && (tile_debug(P) & kDebugStamps) && lane == 0) atomicAdd(&s_dbg[1], prim_sweeps<TS>(r, x0, y0));
                 }
             }
             __syncthreads();
@@ -2737,8 +2795,16 @@ __global__ __launch_bounds__(NT, kTileWgs * kTileThreads / 256) void k_tile(Draw
                 const int4 b0 = b[0], b1 = b[1], b2 = b[2], b3 = b[3];
                 const TriRecord ra = uniform_record(a0, a1, a2, a3);
                 const TriRecord rb = uniform_record(b0, b1, b2, b3);
-                raster_prim<MODE, INITD>(P, ra, entry_seq<PROG>(P, e0), x0, y0, lane, s_key, s_initd);
-                if (two) raster_prim<MODE, INITD>(P, rb, entry_seq<PROG>(P, e1), x0, y0, lane, s_key, s_initd);
+                raster_prim<MODE, INITD, TS>(P, ra, entry_seq<PROG>(P, e0), x0, y0, lane, s_key, s_initd);
+                if (two) raster_prim<MODE, INITD, TS>(P, rb, entry_seq<PROG>(P, e1), x0, y0, lane, s_key, s_initd);
+            }
+            if (kHiz && P.hiz && seg + kSortCap < cnt) {  // another segment follows: the tile's worst key so far
+                unsigned long long m = 0;
+                for (int i = threadIdx.x; i < TP; i += NT) m = max(m, s_key[i]);
+#pragma unroll
+                for (int o = 32; o > 0; o >>= 1) m = max(m, (unsigned long long)__shfl_xor((long long)m, o, 64));
+                if (lane == 0) s_wmax[wave] = m;
+                hiz_on = true;
             }
             __syncthreads();
         }
@@ -2751,8 +2817,8 @@ __global__ __launch_bounds__(NT, kTileWgs * kTileThreads / 256) void k_tile(Draw
                 int4 q0 = make_int4(0, 0, 0, 0), q1 = q0;
                 if (j < n_rec) {
                     const BBox bb = P.bboxes[j];
-                    hit = bb.bb0 != kEmptyBox && (int)(bb.bb0 & 0xFFFFu) < x0 + kTile && (int)(bb.bb1 & 0xFFFFu) >= x0 &&
-                          (int)(bb.bb0 >> 16) < y0 + kTile && (int)(bb.bb1 >> 16) >= y0;
+                    hit = bb.bb0 != kEmptyBox && (int)(bb.bb0 & 0xFFFFu) < x0 + T && (int)(bb.bb1 & 0xFFFFu) >= x0 &&
+                          (int)(bb.bb0 >> 16) < y0 + T && (int)(bb.bb1 >> 16) >= y0;
                 }
                 uint32_t rec = j;  // bboxes by position; records by draw primitive (records mode: gids)
                 if (hit) {
@@ -2763,14 +2829,14 @@ __global__ __launch_bounds__(NT, kTileWgs * kTileThreads / 256) void k_tile(Draw
                 }
                 const bool large = compact_is_large(q0);
                 if (hit && !large)
-                    raster_lane<MODE, INITD>(P, decode_compact(P, q0, q1, true), entry_seq<PROG>(P, rec), x0, y0, s_key,
+                    raster_lane<MODE, INITD, TS>(P, decode_compact(P, q0, q1, true), entry_seq<PROG>(P, rec), x0, y0, s_key,
                                              s_initd, 0, 0);
                 unsigned long long big = __ballot(hit && large);
                 while (big) {
                     const uint32_t i = (uint32_t)__builtin_ctzll(big);
                     big &= big - 1ull;
                     const uint32_t prim = (uint32_t)rl((int)rec, i);
-                    raster_prim<MODE, INITD>(P, load_uniform_record(P.records_big + prim), entry_seq<PROG>(P, prim), x0, y0, lane,
+                    raster_prim<MODE, INITD, TS>(P, load_uniform_record(P.records_big + prim), entry_seq<PROG>(P, prim), x0, y0, lane,
                                              s_key, s_initd);
                 }
             }
@@ -2787,10 +2853,10 @@ __global__ __launch_bounds__(NT, kTileWgs * kTileThreads / 256) void k_tile(Draw
     if ((uint32_t)__builtin_amdgcn_readfirstlane((int)s_misc[10]) > 1u) {
         const uint32_t Kj = (uint32_t)__builtin_amdgcn_readfirstlane((int)s_misc[10]);
         const uint32_t buf0 = (uint32_t)__builtin_amdgcn_readfirstlane((int)s_misc[11]);
-        unsigned long long* mine = P.job_keys + (size_t)(buf0 + part) * kTilePixels;
+        unsigned long long* mine = P.job_keys + (size_t)(buf0 + part) * TP;
         int i0 = threadIdx.x;  // (opaque: the key addresses of the init loop, held across the pass, spilled)
         asm volatile("" : "+v"(i0));
-        for (int i = i0; i < kTilePixels; i += NT)
+        for (int i = i0; i < TP; i += NT)
             __hip_atomic_store(&mine[i], s_key[i], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
         asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // (each thread's stores done before the ticket)
         __syncthreads();
@@ -2800,8 +2866,8 @@ __global__ __launch_bounds__(NT, kTileWgs * kTileThreads / 256) void k_tile(Draw
         if ((uint32_t)__builtin_amdgcn_readfirstlane((int)s_misc[12]) != Kj - 1u) return;
         // (eight buffers' loads in flight per pixel: one buffer at a time, the fold
         // of a 15-job tile was ~15 memory round trips on the pass's critical path)
-        const unsigned long long* keys0 = P.job_keys + (size_t)buf0 * kTilePixels;
-        for (int i = i0; i < kTilePixels; i += NT) {
+        const unsigned long long* keys0 = P.job_keys + (size_t)buf0 * TP;
+        for (int i = i0; i < TP; i += NT) {
             unsigned long long m = s_key[i];
             for (uint32_t j0 = 0; j0 < Kj; j0 += 8u) {
                 unsigned long long v[8];
@@ -2809,7 +2875,7 @@ __global__ __launch_bounds__(NT, kTileWgs * kTileThreads / 256) void k_tile(Draw
                 for (uint32_t k = 0; k < 8u; ++k) {
                     const uint32_t j = j0 + k;
                     v[k] = (j < Kj && j != part)
-                               ? __hip_atomic_load(&keys0[(size_t)j * kTilePixels + i], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT)
+                               ? __hip_atomic_load(&keys0[(size_t)j * TP + i], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT)
                                : ~0ull;
                 }
 #pragma unroll
@@ -2829,14 +2895,14 @@ __global__ __launch_bounds__(NT, kTileWgs * kTileThreads / 256) void k_tile(Draw
     // index loads are issued back to back).
     if constexpr (NT >= 512 && !ZR_RESOLVE_DEDUP512) {
         if (P.index_size == 4)
-            resolve_pixels<PROG, MODE, true, NT, kTab>(kernarg_params(), x0, y0, s_key, s_srgb, s_thash, s_trec, s_sorted);
+            resolve_pixels<PROG, MODE, true, NT, kTab, TS>(kernarg_params(), x0, y0, s_key, s_srgb, s_thash, s_trec, s_sorted);
         else
-            resolve_pixels<PROG, MODE, false, NT, kTab>(kernarg_params(), x0, y0, s_key, s_srgb, s_thash, s_trec, s_sorted);
+            resolve_pixels<PROG, MODE, false, NT, kTab, TS>(kernarg_params(), x0, y0, s_key, s_srgb, s_thash, s_trec, s_sorted);
     } else if (P.index_size == 4) {
-        resolve_tile<PROG, MODE, true, NT>(kernarg_params(), x0, y0, s_key, s_u, kUnionWords, s_nwin, s_srgb,
+        resolve_tile<PROG, MODE, true, NT, TS>(kernarg_params(), x0, y0, s_key, s_u, kUnionWords, s_nwin, s_srgb,
                                           stamp ? ts : nullptr);
     } else {
-        resolve_tile<PROG, MODE, false, NT>(kernarg_params(), x0, y0, s_key, s_u, kUnionWords, s_nwin, s_srgb,
+        resolve_tile<PROG, MODE, false, NT, TS>(kernarg_params(), x0, y0, s_key, s_u, kUnionWords, s_nwin, s_srgb,
                                            stamp ? ts : nullptr);
     }
     // A tile with pool runs (s_misc[9]: its run slots) clears its run table and run
@@ -2909,27 +2975,33 @@ void launch_setup_bin(const DrawParams& p, void* stream) {
     }
 }
 
-template <int PROG, int MODE, int NT>
+template <int PROG, int MODE, int NT, int TS>
 static void launch_tile_pmt(const DrawParams& p, hipStream_t s, bool initd) {
     const uint32_t blocks = p.ntiles + (p.job_entries ? p.job_pad : 0u);  // (tile jobs: part blocks first)
-    if (initd)
-        hipLaunchKernelGGL((k_tile<PROG, MODE, true, NT>), dim3(blocks), dim3(NT), 0, s, p);
-    else
-        hipLaunchKernelGGL((k_tile<PROG, MODE, false, NT>), dim3(blocks), dim3(NT), 0, s, p);
+    if constexpr (MODE == kDepthLastWins) {  // (initial depths: last-wins modes only)
+        if (initd) {
+            hipLaunchKernelGGL((k_tile<PROG, MODE, true, NT, TS>), dim3(blocks), dim3(NT), 0, s, p);
+            return;
+        }
+    }
+    hipLaunchKernelGGL((k_tile<PROG, MODE, false, NT, TS>), dim3(blocks), dim3(NT), 0, s, p);
 }
 
-// (workgroup sizes per tile edge: tile_threads_for)
+// Tile-edge instances (tile_variant_built): every program and mode at 32 px, with
+// 256 or 512 threads (tile_threads_for); 16- and 64-px tiles (256 / 512 or 1024
+// threads) for the flat and Blinn-Phong programs under the depth-writing modes, the draws
+// tile_shift_for picks them for (dense soups, crowded scenes).
 template <int PROG, int MODE>
 static void launch_tile_pm(const DrawParams& p, hipStream_t s, bool initd) {
-    if constexpr (kTile == 64) {
-        launch_tile_pmt<PROG, MODE, 1024>(p, s, initd);
-    } else if constexpr (kTile == 16) {
-        launch_tile_pmt<PROG, MODE, kTileThreads>(p, s, initd);
-    } else {
-        switch (p.tile_threads) {
-        case 512: launch_tile_pmt<PROG, MODE, 512>(p, s, initd); break;
-        default: launch_tile_pmt<PROG, MODE, kTileThreads>(p, s, initd); break;
-        }
+    if constexpr (tile_variant_built(PROG, MODE)) {
+        if (p.tile_shift == 6u)
+            return p.tile_threads == 1024u ? launch_tile_pmt<PROG, MODE, 1024, 6>(p, s, initd)
+                                           : launch_tile_pmt<PROG, MODE, 512, 6>(p, s, initd);
+        if (p.tile_shift == 4u) return launch_tile_pmt<PROG, MODE, kTileThreads, 4>(p, s, initd);
+    }
+    switch (p.tile_threads) {
+    case 512: launch_tile_pmt<PROG, MODE, 512, kTileShift>(p, s, initd); break;
+    default: launch_tile_pmt<PROG, MODE, kTileThreads, kTileShift>(p, s, initd); break;
     }
 }
 

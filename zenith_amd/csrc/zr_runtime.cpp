@@ -290,7 +290,11 @@ struct zr_device_t {
         uint32_t job_parts = 0; // ... and the most parts it put on one XCD
     };
     int jobs = -1;              // ZR_JOBS: tile jobs of N entries (tests), 0 off; -1: use_tile_jobs
-    uint64_t job_want_max = 0;  // the most key buffers a draw asked for since the last shrink check
+    uint64_t job_want_max = 0;  // the most job keys (buffers x tile pixels) a draw asked for since the last shrink check
+    std::vector<uint32_t> slab_tile_px;  // pixels per tile of the draw in each status slot (slab_keys)
+    int hiz = -1;                        // ZR_HIZ=0/1 forces k_tile's max-key test; -1: draws with tile jobs
+    uint32_t forced_tile_shift = 0;      // ZR_TILE: every unsharded draw with a built instance at this edge (16 / 32 / 64)
+    uint32_t last_tile = kTile;          // the tile edge of the last draw recorded
     std::unordered_map<uint64_t, BinShape> bin_shapes;
     std::vector<uint64_t> slab_keys;
     uint32_t forced_slab = ~0u; // ZR_BIN_SLAB: every draw's slab (tests: pool runs everywhere)
@@ -333,6 +337,15 @@ struct zr_device_t {
 // ------------------------------------------------------------ device helpers
 
 namespace {
+
+// A draw shape's key for the bin / job measurements (zr_device_t::bin_shapes):
+// its tile count and its primitive count to 5 significant bits, so draws whose
+// count varies a little (culling, LOD, streaming) share their measurements.
+uint64_t shape_key(uint32_t ntiles, uint32_t prims) {
+    const uint32_t bits = prims ? 32u - (uint32_t)__builtin_clz(prims) : 0u;
+    const uint32_t drop = bits > 5u ? bits - 5u : 0u;
+    return ((uint64_t)ntiles << 32) | ((prims >> drop) << drop);
+}
 
 zr_result set_device(zr_device* d) {
     ZR_HIP(hipSetDevice(d->hip_device));
@@ -532,7 +545,7 @@ zr_result device_sync(zr_device* d) {
         const uint32_t job_bufs = st[kStJobBufSlot0 + i], job_parts = st[kStJobPartSlot0 + i];
         st[kStJobBufSlot0 + i] = 0;
         st[kStJobPartSlot0 + i] = 0;
-        d->job_want_max = std::max<uint64_t>(d->job_want_max, job_bufs);
+        d->job_want_max = std::max<uint64_t>(d->job_want_max, (uint64_t)job_bufs * d->slab_tile_px[i]);
         if (!target) continue;
         need = std::max<uint64_t>({need, (d->slab_keys[i] >> 32) * target + pool,
                                    (d->slab_keys[i] >> 32) * bin_slab_whole(target, max_tile) + 4096});
@@ -551,6 +564,7 @@ zr_result device_sync(zr_device* d) {
         v.job_parts = job_parts;
     }
     d->slab_keys.clear();
+    d->slab_tile_px.clear();
     if (st[kStOverflow]) {
         d->overflowed_draws += st[kStOverflow];
         st[kStOverflow] = 0;
@@ -574,7 +588,7 @@ zr_result device_sync(zr_device* d) {
         if (check) {
             // tile-job key buffers (8 B per pixel of a tile each) follow the most
             // any draw of the interval asked for, the same way
-            const uint64_t keep = (d->job_want_max ? d->job_want_max * 5 / 4 + 16 : 0) * (uint64_t)kTilePixels;
+            const uint64_t keep = d->job_want_max ? d->job_want_max * 5 / 4 + 16 * (uint64_t)kTilePixels : 0;  // (keys)
             for (ScratchSet& S : d->sets) {
                 if (!S.job_keys || S.job_keys_cap <= 2 * keep + (1u << 16)) continue;
                 (void)hipFree(S.job_keys);
@@ -589,6 +603,7 @@ zr_result device_sync(zr_device* d) {
             d->bins_syncs = 0;
         }
     }
+    d->last.tile_size = d->last_tile;
     d->last.job_key_bytes = 0;
     for (const ScratchSet& S : d->sets) d->last.job_key_bytes += S.job_keys ? S.job_keys_cap * 8 : 0;
     d->last.overflowed_draws = d->overflowed_draws;
@@ -659,6 +674,21 @@ int32_t choose_depth_mode(bool test, bool write, int32_t op) {
     return kDepthLastWins;
 }
 
+// The draw's tiles at an edge of 1 << shift pixels: the grid, and the tiles this
+// shard owns (ShardGeom).
+void set_tiles(DrawParams& P, uint32_t shift) {
+    const uint32_t t = 1u << shift;
+    P.tile_shift = shift;
+    P.tiles_x = (P.fb_w + t - 1) >> shift;
+    P.tiles_y = (P.fb_h + t - 1) >> shift;
+    const ShardGeom sg = shard_geom(P.tiles_x, P.tiles_y, P.shard_count, P.shard_rank);
+    P.full_rows = sg.full_rows;
+    P.own_rows = sg.own_rows;
+    P.left_lo = sg.left_lo;
+    P.left_hi = sg.left_hi;
+    P.ntiles = shard_tiles(sg);
+}
+
 zr_result fill_target(const ExecState& s, DrawParams& P) {
     const zr_texture* ct = s.rs.has_color ? s.rs.color.texture : nullptr;
     const zr_texture* dt = s.rs.has_depth ? s.rs.depth.texture : nullptr;
@@ -681,16 +711,9 @@ zr_result fill_target(const ExecState& s, DrawParams& P) {
     P.ra_y0 = ay0;
     P.ra_x1 = (int32_t)ax1;
     P.ra_y1 = (int32_t)ay1;
-    P.tiles_x = (P.fb_w + kTile - 1) / kTile;
-    P.tiles_y = (P.fb_h + kTile - 1) / kTile;
     P.shard_rank = s.shard_rank;
     P.shard_count = s.shard_count;
-    const ShardGeom sg = shard_geom(P.tiles_x, P.tiles_y, s.shard_count, s.shard_rank);
-    P.full_rows = sg.full_rows;
-    P.own_rows = sg.own_rows;
-    P.left_lo = sg.left_lo;
-    P.left_hi = sg.left_hi;
-    P.ntiles = shard_tiles(sg);
+    set_tiles(P, kTileShift);
     // clears (fused into the first draw of the pass, else k_clear at end_rendering)
     P.clear_color_enable = (ct && s.color_clear_pending) ? 1u : 0u;
     if (ct) {
@@ -761,7 +784,7 @@ zr_result ensure_scratch(zr_device* d, ScratchSet& S, DrawParams& P) {
     // goes to the slabs, where no run is needed (cerberus: the target slab put its
     // crowded tiles' excess in runs, setup +8 us).
     const uint64_t nt = std::max<uint32_t>(P.ntiles, 1u), cap = S.bins_cap;
-    const uint64_t key = ((uint64_t)P.ntiles << 32) | P.draw_prims;
+    const uint64_t key = shape_key(P.ntiles, P.draw_prims);
     const auto shape = d->bin_shapes.find(key);
     uint64_t slab = cap / (3 * nt);
     if (d->forced_slab != ~0u) {
@@ -806,14 +829,14 @@ zr_result ensure_scratch(zr_device* d, ScratchSet& S, DrawParams& P) {
             parts = (uint64_t)shape->second.job_parts * 5 / 4 + 8;
         } else {
             const uint64_t pairs = known ? (uint64_t)P.ntiles * shape->second.target + shape->second.pool : cap;
-            bufs = std::min<uint64_t>(2 * (pairs / P.job_entries) + 64, kJobKeyBytesFirst / (8ull * kTilePixels));
+            bufs = std::min<uint64_t>(2 * (pairs / P.job_entries) + 64, kJobKeyBytesFirst / (8ull << (2 * P.tile_shift)));
             parts = pairs / P.job_entries / 4 + 64;  // (a few crowded tiles: parts spread over several XCDs)
         }
         P.job_pad = (uint32_t)std::min<uint64_t>(8 * parts, 1u << 20);
         P.job_slots = (uint32_t)std::min<uint64_t>(bufs, 1u << 20);
         const uint64_t tc = S.job_tickets_cap;
         if ((rc = grow(d, S.job_slot, S.job_slot_cap, P.ntiles, 4))) return rc;
-        if ((rc = grow(d, S.job_keys, S.job_keys_cap, (uint64_t)P.job_slots * kTilePixels, 8))) return rc;
+        if ((rc = grow(d, S.job_keys, S.job_keys_cap, (uint64_t)P.job_slots << (2 * P.tile_shift), 8))) return rc;
         if ((rc = grow(d, S.job_tickets, S.job_tickets_cap, P.job_slots, 4))) return rc;
         if (S.job_tickets_cap != tc) ZR_HIP(hipMemset(S.job_tickets, 0, S.job_tickets_cap * 4));
         P.job_slot = S.job_slot;
@@ -824,6 +847,7 @@ zr_result ensure_scratch(zr_device* d, ScratchSet& S, DrawParams& P) {
     if (!d->capturing && d->slab_keys.size() < kSlabSlots) {
         P.stat_slot = (uint32_t)d->slab_keys.size();
         d->slab_keys.push_back(key);
+        d->slab_tile_px.push_back(1u << (2 * P.tile_shift));
     }
     P.status = d->status_dev;
     return ZR_SUCCESS;
@@ -995,6 +1019,24 @@ zr_result exec_draw(zr_device* d, ExecState& s, const Cmd& c, bool indexed) {
         P.view_proj = nullptr;
     }
     if (mesh && !P.view_proj && !P.view_push) return fail(ZR_ERROR_VALIDATION_FAILED, "descriptor 'View' not bound");
+    // The tile edge (tile_shift_for): 16 px for a shape whose 32-px tiles needed
+    // tile jobs (measured), 64 px for large dense targets, 32 px otherwise and for
+    // shards; ZR_TILE forces an edge (tests, A/B) where the instance exists.
+    if (P.shard_count == 1 && tile_variant_built(P.program, P.depth_mode)) {
+        uint32_t shift = d->forced_tile_shift;
+        if (!shift) {
+            // the edge by size, then 16 px if that edge's shape was measured crowded
+            // (its draws keep consulting that measurement, stable once it is made)
+            shift = tile_shift_for(prims, P.fb_w, P.fb_h, P.shard_count, false);
+            if (shift != P.tile_shift) set_tiles(P, shift);
+            const auto sh = d->bin_shapes.find(shape_key(P.ntiles, P.draw_prims));
+            if (sh != d->bin_shapes.end() && crowded_shape(sh->second.max_tile, sh->second.target))
+                shift = tile_shift_for(prims, P.fb_w, P.fb_h, P.shard_count, true);
+        }
+        if (shift != P.tile_shift) set_tiles(P, shift);
+        if (P.ntiles > kMaxTilesPerPass) set_tiles(P, kTileShift);
+    }
+    d->last_tile = 1u << P.tile_shift;
     // binning geometry: k_setup_bin runs one kSetupThreads workgroup per CU at most
     // (its LDS histogram of all tiles; workgroups never wait for each other)
     if (P.ntiles > kMaxTilesPerPass)
@@ -1055,10 +1097,12 @@ zr_result exec_draw(zr_device* d, ExecState& s, const Cmd& c, bool indexed) {
     // (records mode never runs setup_finish: no effect there)
     P.micro = (d->micro < 0 ? use_micro_test(prims, (uint64_t)(P.ra_x1 - P.ra_x0 + 1) * (uint64_t)(P.ra_y1 - P.ra_y0 + 1))
                             : d->micro != 0) ? 1u : 0u;
-    P.tile_threads = (d->tile_threads && kTile == 32) ? d->tile_threads
-                                     : tile_threads_for(P.ntiles, (uint32_t)std::max(d->cu_count, 1), prims, partitioned);
-    P.rec_table = (d->rec_table < 0 ? use_record_table(prims, P.tiles_x, P.tiles_y) : d->rec_table != 0) ? 1u : 0u;
-    const bool sched = d->tile_sched < 0 ? use_tile_schedule(P.ntiles, (uint32_t)std::max(d->cu_count, 1), P.tile_threads, prims)
+    P.tile_threads = (d->tile_threads && P.tile_shift == kTileShift)
+                         ? d->tile_threads
+                         : tile_threads_for(P.ntiles, (uint32_t)std::max(d->cu_count, 1), prims, partitioned, P.tile_shift);
+    P.rec_table = (d->rec_table < 0 ? use_record_table(prims, P.tiles_x, P.tiles_y, P.tile_shift) : d->rec_table != 0) ? 1u : 0u;
+    const bool sched = d->tile_sched < 0 ? use_tile_schedule(P.ntiles, (uint32_t)std::max(d->cu_count, 1), P.tile_threads,
+                                                             prims, P.tile_shift)
                                          : d->tile_sched != 0;
     P.debug = d->debug;
     if (d->census && !d->capturing) {  // winner census: a bitmap over the draw's primitives, zeroed per draw
@@ -1087,6 +1131,8 @@ zr_result exec_draw(zr_device* d, ExecState& s, const Cmd& c, bool indexed) {
     // writes no schedule: k_tile then keeps xcd_tile order instead of reading an
     // unwritten one)
     P.tile_sched = sched && !(d->debug & kDebugPhase1Only) ? 1u : 0u;
+    // the max-key test for draws whose lists are long enough to split (tile jobs)
+    P.hiz = d->hiz >= 0 ? (uint32_t)d->hiz : (P.job_entries ? 1u : 0u);
     if ((sched || P.job_entries) && !(d->debug & kDebugPhase1Only)) {
         if ((rc = grow(d, S.tile_order, S.tile_order_cap, (uint64_t)P.ntiles + P.job_pad, 4))) return rc;
         P.tile_order = S.tile_order;
@@ -1325,6 +1371,11 @@ ZR_API zr_result zr_device_create(int32_t hip_device, zr_device** out) {
     if (const char* mi = getenv("ZR_MICRO")) d->micro = atoi(mi) != 0 ? 1 : 0;
     if (const char* ss = getenv("ZR_BIN_SHRINK_SYNCS")) d->shrink_syncs = (uint32_t)strtoul(ss, nullptr, 0);
     if (const char* jb = getenv("ZR_JOBS")) d->jobs = atoi(jb) > 0 ? std::max(atoi(jb), 256) : 0;
+    if (const char* hz = getenv("ZR_HIZ")) d->hiz = atoi(hz) != 0 ? 1 : 0;
+    if (const char* tl = getenv("ZR_TILE")) {
+        const unsigned long v = strtoul(tl, nullptr, 0);
+        d->forced_tile_shift = v == 16 ? 4u : v == 32 ? 5u : v == 64 ? 6u : 0u;
+    }
     if (const char* nt = getenv("ZR_TILE_NT")) {
         const unsigned long v = strtoul(nt, nullptr, 0);
         d->tile_threads = v >= 512 ? 512u : v ? 256u : 0u;

@@ -87,7 +87,8 @@ class zr_draw_stats(C.Structure):
                 ("bin_capacity", C.c_uint64), ("overflowed_draws", C.c_uint64),
                 ("route_max_entries", C.c_uint64), ("route_fallback_draws", C.c_uint64), ("winners", C.c_uint64),
                 ("micro_fragments", C.c_uint64), ("bin_pool_pairs", C.c_uint64), ("bin_pool_runs", C.c_uint64),
-                ("tile_jobs", C.c_uint64), ("job_key_bytes", C.c_uint64)]
+                ("tile_jobs", C.c_uint64), ("job_key_bytes", C.c_uint64),
+                ("tile_size", C.c_uint64)]
 
 
 class zr_buffer_desc(C.Structure):
