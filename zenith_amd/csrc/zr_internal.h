@@ -119,6 +119,7 @@ constexpr uint32_t kJobNone = 0xFFFFFFFFu;     // tile_order item of a spare blo
 // tile_order item flag: part 0 of a split tile, placed among the part blocks
 // (parts < 2^17: a list of at most 2^26 entries in jobs of at least 256)
 constexpr uint32_t kJobFront = 1u << 31;
+constexpr uint32_t kJobSplit = 1u << 31;  // job_slot[t] flag: tile t is split (its own k_tile block exits)
 #ifndef ZR_JOBS_FRONT
 #define ZR_JOBS_FRONT 1
 #endif
@@ -385,9 +386,6 @@ struct DrawParams {
     // log2 of the draw's tile edge (kTileShiftMin..kTileShiftMax; tile_shift_for):
     // k_setup_bin bins and k_tile rasterizes tiles of 1 << tile_shift pixels a side
     uint32_t tile_shift;
-    // k_tile's max-key test between a tile's segments (crowded lists; zr_runtime
-    // exec_draw): 1 for draws with tile jobs, ZR_HIZ forces it
-    uint32_t hiz;
     // push-constant state at the draw (zr_cmd_push_constants): the bytes ride in
     // the launch's kernel arguments, as Vulkan push constants ride in user SGPRs
     // (last, so the fields above keep their kernarg offsets; fields added later

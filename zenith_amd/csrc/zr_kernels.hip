@@ -1053,7 +1053,7 @@ __device__ __noinline__ void build_job_schedule(const DrawParams& P, uint32_t nt
         const uint32_t K = P.job_slot[t];
         if (K <= 1u) continue;
         const uint32_t x = xcd_block(t, nt) & 7u;
-        P.job_slot[t] = atomicAdd(&s_tot[1], K);  // (K key buffers, one per job)
+        P.job_slot[t] = atomicAdd(&s_tot[1], K) | kJobSplit;  // (K key buffers, one per job)
         const uint32_t p0 = kJobsFront ? 0u : 1u;
         const uint32_t l0 = atomicAdd(&s_cnt[x], K - p0);
         for (uint32_t p = p0; p < K; ++p)
@@ -1755,14 +1755,6 @@ __device__ __forceinline__ void raster_lane(const DrawParams& P, const TriRecord
         sweep(std::true_type{}, std::true_type{});
 }
 
-// The tile's max-key test (k_tile, DrawParams::hiz): depth-writing modes only; the
-// margin on a primitive's best vertex depth bounds the depth plane's rounding
-// (a few ulp of the depths' magnitude, which lie in [0, 1]) with room to spare.
-#ifndef ZR_HIZ_BUILD
-#define ZR_HIZ_BUILD 1
-#endif
-constexpr float kHizMargin = 1e-5f;
-
 // Visibility sequence of setup record e (API order): e + 1, or for the mesh
 // program 4p + k + 1 for fan k of primitive p (zr_internal.h kMeshFans).
 template <int PROG>
@@ -2360,8 +2352,7 @@ __global__ __launch_bounds__(NT, kTileWgs * kTileThreads / 256) void k_tile(Draw
     constexpr uint32_t kWgsPerCu = kTileWgs * (uint32_t)kTileThreads / (uint32_t)NT;
     constexpr uint32_t kBudget = 160u * 1024u / kWgsPerCu;
     constexpr uint32_t kMiscWords = 16;
-    constexpr uint32_t kWaves = (uint32_t)NT / 64u;
-    constexpr uint32_t kUnionWords = (kBudget - TP * 8u - 256u * 4u - kMiscWords * 4u - kWaves * 8u) / 4u;
+    constexpr uint32_t kUnionWords = (kBudget - TP * 8u - 256u * 4u - kMiscWords * 4u) / 4u;
     static_assert(kSortCap + kBigQueue + kSortBuckets + (INITD ? TP : 0u) +
                           ((NT >= 512 && MODE != kDepthLastWins && PROG != kProgMesh && !INITD && (TS <= 5 || NT >= 1024))
                                ? 4u * kSortCap + kRecHashSlots
@@ -2372,7 +2363,6 @@ __global__ __launch_bounds__(NT, kTileWgs * kTileThreads / 256) void k_tile(Draw
     __shared__ float s_srgb[256];
     __shared__ __attribute__((aligned(16))) uint32_t s_u[kUnionWords];
     __shared__ uint32_t s_misc[kMiscWords];
-    __shared__ unsigned long long s_wmax[kWaves];  // per wave: the worst key of its pixels (the tile's max-key test)
     uint32_t* s_sorted = s_u;                       // [kSortCap]
     // wave-path (large) primitives of the segment, rasterized after its
     // chunks by whichever wave claims them next: the area sort groups them, so the
@@ -2383,7 +2373,6 @@ __global__ __launch_bounds__(NT, kTileWgs * kTileThreads / 256) void k_tile(Draw
     // 512-thread tiles: the record table of the resolve (rec_table_insert); last-wins
     // modes need the records' depth terms, which it does not hold
     // (64-px tiles: only 1024-thread workgroups have the LDS for it beside 32 KiB of keys)
-    constexpr bool kHiz = ZR_HIZ_BUILD && MODE != kDepthLastWins && !INITD;
     constexpr bool kTab = ZR_TAB && !ZR_RESOLVE_DEDUP512 && NT >= 512 && MODE != kDepthLastWins && PROG != kProgMesh &&
                           !INITD && (TS <= 5 || NT >= 1024);
     int4* s_trec = reinterpret_cast<int4*>(s_bucket + kSortBuckets);        // [kSortCap]
@@ -2403,6 +2392,9 @@ __global__ __launch_bounds__(NT, kTileWgs * kTileThreads / 256) void k_tile(Draw
     if (item == kJobNone) return;
     const bool front = (item & kJobFront) != 0u;  // part 0 of a split tile among the part blocks
     const uint32_t t = item & kJobTileMask, part = (item & ~kJobFront) >> kJobTileBits;
+    const bool own_split = kJobsFront && jp && part == 0u && !front &&
+                           (__builtin_amdgcn_readfirstlane((int)P.job_slot[t]) & (int)kJobSplit) != 0;
+    if (own_split && blockIdx.x != jp) return;  // (block jp reports the draw's stats first, below)
     uint32_t tx, ty;
     shard_tile_xy(shard_geom(P), t, tx, ty);
     const int x0 = (int)tx * T, y0 = (int)ty * T;
@@ -2559,7 +2551,7 @@ __global__ __launch_bounds__(NT, kTileWgs * kTileThreads / 256) void k_tile(Draw
         s_misc[8] = (rcw & kRunFill) ? (rcw & ~(kRunFill | kRunDropped)) >> kRunFillShift : min(count, slab);
         s_misc[9] = has_runs ? P.run_cap : 0u;  // (one run slot per setup workgroup, empty ones of length 0)
         s_misc[10] = K;
-        s_misc[11] = K > 1u ? P.job_slot[t] : 0u;
+        s_misc[11] = K > 1u ? P.job_slot[t] & ~kJobSplit : 0u;
     }
     // k_setup_bin's counters back to zero for the next draw on this scratch set:
     // each tile its own count (every wave has read it: the barrier above) and, at
@@ -2568,8 +2560,10 @@ __global__ __launch_bounds__(NT, kTileWgs * kTileThreads / 256) void k_tile(Draw
     if (threadIdx.x == 0 && K == 1u) P.tile_counts[t] = 0u;  // (a split tile: its resolving job)
     if (blockIdx.x == jp)
         for (uint32_t i = threadIdx.x; i < kCtWords; i += NT) P.counters[i] = 0u;
-    // a split tile's own block: its part 0 runs among the part blocks (build_job_schedule)
-    if (kJobsFront && K > 1u && part == 0u && !front) return;
+    // a split tile's own block: its part 0 runs among the part blocks (build_job_schedule).
+    // Decided by the builder's mark, not by the count: the tile's jobs may have
+    // resolved it and reset its count before this block starts.
+    if (own_split) return;
 
     const uint32_t wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
     const int lane = threadIdx.x & 63;
@@ -2580,24 +2574,8 @@ __global__ __launch_bounds__(NT, kTileWgs * kTileThreads / 256) void k_tile(Draw
         // so that a 64-lane chunk holds primitives of similar cost (the lane loop runs
         // as long as its largest member).  Then each wave takes every 4th chunk: one
         // lane per entry loads the 64-B record, and the wave walks the chunk.
-        bool hiz_on = false;  // s_wmax holds the keys of the segments so far (kHiz)
         for (uint32_t seg = seg_lo; seg < cnt; seg += kSortCap) {
             const uint32_t n = min(kSortCap, cnt - seg);
-            // The tile's max-key test (crowded lists, DrawParams::hiz): after a segment, the
-            // worst (largest) key of any pixel of the tile; a primitive whose every
-            // fragment's key would exceed it -- its best vertex depth, less a margin
-            // far above the depth plane's rounding, is strictly worse than that pixel
-            // depth -- cannot win a pixel and is skipped before its walk.  Ties are not
-            // skipped (the sequence decides them), nor is anything in last-wins modes.
-            // (the depth half of the key decides: a bound key's sequence half is 0;
-            // wave-uniform, in an SGPR)
-            uint32_t kmax_hi = ~0u;
-            if (kHiz && hiz_on) {
-                uint32_t m = 0;
-#pragma unroll
-                for (uint32_t w = 0; w < kWaves; ++w) m = max(m, (uint32_t)(s_wmax[w] >> 32));
-                kmax_hi = (uint32_t)__builtin_amdgcn_readfirstlane((int)m);
-            }
             // a list with pool runs loads its segments past the slab part through
             // the run table (s_misc[9]: runs, s_misc[8]: the slab part's length)
             const uint32_t nr = (uint32_t)__builtin_amdgcn_readfirstlane((int)s_misc[9]);
@@ -2692,14 +2670,7 @@ __global__ __launch_bounds__(NT, kTileWgs * kTileThreads / 256) void k_tile(Draw
                     q0 = rp[0];
                     q1 = rp[1];
                 }
-                bool valid = j < n && !(tile_debug(P) & kDebugLoadOnly);
-                if (kHiz && kmax_hi != ~0u && valid) {
-                    const float z0 = __int_as_float(q1.x), z1 = z0 + __int_as_float(q1.y), z2 = z0 + __int_as_float(q1.z);
-                    const bool lt = MODE == kDepthMinStrict || MODE == kDepthMinNonStrict;
-                    const float zb = lt ? fmaxf(fminf(z0, fminf(z1, z2)) - kHizMargin, 0.0f)
-                                        : fmaxf(z0, fmaxf(z1, z2)) + kHizMargin;
-                    valid = (uint32_t)(frag_key<MODE>(zb, 0u) >> 32) <= kmax_hi;
-                }
+                const bool valid = j < n && !(tile_debug(P) & kDebugLoadOnly);
                 if (tile_debug(P) & kDebugLoadOnly) asm volatile("" ::"v"(q0.x), "v"(q1.x), "v"(my_prim));
                 const bool large = compact_is_large(q0);
                 // A large primitive below the last cost bucket (bbox ∩ tile under ~253
@@ -2797,14 +2768,6 @@ __global__ __launch_bounds__(NT, kTileWgs * kTileThreads / 256) void k_tile(Draw
                 const TriRecord rb = uniform_record(b0, b1, b2, b3);
                 raster_prim<MODE, INITD, TS>(P, ra, entry_seq<PROG>(P, e0), x0, y0, lane, s_key, s_initd);
                 if (two) raster_prim<MODE, INITD, TS>(P, rb, entry_seq<PROG>(P, e1), x0, y0, lane, s_key, s_initd);
-            }
-            if (kHiz && P.hiz && seg + kSortCap < cnt) {  // another segment follows: the tile's worst key so far
-                unsigned long long m = 0;
-                for (int i = threadIdx.x; i < TP; i += NT) m = max(m, s_key[i]);
-#pragma unroll
-                for (int o = 32; o > 0; o >>= 1) m = max(m, (unsigned long long)__shfl_xor((long long)m, o, 64));
-                if (lane == 0) s_wmax[wave] = m;
-                hiz_on = true;
             }
             __syncthreads();
         }

@@ -292,7 +292,7 @@ struct zr_device_t {
     int jobs = -1;              // ZR_JOBS: tile jobs of N entries (tests), 0 off; -1: use_tile_jobs
     uint64_t job_want_max = 0;  // the most job keys (buffers x tile pixels) a draw asked for since the last shrink check
     std::vector<uint32_t> slab_tile_px;  // pixels per tile of the draw in each status slot (slab_keys)
-    int hiz = -1;                        // ZR_HIZ=0/1 forces k_tile's max-key test; -1: draws with tile jobs
+    uint32_t setup_batch = 0;            // ZR_SETUP_BATCH: primitives per lane in flight (1, 2, 4; 0: 2)
     uint32_t forced_tile_shift = 0;      // ZR_TILE: every unsharded draw with a built instance at this edge (16 / 32 / 64)
     uint32_t last_tile = kTile;          // the tile edge of the last draw recorded
     std::unordered_map<uint64_t, BinShape> bin_shapes;
@@ -1041,7 +1041,8 @@ zr_result exec_draw(zr_device* d, ExecState& s, const Cmd& c, bool indexed) {
     // (its LDS histogram of all tiles; workgroups never wait for each other)
     if (P.ntiles > kMaxTilesPerPass)
         return fail(ZR_ERROR_FEATURE_NOT_PRESENT, "more owned tiles in one pass than the setup pass histogram holds (kMaxTilesPerPass)");
-    P.setup_batch = mesh ? 1u : 2u;  // k_setup_bin<2> (the mesh instance: <1, true>)
+    P.setup_batch = mesh ? 1u : (d->setup_batch ? d->setup_batch : 2u);  // k_setup_bin<2> (the mesh instance: <1, true>)
+    const uint64_t lds_budget = kSetupLdsBudget;  // (one workgroup per CU owns the LDS; two measured slower)
     if (d->occupancy_checked_tiles != P.ntiles || d->occupancy_checked_mesh != mesh) {
         int nb = 0;
         ZR_HIP(hipOccupancyMaxActiveBlocksPerMultiprocessor(&nb, setup_bin_kernel(P.setup_batch, mesh), kSetupThreads,
@@ -1072,7 +1073,7 @@ zr_result exec_draw(zr_device* d, ExecState& s, const Cmd& c, bool indexed) {
         const uint64_t own_max = ((uint64_t)P.units + P.setup_wgs - 1) / P.setup_wgs;
         const uint64_t entries = own_max << shift;
         const uint64_t hist = setup_bin_lds_bytes(P.ntiles, 0);
-        const uint64_t budget = std::min<uint64_t>(kSetupBboxLdsBytes, hist < kSetupLdsBudget ? kSetupLdsBudget - hist : 0);
+        const uint64_t budget = std::min<uint64_t>(kSetupBboxLdsBytes, hist < lds_budget ? lds_budget - hist : 0);
         // (mesh: fans 1 and 2 keep their bboxes in global memory, so all of them do)
         P.bbox_lds = (!mesh && entries * sizeof(BBox) <= budget) ? (uint32_t)entries : 0u;
         stage_entries = entries;
@@ -1089,7 +1090,7 @@ zr_result exec_draw(zr_device* d, ExecState& s, const Cmd& c, bool indexed) {
     {
         const uint64_t used = setup_bin_lds_bytes(P.ntiles, P.bbox_lds);
         const uint64_t cur = ((uint64_t)P.ntiles + 3u) / 4u * 4u * 4u;
-        const uint64_t room = used + cur < kSetupLdsBudget ? (kSetupLdsBudget - used - cur) / 8u : 0u;
+        const uint64_t room = used + cur < lds_budget ? (lds_budget - used - cur) / 8u : 0u;
         const uint64_t cap = std::min<uint64_t>(room, 2u * std::max<uint64_t>(stage_entries, 1024u));
         const bool on = d->bin_stage > 0 || (d->bin_stage < 0 && kBinStageDefault && !overlap_setup);
         P.bin_stage = on && cap >= 1024u ? (uint32_t)cap : 0u;
@@ -1131,8 +1132,6 @@ zr_result exec_draw(zr_device* d, ExecState& s, const Cmd& c, bool indexed) {
     // writes no schedule: k_tile then keeps xcd_tile order instead of reading an
     // unwritten one)
     P.tile_sched = sched && !(d->debug & kDebugPhase1Only) ? 1u : 0u;
-    // the max-key test for draws whose lists are long enough to split (tile jobs)
-    P.hiz = d->hiz >= 0 ? (uint32_t)d->hiz : (P.job_entries ? 1u : 0u);
     if ((sched || P.job_entries) && !(d->debug & kDebugPhase1Only)) {
         if ((rc = grow(d, S.tile_order, S.tile_order_cap, (uint64_t)P.ntiles + P.job_pad, 4))) return rc;
         P.tile_order = S.tile_order;
@@ -1371,7 +1370,10 @@ ZR_API zr_result zr_device_create(int32_t hip_device, zr_device** out) {
     if (const char* mi = getenv("ZR_MICRO")) d->micro = atoi(mi) != 0 ? 1 : 0;
     if (const char* ss = getenv("ZR_BIN_SHRINK_SYNCS")) d->shrink_syncs = (uint32_t)strtoul(ss, nullptr, 0);
     if (const char* jb = getenv("ZR_JOBS")) d->jobs = atoi(jb) > 0 ? std::max(atoi(jb), 256) : 0;
-    if (const char* hz = getenv("ZR_HIZ")) d->hiz = atoi(hz) != 0 ? 1 : 0;
+    if (const char* sb = getenv("ZR_SETUP_BATCH")) {
+        const int b = atoi(sb);
+        d->setup_batch = b == 1 || b == 2 || b == 4 ? (uint32_t)b : 0u;
+    }
     if (const char* tl = getenv("ZR_TILE")) {
         const unsigned long v = strtoul(tl, nullptr, 0);
         d->forced_tile_shift = v == 16 ? 4u : v == 32 ? 5u : v == 64 ? 6u : 0u;
