@@ -14,16 +14,16 @@ mkdir -p $O
 if [ "$2" != pmc ]; then  # "pmc": the profiler passes only
 timeout -k 10 700 python -u -m pytest tests -m gpu -x -q --timeout 120 --timeout-method thread > $O/pytest.log 2>&1 || exit 1
 timeout -k 10 300 python bench.py > $O/bench_c2.json 2> $O/bench.err || exit 2
-for c in c1 c3 c4 cerberus; do timeout -k 10 200 python bench.py --config $c --no-cpu-baseline > $O/bench_$c.json 2>> $O/bench.err || exit 3; done
+for c in c1 c3 c4 cerberus c2x c3x; do timeout -k 10 200 python bench.py --config $c --no-cpu-baseline > $O/bench_$c.json 2>> $O/bench.err || exit 3; done
 for g in 2 4 8; do timeout -k 10 200 python bench.py --emulate-shard $g --no-cpu-baseline > $O/bench_c2_shard$g.json 2>> $O/bench.err || exit 3; done
 for c in c2 c3; do timeout -k 10 200 python bench.py --config $c --emulate-shard 8 --setup partitioned --no-cpu-baseline > $O/bench_${c}_shard8_part.json 2>> $O/bench.err || exit 3; done
 timeout -k 10 200 python bench.py --config c3 --emulate-shard 8 --no-cpu-baseline > $O/bench_c3_shard8.json 2>> $O/bench.err || exit 3
 [ "$2" = quick ] && { echo done; exit 0; }
 fi
-timeout -k 10 200 rocprofv3 --kernel-trace --stats -d $O/kt -o run --output-format csv -- python3 bench.py --steps 50 --warmup 5 --no-cpu-baseline --no-census > $O/kt.log 2>&1 || exit 4
+timeout -k 10 200 rocprofv3 --kernel-trace --stats -d $O/kt -o run --output-format csv -- python3 bench.py --steps 50 --warmup 10 --no-cpu-baseline --cold-copies 0 --no-census > $O/kt.log 2>&1 || exit 4
 python3 tools/kt_summary.py $O/kt/run_kernel_stats.csv --config c2 -o $O/kt_c2.json > /dev/null || exit 4
-timeout -k 10 200 rocprofv3 --pmc FETCH_SIZE -d $O/pf -o run --output-format csv -- python3 bench.py --steps 5 --warmup 2 --no-cpu-baseline --no-census > $O/pf.log 2>&1 || exit 5
-timeout -k 10 200 rocprofv3 --pmc WRITE_SIZE -d $O/pw -o run --output-format csv -- python3 bench.py --steps 5 --warmup 2 --no-cpu-baseline --no-census > $O/pw.log 2>&1 || exit 6
+timeout -k 10 200 rocprofv3 --pmc FETCH_SIZE -d $O/pf -o run --output-format csv -- python3 bench.py --steps 20 --warmup 10 --no-cpu-baseline --cold-copies 0 --no-census > $O/pf.log 2>&1 || exit 5
+timeout -k 10 200 rocprofv3 --pmc WRITE_SIZE -d $O/pw -o run --output-format csv -- python3 bench.py --steps 20 --warmup 10 --no-cpu-baseline --cold-copies 0 --no-census > $O/pw.log 2>&1 || exit 6
 timeout -k 10 120 rocprofv3 --pmc FETCH_SIZE -d $O/cf -o run --output-format csv -- tools/build/pmc_calib > $O/calib_known.txt 2>&1 || exit 7
 timeout -k 10 120 rocprofv3 --pmc WRITE_SIZE -d $O/cw -o run --output-format csv -- tools/build/pmc_calib > $O/calib_w.txt 2>&1 || exit 8
 bash tools/pmc_classes.sh $V || exit 9

@@ -20,7 +20,7 @@ run() {  # name lib debug counter
   local n=$1 lib=$2 dbg=$3 ctr=$4
   shift 4
   ZR_LIB_PATH=$lib ZR_DEBUG=$dbg timeout -s KILL 90 rocprofv3 --pmc $ctr -d $O/$n -o run --output-format csv -- \
-    python3 bench.py --steps 5 --warmup 2 --no-cpu-baseline --cold-copies 0 --no-census "$@" > $O/$n.log 2>&1
+    python3 bench.py --steps 20 --warmup 10 --no-cpu-baseline --cold-copies 0 --no-census "$@" > $O/$n.log 2>&1
   local rc=$?
   echo "$n rc=$rc" >> $O/passes.txt
   case $rc in 0) ;; *) echo "pass $n ended with $rc; stopping"; exit $rc;; esac

@@ -35,7 +35,7 @@ fi
 i=0
 for p in "${PASSES[@]}"; do
   i=$((i+1))
-  timeout -s KILL 90 rocprofv3 --pmc $p -d $O/p$i -o run --output-format csv -- python3 bench.py --steps 5 --warmup 2 --no-cpu-baseline --cold-copies 0 --no-census "$@" > $O/p$i.log 2>&1
+  timeout -s KILL 90 rocprofv3 --pmc $p -d $O/p$i -o run --output-format csv -- python3 bench.py --steps 20 --warmup 10 --no-cpu-baseline --cold-copies 0 --no-census "$@" > $O/p$i.log 2>&1
   rc=$?
   echo "pass $i rc=$rc: $p" >> $O/passes.txt
   case $rc in 124|137|134|139) echo "pass $i ended with $rc; stopping"; exit $rc;; esac

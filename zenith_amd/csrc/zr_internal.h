@@ -116,14 +116,6 @@ constexpr uint32_t kMaxTilesPerPass = 16384;  // LDS histogram of the setup pass
 constexpr uint32_t kJobTileBits = 14;          // tile_order item: tile | part << kJobTileBits (tiles < kMaxTilesPerPass)
 constexpr uint32_t kJobTileMask = (1u << kJobTileBits) - 1u;
 constexpr uint32_t kJobNone = 0xFFFFFFFFu;     // tile_order item of a spare block (job grids)
-// tile_order item flag: part 0 of a split tile, placed among the part blocks
-// (parts < 2^17: a list of at most 2^26 entries in jobs of at least 256)
-constexpr uint32_t kJobFront = 1u << 31;
-constexpr uint32_t kJobSplit = 1u << 31;  // job_slot[t] flag: tile t is split (its own k_tile block exits)
-#ifndef ZR_JOBS_FRONT
-#define ZR_JOBS_FRONT 1
-#endif
-constexpr bool kJobsFront = ZR_JOBS_FRONT;  // every job of a split tile among the first blocks (A/B: 0)
 static_assert((1u << kJobTileBits) == kMaxTilesPerPass, "job items hold any tile index");
 constexpr uint32_t kMaxPushBytes = 128;       // ZR_MAX_PUSH_CONSTANTS_SIZE (Vulkan's guaranteed minimum)
 constexpr uint32_t kMaxPushWords = kMaxPushBytes / 4;

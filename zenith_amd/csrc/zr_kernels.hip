@@ -974,13 +974,12 @@ __device__ void build_tile_schedule(const DrawParams& P, uint32_t nt, uint32_t* 
 // Tile jobs (DrawParams::job_entries), built by the same last workgroup.  A
 // tile whose list is longer than J (and takes no record scan) becomes
 // K = ceil(count / J) jobs, part p covering list entries [p J, (p + 1) J), with
-// K key buffers from job_slot[t].  Every part takes a block of [0, job_pad), the
-// blocks dispatched first (round 6: part 0 kept the tile's own block in the usual
-// order and c2x's crowded tiles resolved late, their last jobs starting 92 us into
-// a 163-us pass), spread like its tile (block b % 8 = the tile's XCD in that
-// order, for L2 locality only); part 0's item carries kJobFront, and the tile's
-// own block (blocks [job_pad, job_pad + nt)) then exits after the block-level
-// duties; the blocks of [0, job_pad) left over get kJobNone.  When the
+// K key buffers from job_slot[t].  Part 0 keeps the tile's block in the usual
+// order (blocks [job_pad, job_pad + nt)); parts 1.. take blocks of [0, job_pad)
+// spread like their tile (block b % 8 = the tile's XCD in that order, for L2
+// locality only); the blocks of [0, job_pad) left over get kJobNone.  (Every
+// part among the first blocks, part 0 included, measured slower on c2x: 167.7 ->
+// 172.0 us per frame, docs/EXPERIMENTS.md round 6.)  When the
 // parts do not fit (an XCD's share of job_pad, or the key buffers) no tile is
 // split and the draw is counted (kCtJobsDenied) for the runtime to size them up.  k_tile derives K from the
 // same count and run word.
@@ -1018,7 +1017,7 @@ __device__ __noinline__ void build_job_schedule(const DrawParams& P, uint32_t nt
             const uint32_t K = tile_jobs(c[k] & ~kCountRuns, w[k], J);
             P.job_slot[t] = K;
             if (K > 1u) {
-                atomicAdd(&s_cnt[xcd_block(t, nt) & 7u], kJobsFront ? K : K - 1u);
+                atomicAdd(&s_cnt[xcd_block(t, nt) & 7u], K - 1u);
                 atomicAdd(&s_tot[0], K);
                 atomicAdd(&s_tot[3], 1u);
             }
@@ -1053,11 +1052,9 @@ __device__ __noinline__ void build_job_schedule(const DrawParams& P, uint32_t nt
         const uint32_t K = P.job_slot[t];
         if (K <= 1u) continue;
         const uint32_t x = xcd_block(t, nt) & 7u;
-        P.job_slot[t] = atomicAdd(&s_tot[1], K) | kJobSplit;  // (K key buffers, one per job)
-        const uint32_t p0 = kJobsFront ? 0u : 1u;
-        const uint32_t l0 = atomicAdd(&s_cnt[x], K - p0);
-        for (uint32_t p = p0; p < K; ++p)
-            P.tile_order[(l0 + p - p0) * 8u + x] = t | (p << kJobTileBits) | (p ? 0u : kJobFront);
+        P.job_slot[t] = atomicAdd(&s_tot[1], K);  // (K key buffers, one per job)
+        const uint32_t l0 = atomicAdd(&s_cnt[x], K - 1u);
+        for (uint32_t p = 1; p < K; ++p) P.tile_order[(l0 + p - 1u) * 8u + x] = t | (p << kJobTileBits);
     }
     for (uint32_t i = tid; i < P.job_pad; i += kSetupThreads)  // the spare part blocks
         if ((i >> 3) >= s_cnt[16 + (i & 7u)]) P.tile_order[i] = kJobNone;
@@ -2390,11 +2387,7 @@ __global__ __launch_bounds__(NT, kTileWgs * kTileThreads / 256) void k_tile(Draw
                                                                                    : blockIdx.x;
     const uint32_t item = (b < jp || P.tile_sched) ? P.tile_order[b] : xcd_tile(b - jp, P.ntiles);
     if (item == kJobNone) return;
-    const bool front = (item & kJobFront) != 0u;  // part 0 of a split tile among the part blocks
-    const uint32_t t = item & kJobTileMask, part = (item & ~kJobFront) >> kJobTileBits;
-    const bool own_split = kJobsFront && jp && part == 0u && !front &&
-                           (__builtin_amdgcn_readfirstlane((int)P.job_slot[t]) & (int)kJobSplit) != 0;
-    if (own_split && blockIdx.x != jp) return;  // (block jp reports the draw's stats first, below)
+    const uint32_t t = item & kJobTileMask, part = item >> kJobTileBits;
     uint32_t tx, ty;
     shard_tile_xy(shard_geom(P), t, tx, ty);
     const int x0 = (int)tx * T, y0 = (int)ty * T;
@@ -2551,7 +2544,7 @@ __global__ __launch_bounds__(NT, kTileWgs * kTileThreads / 256) void k_tile(Draw
         s_misc[8] = (rcw & kRunFill) ? (rcw & ~(kRunFill | kRunDropped)) >> kRunFillShift : min(count, slab);
         s_misc[9] = has_runs ? P.run_cap : 0u;  // (one run slot per setup workgroup, empty ones of length 0)
         s_misc[10] = K;
-        s_misc[11] = K > 1u ? P.job_slot[t] & ~kJobSplit : 0u;
+        s_misc[11] = K > 1u ? P.job_slot[t] : 0u;
     }
     // k_setup_bin's counters back to zero for the next draw on this scratch set:
     // each tile its own count (every wave has read it: the barrier above) and, at
@@ -2560,10 +2553,6 @@ __global__ __launch_bounds__(NT, kTileWgs * kTileThreads / 256) void k_tile(Draw
     if (threadIdx.x == 0 && K == 1u) P.tile_counts[t] = 0u;  // (a split tile: its resolving job)
     if (blockIdx.x == jp)
         for (uint32_t i = threadIdx.x; i < kCtWords; i += NT) P.counters[i] = 0u;
-    // a split tile's own block: its part 0 runs among the part blocks (build_job_schedule).
-    // Decided by the builder's mark, not by the count: the tile's jobs may have
-    // resolved it and reset its count before this block starts.
-    if (own_split) return;
 
     const uint32_t wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
     const int lane = threadIdx.x & 63;
