@@ -49,6 +49,31 @@ def test_design_bytes_by_request_class():
     assert d == {"bins": 4_000, "records": 32_000, "winner_gathers": 25_200, "stores": 16_000}
 
 
+def test_quoted_profiles_name_this_build():
+    """The PMC and kernel-trace summaries bench.py quotes by default (roofline.traffic,
+    kernels_rocprof) profiled the library built from this tree: their build stamp
+    is the hash of the current sources (zenith_amd/buildinfo.py), and a profile of
+    another build is never quoted (build_profile)."""
+    import bench
+    from zenith_amd import buildinfo
+    for name in ("pmc", "kt"):
+        path = os.path.join(ROOT, "profiles", f"{bench.PROFILE_TAG}_{name}_c2.json")
+        prof, src = bench.build_profile(path, "c2")
+        assert prof is not None, src
+        assert prof["build"] == buildinfo.source_hash()
+    pmc, _ = bench.build_profile(os.path.join(ROOT, "profiles", f"{bench.PROFILE_TAG}_pmc_c2.json"), "c2")
+    assert pmc["kernels"]["tile"]["hbm_bytes_per_launch"] > 0
+    stale = dict(pmc, build="0" * 16)
+    import tempfile
+    with tempfile.NamedTemporaryFile("w", suffix=".json", delete=False) as fh:
+        json.dump(stale, fh)
+    try:
+        prof, src = bench.build_profile(fh.name, "c2")
+        assert prof is None and "not this tree's" in src
+    finally:
+        os.unlink(fh.name)
+
+
 @pytest.mark.gpu
 def test_bench_json_line():
     """One short C1 run with a two-copy cold pass, as a child process: stdout holds
