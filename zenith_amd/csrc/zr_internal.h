@@ -230,7 +230,7 @@ enum StatusWord : uint32_t {
     kStJobsDenied = 11,     // draws whose tile jobs did not fit DrawParams::job_pad / job_slots (since the last sync)
     kStJobs = 12,           // tile jobs of the last draw beyond one per tile
     kStSlabSlot0 = 16,      // [kSlabSlots]: the slab target (bin_slab_target) of the draw given slot i (DrawParams::stat_slot)
-    kStPoolSlot0 = 64,      // [kSlabSlots]: the pool entries that draw's runs asked for (saturating)
+    kStPoolSlot0 = 64,      // [kSlabSlots]: the pool that draw's runs need (sub-pools x the fullest one's asks; saturating)
     kStMaxSlot0 = 112,      // [kSlabSlots]: that draw's longest tile list
     kStJobBufSlot0 = 160,   // [kSlabSlots]: the tile-job key buffers that draw's split tiles needed (0: no jobs built)
     kStJobPartSlot0 = 208,  // [kSlabSlots]: ... and the most parts (jobs past the first) it put on one XCD
@@ -242,16 +242,24 @@ enum CounterWord : uint32_t {
     kCtSetup = 0, kCtDropped = 1,
     kCtMaxTile = 2,   // the largest tile list of the draw (pairs, including any past the slab)
     kCtPairs = 4,     // u64 (words 4-5): (tile, primitive) pairs of the draw
-    kCtSchedTicket = 6,  // k_setup_bin workgroups past phase 2 (the last one builds the tile schedule)
+    kCtSchedTicket = 6,  // k_setup_bin ticket groups past phase 2 (the last group's last workgroup builds the schedules)
     kCtMicro = 7,        // covered micro primitives of the draw (DrawParams::micro)
-    kCtPoolTop = 8,      // u64 (words 8-9): pool entries the draw's runs asked for (the bump allocator; may pass pool_cap)
     kCtPoolRuns = 10,    // pool runs the draw registered
     kCtJobsDenied = 11,  // 1: the draw's tile jobs did not fit (build_job_schedule)
     kCtJobs = 12,        // tile jobs of the draw beyond one per tile
     kCtJobBufs = 13,     // key buffers the draw's split tiles needed (build_job_schedule; fitting or not)
     kCtJobXcdMax = 14,   // the most parts of the draw on one XCD (build_job_schedule)
-    kCtWords = 32,
+    // Words each on a 64-B line of its own, kCtSpread apart (one returning atomic
+    // per workgroup on a shared word queues the 256 workgroups on it at the memory
+    // side: ~90 ns apiece, docs/EXPERIMENTS.md round 6):
+    kCtPoolSub0 = 32,    // u64 x kPoolSubs: entries the runs of sub-pool k asked for (its bump allocator; may pass its size)
+    kCtTicketGroup0 = kCtPoolSub0 + 16 * 16,  // x kTicketGroups: workgroups of ticket group g past phase 2
+    kCtWords = kCtTicketGroup0 + 16 * 16,
 };
+constexpr uint32_t kCtSpread = 16;      // words between the spread counters (64 B)
+constexpr uint32_t kPoolSubs = 16;      // pool regions, each the bump allocator of workgroups w % kPoolSubs
+constexpr uint32_t kTicketGroup = 16;   // workgroups per ticket group (w / kTicketGroup)
+static_assert(kMaxRunsPerTile / kTicketGroup <= 16u, "ticket-group words for the largest setup grid");
 // draw_info words (written by k_setup_bin for k_tile)
 enum DrawInfoWord : uint32_t {
     kInfoRecords = 0,     // setup records the overflow scan covers (bboxes[0, n))
@@ -353,7 +361,7 @@ struct DrawParams {
     uint32_t micro;
     // Overflow runs: a workgroup whose run of pairs for tile t does
     // not fit what is left of t's slab stores it in the pool instead,
-    // bins[pool_off + base, + its pairs) from a bump allocator (kCtPoolTop), and
+    // bins[pool_off + base, + its pairs) from a bump allocator (kCtPoolSub0, pool_commit), and
     // registers (pool_off + base, pairs) in runs[t * run_cap + w], w its
     // workgroup index (slots of other workgroups hold length 0).  The run that
     // straddles the slab end records its offset, the slab's fill (kRunFill); a run

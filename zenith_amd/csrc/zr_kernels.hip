@@ -993,32 +993,38 @@ __device__ __noinline__ void build_job_schedule(const DrawParams& P, uint32_t nt
     uint32_t* s_tot = s_buf + 8;   // [0] key buffers (jobs of split tiles), [1] buffer cursor, [2] denied, [3] split tiles
     if (tid < 16u) s_buf[tid] = 0u;
     __syncthreads();
-    // pass 1: every tile's job count, parked in job_slot[t] (this thread reads it
-    // back in pass 2), and the parts each XCD gets
-    // (batches of 4 tiles per thread, their loads in flight together: one at a
-    // time, c3x's 8160 tiles kept this last workgroup ~10 us)
-    constexpr uint32_t kB = 4;
-    for (uint32_t t0 = tid; t0 < nt; t0 += kB * kSetupThreads) {
-        uint32_t c[kB], w[kB];
+    // pass 1: every tile's job count, kept in this thread's registers for pass 2
+    // (tiles tid + k * kSetupThreads), and the parts each XCD gets; loads in
+    // batches of kB in flight together (one tile at a time, and the counts parked
+    // in job_slot and read back, kept this last workgroup ~11 us at 8160 tiles;
+    // all 16 at once took 120 VGPRs, which every k_setup_bin instance reserves)
+    constexpr uint32_t kPer = kMaxTilesPerPass / kSetupThreads, kB = 4;
+    uint32_t K[kPer];
+#pragma unroll
+    for (uint32_t k0 = 0; k0 < kPer; k0 += kB) {
+        uint32_t c[kB], rw[kB];
+        if (tid + k0 * kSetupThreads >= nt) {
+#pragma unroll
+            for (uint32_t k = 0; k < kB; ++k) K[k0 + k] = 1u;
+            continue;
+        }
 #pragma unroll
         for (uint32_t k = 0; k < kB; ++k) {
-            const uint32_t t = t0 + k * kSetupThreads;
+            const uint32_t t = tid + (k0 + k) * kSetupThreads;
             c[k] = t < nt ? __hip_atomic_load(&P.tile_counts[t], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) : 0u;
         }
 #pragma unroll
         for (uint32_t k = 0; k < kB; ++k) {
-            const uint32_t t = t0 + k * kSetupThreads;
-            w[k] = (c[k] & kCountRuns) ? __hip_atomic_load(&P.run_counts[t], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) : 0u;
+            const uint32_t t = tid + (k0 + k) * kSetupThreads;
+            rw[k] = (c[k] & kCountRuns) ? __hip_atomic_load(&P.run_counts[t], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) : 0u;
         }
 #pragma unroll
         for (uint32_t k = 0; k < kB; ++k) {
-            const uint32_t t = t0 + k * kSetupThreads;
-            if (t >= nt) continue;
-            const uint32_t K = tile_jobs(c[k] & ~kCountRuns, w[k], J);
-            P.job_slot[t] = K;
-            if (K > 1u) {
-                atomicAdd(&s_cnt[xcd_block(t, nt) & 7u], K - 1u);
-                atomicAdd(&s_tot[0], K);
+            const uint32_t t = tid + (k0 + k) * kSetupThreads;
+            K[k0 + k] = t < nt ? tile_jobs(c[k] & ~kCountRuns, rw[k], J) : 1u;
+            if (K[k0 + k] > 1u) {
+                atomicAdd(&s_cnt[xcd_block(t, nt) & 7u], K[k0 + k] - 1u);
+                atomicAdd(&s_tot[0], K[k0 + k]);
                 atomicAdd(&s_tot[3], 1u);
             }
         }
@@ -1047,14 +1053,15 @@ __device__ __noinline__ void build_job_schedule(const DrawParams& P, uint32_t nt
     }
     if (tid == 0 && ok && s_tot[0]) atomicAdd(&P.counters[kCtJobs], s_tot[0] - s_tot[3]);  // (jobs beyond one per tile)
     __syncthreads();
-    // pass 2: key slots and part items (same thread -> tile mapping as pass 1)
-    for (uint32_t t = tid; ok && t < nt; t += kSetupThreads) {
-        const uint32_t K = P.job_slot[t];
-        if (K <= 1u) continue;
+    // pass 2: key slots (k_tile reads job_slot[t] of split tiles only) and part items
+#pragma unroll
+    for (uint32_t k = 0; k < kPer; ++k) {
+        const uint32_t t = tid + k * kSetupThreads;
+        if (!ok || K[k] <= 1u) continue;
         const uint32_t x = xcd_block(t, nt) & 7u;
-        P.job_slot[t] = atomicAdd(&s_tot[1], K);  // (K key buffers, one per job)
-        const uint32_t l0 = atomicAdd(&s_cnt[x], K - 1u);
-        for (uint32_t p = 1; p < K; ++p) P.tile_order[(l0 + p - 1u) * 8u + x] = t | (p << kJobTileBits);
+        P.job_slot[t] = atomicAdd(&s_tot[1], K[k]);  // (K key buffers, one per job)
+        const uint32_t l0 = atomicAdd(&s_cnt[x], K[k] - 1u);
+        for (uint32_t p = 1; p < K[k]; ++p) P.tile_order[(l0 + p - 1u) * 8u + x] = t | (p << kJobTileBits);
     }
     for (uint32_t i = tid; i < P.job_pad; i += kSetupThreads)  // the spare part blocks
         if ((i >> 3) >= s_cnt[16 + (i & 7u)]) P.tile_order[i] = kJobNone;
@@ -1116,16 +1123,26 @@ __device__ __noinline__ uint32_t pool_run(const DrawParams& P, uint32_t t, uint3
     return kPoolPending | atomicAdd(&s_pool[0], c);
 }
 
-// After phase 2's tile loop (same thread -> tile mapping): the workgroup's pool
-// runs take one allocation of s_pool[0] entries; each pending cursor becomes its
-// run's position, or kDropCursor (and the tile's kRunDropped) when the pool is full.
+// After phase 2's tile loop: the workgroup's pool runs take one allocation of
+// s_pool[0] entries from its sub-pool (pool_subs); each pending cursor becomes its
+// run's position, or kDropCursor (and the tile's kRunDropped) when the sub-pool is
+// full.
+__device__ __forceinline__ uint32_t pool_subs(const DrawParams& P) { return min(kPoolSubs, max(P.setup_wgs, 1u)); }
+
+// The pool is kPoolSubs regions of pool_cap / subs entries (the remainder unused),
+// region k the bump allocator of workgroups w % subs: one allocator for all 256
+// workgroups queued their returning atomics on one word (c2x: phase 2 +8.7 us on
+// average, the last workgroup's ticket 22 us late).  A workgroup's draw is a
+// random sample of the primitives, so the regions fill alike; k_tile reports subs
+// x the fullest region's requests as the pool the draw needs.
 __device__ __noinline__ void pool_commit(const DrawParams& P, uint32_t* s_hist, uint32_t* s_pool, uint32_t rot,
                                          uint32_t w) {
     const uint32_t nt = P.ntiles, tid = threadIdx.x;
     if (tid == 0) {
-        const unsigned long long base =
-            atomicAdd(reinterpret_cast<unsigned long long*>(&P.counters[kCtPoolTop]), (unsigned long long)s_pool[0]);
-        s_pool[2] = base + s_pool[0] <= P.pool_cap ? P.pool_off + (uint32_t)base : kDropCursor;
+        const uint32_t subs = pool_subs(P), k = w % subs, size = P.pool_cap / subs;
+        const unsigned long long base = atomicAdd(
+            reinterpret_cast<unsigned long long*>(&P.counters[kCtPoolSub0 + k * kCtSpread]), (unsigned long long)s_pool[0]);
+        s_pool[2] = base + s_pool[0] <= size ? P.pool_off + k * size + (uint32_t)base : kDropCursor;
         atomicAdd(&P.counters[kCtPoolRuns], s_pool[1]);
     }
     __syncthreads();
@@ -1315,13 +1332,26 @@ __global__ __launch_bounds__(kSetupThreads) void k_setup_bin(DrawParams P) {
             // the memory side, and every one of this workgroup's has completed before
             // its ticket (returned, or drained by the wait below); the schedule reads
             // them back with atomics too, so no L2 holds a stale copy in between.
+            // Tickets in two levels: a workgroup takes one in its group of
+            // kTicketGroup (w / kTicketGroup, a word of its own), the group's last
+            // one a ticket of the groups; the last group's last workgroup builds.
+            // (One word for all 256 queued their returning atomics on it.)  The
+            // chain keeps the order argument: every workgroup's atomics precede its
+            // group ticket, which precedes its group's ticket of the groups.
             asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
             __syncthreads();
-            if (tid == 0)
-                s_misc[5] = __hip_atomic_fetch_add(&P.counters[kCtSchedTicket], 1u, __ATOMIC_RELAXED,
-                                                   __HIP_MEMORY_SCOPE_AGENT);
+            if (tid == 0) {
+                const uint32_t g = w / kTicketGroup, gsize = min(kTicketGroup, G - g * kTicketGroup);
+                const uint32_t gt = __hip_atomic_fetch_add(&P.counters[kCtTicketGroup0 + g * kCtSpread], 1u,
+                                                           __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                uint32_t last = 0u;
+                if (gt == gsize - 1u)
+                    last = __hip_atomic_fetch_add(&P.counters[kCtSchedTicket], 1u, __ATOMIC_RELAXED,
+                                                  __HIP_MEMORY_SCOPE_AGENT) == (G + kTicketGroup - 1u) / kTicketGroup - 1u;
+                s_misc[5] = last;
+            }
             __syncthreads();
-            if (s_misc[5] == G - 1u) {
+            if (s_misc[5]) {
                 if (P.job_entries) build_job_schedule(P, nt, s_sched);
                 if (P.tile_sched) build_tile_schedule(P, nt, s_sched, P.tile_order + (P.job_entries ? P.job_pad : 0u));
             }
@@ -2500,7 +2530,16 @@ __global__ __launch_bounds__(NT, kTileWgs * kTileThreads / 256) void k_tile(Draw
     if (blockIdx.x == jp && threadIdx.x == 0) {  // (jp: the first tile block; part blocks before it may be spare)
         uint32_t* st = P.status;
         const unsigned long long pairs = *reinterpret_cast<const unsigned long long*>(&P.counters[kCtPairs]);
-        const unsigned long long pool = *reinterpret_cast<const unsigned long long*>(&P.counters[kCtPoolTop]);
+        // pool: what the runs asked for; need: subs x the fullest sub-pool's asks,
+        // which passes pool_cap exactly when a sub-pool dropped a run (pool_commit)
+        unsigned long long pool = 0ull, need_sub = 0ull;
+        const uint32_t subs = pool_subs(P);
+        for (uint32_t k = 0; k < subs; ++k) {
+            const unsigned long long a = *reinterpret_cast<const unsigned long long*>(&P.counters[kCtPoolSub0 + k * kCtSpread]);
+            pool += a;
+            need_sub = max(need_sub, a);
+        }
+        const unsigned long long pool_need = need_sub * subs;
         st[kStTrianglesSetup] = P.counters[kCtSetup];
         st[kStDroppedClip] = P.counters[kCtDropped];
         st[kStMicro] = P.counters[kCtMicro];
@@ -2513,8 +2552,8 @@ __global__ __launch_bounds__(NT, kTileWgs * kTileThreads / 256) void k_tile(Draw
             st[kStJobsDenied] = jd + 1u;
         }
         const uint32_t target = bin_slab_target(pairs, P.ntiles);
-        if (pool > P.pool_cap) {  // a dropped run: the buffer this draw asks for (read-modify-write only here)
-            const unsigned long long need = (unsigned long long)P.ntiles * target + pool;
+        if (pool_need > P.pool_cap) {  // a dropped run: the buffer this draw asks for (read-modify-write only here)
+            const unsigned long long need = (unsigned long long)P.ntiles * target + pool_need;
             const uint32_t need32 = need > 0x80000000ull ? 0x80000000u : (uint32_t)need;
             const uint32_t ov = st[kStOverflow], bn = st[kStBinNeed];
             st[kStOverflow] = ov + 1u;
@@ -2522,7 +2561,7 @@ __global__ __launch_bounds__(NT, kTileWgs * kTileThreads / 256) void k_tile(Draw
         }
         if (P.stat_slot < kSlabSlots) {  // (the runtime derives the buffer the draw asks for from these)
             st[kStSlabSlot0 + P.stat_slot] = target;
-            st[kStPoolSlot0 + P.stat_slot] = pool > 0xFFFFFFFFull ? 0xFFFFFFFFu : (uint32_t)pool;
+            st[kStPoolSlot0 + P.stat_slot] = pool_need > 0xFFFFFFFFull ? 0xFFFFFFFFu : (uint32_t)pool_need;
             st[kStMaxSlot0 + P.stat_slot] = P.counters[kCtMaxTile];
             st[kStJobBufSlot0 + P.stat_slot] = P.counters[kCtJobBufs];
             st[kStJobPartSlot0 + P.stat_slot] = P.counters[kCtJobXcdMax];
