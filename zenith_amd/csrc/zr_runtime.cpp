@@ -213,7 +213,7 @@ struct ScratchSet {
     uint64_t runs_cap = 0;
     uint32_t* run_counts = nullptr;  // [ntiles] (zero between draws: k_tile resets it)
     uint64_t run_counts_cap = 0;
-    uint32_t* tile_order = nullptr;  // k_tile's block -> tile schedule (k_setup_bin's last workgroup writes it)
+    uint32_t* tile_order = nullptr;  // k_tile's block -> tile schedule (k_setup_bin's schedule_builder writes it)
     uint32_t* job_slot = nullptr;    // tile jobs (DrawParams::job_entries): key slot per split tile
     uint64_t job_slot_cap = 0;
     unsigned long long* job_keys = nullptr;  // [slots][kTilePixels] per-job key buffers
@@ -1128,9 +1128,9 @@ zr_result exec_draw(zr_device* d, ExecState& s, const Cmd& c, bool indexed) {
     ScratchSet& S = d->sets[overlap ? d->cur_set : 0];
     if (overlap) d->cur_set = (d->cur_set + 1u) % kScratchSets;
     if ((rc = ensure_scratch(d, S, P))) return rc;
-    // (a phase-1-only timing run never reaches the last workgroup's ticket, so it
-    // writes no schedule: k_tile then keeps xcd_tile order instead of reading an
-    // unwritten one)
+    // (a phase-1-only timing run takes no tickets, so it has no schedule -- its
+    // schedule_builder would wait forever -- and k_tile keeps xcd_tile order
+    // instead of reading an unwritten one)
     P.tile_sched = sched && !(d->debug & kDebugPhase1Only) ? 1u : 0u;
     if ((sched || P.job_entries) && !(d->debug & kDebugPhase1Only)) {
         if ((rc = grow(d, S.tile_order, S.tile_order_cap, (uint64_t)P.ntiles + P.job_pad, 4))) return rc;
