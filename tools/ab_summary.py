@@ -15,6 +15,11 @@ for f in sorted(glob.glob(os.path.join(d, "*.json"))):
     except (ValueError, IndexError):
         continue
     rows[(c, v)].append(j)
+for js in rows.values():  # --emulate-shard lines: the slowest rank's frame and kernels
+    for j in js:
+        if "max_rank_ms" in j:
+            j["ms_per_step"] = j["max_rank_ms"]
+            j["kernels"] = {k: {"avg_us": u} for k, u in j["ranks"][j["max_rank"]]["kernels_us"].items()}
 for (c, v), js in sorted(rows.items()):
     ms = statistics.median(j["ms_per_step"] for j in js) * 1e3
     ks = {k: statistics.median(j["kernels"][k]["avg_us"] for j in js) for k in js[0]["kernels"]}
