@@ -841,10 +841,11 @@ def test_partitioned_beside_busy_stream():
 
 
 def test_mixed_draw_sizes_no_sync(device):
-    """A draw above 2^18 primitives (setup on the main stream, scratch set 0)
-    followed by small draws (setup on the setup stream, alternating sets)
-    with no host sync in between: every target equals its own oracle frame."""
-    big = scenes.soup_scene(79, 300_000, 640, 480, 3.0, scenes.PROGRAM_BLINN_PHONG)
+    """A draw above 2^18 primitives and one per pixel (setup on the main stream,
+    scratch set 0) followed by small draws (setup on the setup stream,
+    alternating sets) with no host sync in between: every target equals its own
+    oracle frame."""
+    big = scenes.soup_scene(79, 400_000, 640, 480, 3.0, scenes.PROGRAM_BLINN_PHONG)
     small = [scenes.soup_scene(80 + i, 2000 + 1000 * i, 320, 240, 9.0, scenes.PROGRAM_FLAT_COLOR) for i in range(3)]
     jobs = []
     for s in [big] + small:
@@ -859,6 +860,37 @@ def test_mixed_draw_sizes_no_sync(device):
     device.wait_idle()
     for s, _, enc, color, depth in jobs:
         oc, od = oracle.render(s)
+        assert np.array_equal(color.read(), oc), s.name
+        assert np.array_equal(depth.read().view(np.uint32), od.view(np.uint32)), s.name
+        enc.destroy()
+        color.destroy()
+        depth.destroy()
+
+
+def test_overlapped_large_draws_no_sync(device):
+    """Draws above 2^18 primitives but below one per pixel set up beside the
+    previous draw's tile pass (use_overlap_setup: the setup stream, alternating
+    scratch sets).  Back to back, twice, with no host sync: the clustered c2x
+    (tile jobs, pool runs, the schedule workgroup), a uniform soup, a draw above
+    one primitive per pixel (main stream) between them -- every target equals its
+    own oracle frame."""
+    todo = [scenes.config_scene("c2x"),
+            scenes.soup_scene(91, 400_000, 1280, 720, 5.0, scenes.PROGRAM_BLINN_PHONG),
+            scenes.soup_scene(92, 400_000, 640, 480, 3.0, scenes.PROGRAM_FLAT_COLOR),
+            scenes.soup_scene(93, 300_000, 800, 600, 4.0, scenes.PROGRAM_FLAT_COLOR)]
+    jobs = []
+    for s in todo:
+        color = rhi.Texture(device, rhi.TextureDesc.new_color("rt", s.width, s.height, s.color_format))
+        depth = rhi.Texture(device, rhi.TextureDesc.new_depth("ds", s.width, s.height))
+        r = renderer.SceneRenderer(device, s)
+        enc = r.record(color, depth, encoder=rhi.CommandEncoder(device))
+        jobs.append((s, r, enc, color, depth))
+    for _ in range(2):
+        for _, _, enc, _, _ in jobs:
+            device.submit(enc)
+    device.wait_idle()
+    for s, _, enc, color, depth in jobs:
+        oc, od = oracle.render(s, nthreads=16)
         assert np.array_equal(color.read(), oc), s.name
         assert np.array_equal(depth.read().view(np.uint32), od.view(np.uint32)), s.name
         enc.destroy()

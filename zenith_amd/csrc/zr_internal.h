@@ -242,7 +242,7 @@ enum CounterWord : uint32_t {
     kCtSetup = 0, kCtDropped = 1,
     kCtMaxTile = 2,   // the largest tile list of the draw (pairs, including any past the slab)
     kCtPairs = 4,     // u64 (words 4-5): (tile, primitive) pairs of the draw
-    kCtSchedTicket = 6,  // k_setup_bin ticket groups past phase 2 (schedule_builder waits for all of them)
+    kCtSchedTicket = 6,  // k_setup_bin ticket groups past phase 2 (the last group's last workgroup builds the schedules)
     kCtMicro = 7,        // covered micro primitives of the draw (DrawParams::micro)
     kCtPoolRuns = 10,    // pool runs the draw registered
     kCtJobsDenied = 11,  // 1: the draw's tile jobs did not fit (build_job_schedule)
@@ -351,7 +351,7 @@ struct DrawParams {
     uint32_t bin_stage;       // k_setup_bin phase 4: LDS staging capacity in pairs (0: scatter straight to the bins)
     uint32_t debug;           // kDebug* bits (timing experiments only)
     unsigned long long* dbg_ts; // [setup_wgs][8] s_memrealtime stamps (kDebugStamps only)
-    uint32_t* tile_order;     // tile schedule (k_setup_bin's schedule_builder -> k_tile), or nullptr: xcd_tile order
+    uint32_t* tile_order;     // tile schedule (k_setup_bin's last workgroup -> k_tile), or nullptr: xcd_tile order
     uint32_t* win_bits;       // winner census (zr_device_set_profiling level 2): bit p = draw primitive p won a pixel
     uint32_t* status;         // host-mapped
     // Micro primitives: k_setup_bin tests a primitive whose clipped
@@ -373,7 +373,7 @@ struct DrawParams {
     uint32_t* run_counts;     // [ntiles] run word (kRunFill, kRunDropped; zero between draws: k_tile resets it)
     // Tile jobs: a list longer than job_entries is split into
     // jobs of job_entries entries, each its own k_tile block (tile_order items
-    // t | part << kJobTileBits, built by k_setup_bin's schedule_builder), which
+    // t | part << kJobTileBits, built by k_setup_bin's last workgroup), which
     // store their keys to job_keys[job_slot[t] + part]; the last job of the tile
     // (job_tickets) folds them in with a min and resolves it.  job_entries 0: off.
     // tile_order: [0, job_pad) parts 1.. (and spare kJobNone blocks), then the
@@ -400,7 +400,7 @@ struct DrawParams {
 // G): G=4 tile pass 44 -> 39 us, G=8 40 -> 33 us; 16 waves per tile was slower
 // than 4 (61 / 43 us), so it is not built.
 // k_setup_bin LDS words besides the two tile arrays: misc (32) + list prefix (64)
-// + the tile schedule's per-XCD bucket counts (8 x 64, schedule_builder only).
+// + the tile schedule's per-XCD bucket counts (8 x 64, the last workgroup only).
 constexpr uint32_t kSchedBuckets = 64;
 constexpr uint32_t kSetupMiscWords = 96 + 8 * kSchedBuckets;
 // A draw of fewer than 32 primitives per tile (cerberus at 1080p: 16) also gets 8
@@ -522,6 +522,14 @@ inline bool use_tile_schedule(uint32_t ntiles, uint32_t cus, uint32_t tile_threa
                               uint32_t tile_shift = kTileShift) {
     const uint64_t slots = (uint64_t)cus * (8u * kTileThreads / tile_threads);
     return ntiles > slots && 32ull * prims < ((uint64_t)ntiles << (2u * tile_shift));  // (< 1/32 primitive per pixel)
+}
+
+// Draw i+1's setup beside draw i's tile pass (zr_device_t::setup_overlap): small
+// draws, tile-row shards, and draws of fewer primitives than pixels -- not a
+// draw whose HBM-bound setup is the frame (C4's 4.8 per pixel: +28 % beside its
+// tile pass; C2 -11 %, C3 -5 %, docs/EXPERIMENTS.md round 6).
+inline bool use_overlap_setup(uint64_t prims, uint32_t w, uint32_t h, uint32_t shards) {
+    return prims <= (1u << 18) || shards > 1 || prims < (uint64_t)w * h;
 }
 
 // A measured draw shape is crowded when its longest list needed tile jobs and is

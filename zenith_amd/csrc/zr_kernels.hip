@@ -926,8 +926,8 @@ __device__ __forceinline__ uint32_t xcd_block(uint32_t t, uint32_t n) {
     return ((R >> 3) * K + o) * 8u + (R & 7u);
 }
 
-// Tile schedule (longest-processing-time first): built by k_setup_bin's
-// schedule_builder once every binning workgroup is past phase 2 (every tile's count final).  Each tile keeps the
+// Tile schedule (longest-processing-time first): built by the last k_setup_bin
+// workgroup past phase 2, when every tile's count is final.  Each tile keeps the
 // XCD xcd_tile gives it (block % 8), but within an XCD the blocks take its tiles
 // heaviest list first, so the hardware, which dispatches blocks in order as slots
 // free up, starts the long tiles first and ends the pass on short ones (the
@@ -971,7 +971,7 @@ __device__ void build_tile_schedule(const DrawParams& P, uint32_t nt, uint32_t* 
     }
 }
 
-// Tile jobs (DrawParams::job_entries), built by the same schedule_builder.  A
+// Tile jobs (DrawParams::job_entries), built by the same last workgroup.  A
 // tile whose list is longer than J (and takes no record scan) becomes
 // K = ceil(count / J) jobs, part p covering list entries [p J, (p + 1) J), with
 // K key buffers from job_slot[t].  Part 0 keeps the tile's block in the usual
@@ -996,7 +996,7 @@ __device__ __noinline__ void build_job_schedule(const DrawParams& P, uint32_t nt
     // pass 1: every tile's job count, kept in this thread's registers for pass 2
     // (tiles tid + k * kSetupThreads), and the parts each XCD gets; loads in
     // batches of kB in flight together (one tile at a time, and the counts parked
-    // in job_slot and read back, took ~11 us at 8160 tiles;
+    // in job_slot and read back, kept this last workgroup ~11 us at 8160 tiles;
     // all 16 at once took 120 VGPRs, which every k_setup_bin instance reserves)
     constexpr uint32_t kPer = kMaxTilesPerPass / kSetupThreads, kB = 4;
     uint32_t K[kPer];
@@ -1167,41 +1167,14 @@ __device__ __noinline__ void pool_commit(const DrawParams& P, uint32_t* s_hist, 
 // blocks per workgroup measured slower: C4 setup 286 vs 339 us).
 __device__ __forceinline__ uint32_t own_unit(uint32_t w, uint32_t G, uint32_t i) { return w + i * G; }
 
-// The schedules (tile jobs, tile schedule) need every tile's final count, known
-// only when the last binning workgroup is past phase 2.  Built by that last
-// workgroup, they delayed its phase 4 and so the kernel's end (c2x: ~9 us of
-// schedule, then ~11 us of phase 4, the last workgroup ending ~15 us after the
-// average one).  Instead a draw with a schedule launches one workgroup more,
-// w == setup_wgs, which bins nothing: it waits until every ticket group is done
-// and builds the schedules while the binning workgroups scatter.  It waits for no
-// workgroup that waits for anything (they never wait), so it cannot stall them:
-// until one of them ends and frees a CU's LDS it is not even resident.  The
-// tickets' order argument holds: each group's count follows the atomics of all
-// its workgroups, and this reads the counts with atomics after the last one.
-__device__ __forceinline__ void schedule_builder(const DrawParams& P, uint32_t nt, uint32_t* s_sched) {
-    const uint32_t groups = (P.setup_wgs + kTicketGroup - 1u) / kTicketGroup;
-    if (threadIdx.x == 0)
-        while (__hip_atomic_load(&P.counters[kCtSchedTicket], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) < groups)
-            __builtin_amdgcn_s_sleep(8);
-    __syncthreads();
-    if (P.job_entries) build_job_schedule(P, nt, s_sched);
-    if (P.tile_sched) build_tile_schedule(P, nt, s_sched, P.tile_order + (P.job_entries ? P.job_pad : 0u));
-}
-
 template <uint32_t KB, bool MESH>
 __global__ __launch_bounds__(kSetupThreads) void k_setup_bin(DrawParams P) {
     extern __shared__ __attribute__((aligned(16))) uint32_t s_lds[];  // [ntiles (16-B padded) + kSetupMiscWords] + bboxes
-    const uint32_t nt = P.ntiles, G = P.setup_wgs, w = blockIdx.x, tid = threadIdx.x;  // (G: the binning workgroups)
-    if (w == G) {  // the extra workgroup of a draw with a schedule (launch_setup_bin)
-        // (kernarg_params: a call taking the parameter itself copies all of it to
-        // the stack in every workgroup, which then read it from there: phase 1 2x)
-        schedule_builder(kernarg_params(), nt, s_lds + ((nt + 3u) & ~3u) + 32 + 96);  // (s_sched below)
-        return;
-    }
+    const uint32_t nt = P.ntiles, G = gridDim.x, w = blockIdx.x, tid = threadIdx.x;
     uint32_t* s_hist = s_lds;                       // histogram -> cursors
     uint32_t* s_misc = s_hist + ((nt + 3u) & ~3u);  // [32]
     uint32_t* s_pre = s_misc + 32;       // records mode: exclusive prefix of the received blocks' counts
-    uint32_t* s_sched = s_misc + 96;     // [8 x kSchedBuckets] the tile schedule (schedule_builder)
+    uint32_t* s_sched = s_misc + 96;     // [8 x kSchedBuckets] the tile schedule (last workgroup)
     // this workgroup's primitives' tile bboxes, indexed like phase 4's flattened
     // (own unit, primitive in unit) space, when they fit (P.bbox_lds)
     BBox* s_bbox = reinterpret_cast<BBox*>(s_misc + kSetupMiscWords);
@@ -1252,7 +1225,10 @@ __global__ __launch_bounds__(kSetupThreads) void k_setup_bin(DrawParams P) {
     if (w == 0 && tid == 0) {
         P.draw_info[kInfoRecords] = MESH ? kMeshFans * n_pos : n_pos;
         P.draw_info[kInfoByPosition] = rec_mode ? 1u : 0u;
-        P.draw_info[kInfoJobEntries] = 0u;  // (build_job_schedule sets it, after this store: the ticket orders them)
+        // (kInfoJobEntries: build_job_schedule's alone.  A store of 0 here raced with
+        // it -- plain stores of two workgroups, possibly in two XCDs' L2s, written
+        // back at the kernel's end in either order -- and k_tile reads it only for
+        // draws with tile jobs, whose schedule always writes it.)
     }
 
     // ---- phase 1
@@ -1353,21 +1329,34 @@ __global__ __launch_bounds__(kSetupThreads) void k_setup_bin(DrawParams P) {
             pool_commit(P, s_hist, s_misc + 8, rot, w);
             __syncthreads();
         }
-        if (P.tile_order) {  // (the tile schedule and / or tile jobs: schedule_builder waits for the tickets)
+        if (P.tile_order) {  // (the tile schedule and / or tile jobs)
+            // The last workgroup to take a ticket sees every tile's final count: the
+            // counts and the max are only ever changed by atomics, which execute at
+            // the memory side, and every one of this workgroup's has completed before
+            // its ticket (returned, or drained by the wait below); the schedule reads
+            // them back with atomics too, so no L2 holds a stale copy in between.
             // Tickets in two levels: a workgroup takes one in its group of
             // kTicketGroup (w / kTicketGroup, a word of its own), the group's last
-            // one adds to the count of groups done.  (One word for all 256 queued
-            // their returning atomics on it.)  Every workgroup's atomics have
-            // completed before its ticket (returned, or drained by the wait below),
-            // its ticket before its group's count.
+            // one a ticket of the groups; the last group's last workgroup builds.
+            // (One word for all 256 queued their returning atomics on it.)  The
+            // chain keeps the order argument: every workgroup's atomics precede its
+            // group ticket, which precedes its group's ticket of the groups.
             asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
             __syncthreads();
             if (tid == 0) {
                 const uint32_t g = w / kTicketGroup, gsize = min(kTicketGroup, G - g * kTicketGroup);
                 const uint32_t gt = __hip_atomic_fetch_add(&P.counters[kCtTicketGroup0 + g * kCtSpread], 1u,
                                                            __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                uint32_t last = 0u;
                 if (gt == gsize - 1u)
-                    __hip_atomic_fetch_add(&P.counters[kCtSchedTicket], 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                    last = __hip_atomic_fetch_add(&P.counters[kCtSchedTicket], 1u, __ATOMIC_RELAXED,
+                                                  __HIP_MEMORY_SCOPE_AGENT) == (G + kTicketGroup - 1u) / kTicketGroup - 1u;
+                s_misc[5] = last;
+            }
+            __syncthreads();
+            if (s_misc[5]) {
+                if (P.job_entries) build_job_schedule(P, nt, s_sched);
+                if (P.tile_sched) build_tile_schedule(P, nt, s_sched, P.tile_order + (P.job_entries ? P.job_pad : 0u));
             }
         }
     }
@@ -2430,7 +2419,9 @@ __global__ __launch_bounds__(NT, kTileWgs * kTileThreads / 256) void k_tile(Draw
     const uint32_t b = ((tile_debug(P) & kDebugReverseTiles) && blockIdx.x >= jp) ? jp + (gridDim.x - 1u - blockIdx.x)
                                                                                    : blockIdx.x;
     const uint32_t item = (b < jp || P.tile_sched) ? P.tile_order[b] : xcd_tile(b - jp, P.ntiles);
-    if (item == kJobNone) return;
+    // (a tile past the draw's would be a schedule bug: a wrong image the parity
+    // tests see, not an access outside the buffers)
+    if (item == kJobNone || (item & kJobTileMask) >= P.ntiles) return;
     const uint32_t t = item & kJobTileMask, part = item >> kJobTileBits;
     uint32_t tx, ty;
     shard_tile_xy(shard_geom(P), t, tx, ty);
@@ -2969,15 +2960,14 @@ const void* setup_bin_kernel(uint32_t batch, bool mesh) {
 void launch_setup_bin(const DrawParams& p, void* stream) {
     const size_t lds = setup_bin_lds_bytes(p.ntiles, p.bbox_lds, p.bin_stage);
     const hipStream_t s = (hipStream_t)stream;
-    const dim3 grid(p.setup_wgs + (p.tile_order ? 1u : 0u));  // (+ schedule_builder)
     if (p.program == kProgMesh) {  // batch 1: the clip path is heavy
-        hipLaunchKernelGGL((k_setup_bin<1, true>), grid, dim3(kSetupThreads), lds, s, p);
+        hipLaunchKernelGGL((k_setup_bin<1, true>), dim3(p.setup_wgs), dim3(kSetupThreads), lds, s, p);
         return;
     }
     switch (p.setup_batch) {
-    case 1: hipLaunchKernelGGL((k_setup_bin<1, false>), grid, dim3(kSetupThreads), lds, s, p); break;
-    case 2: hipLaunchKernelGGL((k_setup_bin<2, false>), grid, dim3(kSetupThreads), lds, s, p); break;
-    default: hipLaunchKernelGGL((k_setup_bin<4, false>), grid, dim3(kSetupThreads), lds, s, p); break;
+    case 1: hipLaunchKernelGGL((k_setup_bin<1, false>), dim3(p.setup_wgs), dim3(kSetupThreads), lds, s, p); break;
+    case 2: hipLaunchKernelGGL((k_setup_bin<2, false>), dim3(p.setup_wgs), dim3(kSetupThreads), lds, s, p); break;
+    default: hipLaunchKernelGGL((k_setup_bin<4, false>), dim3(p.setup_wgs), dim3(kSetupThreads), lds, s, p); break;
     }
 }
 

@@ -213,7 +213,7 @@ struct ScratchSet {
     uint64_t runs_cap = 0;
     uint32_t* run_counts = nullptr;  // [ntiles] (zero between draws: k_tile resets it)
     uint64_t run_counts_cap = 0;
-    uint32_t* tile_order = nullptr;  // k_tile's block -> tile schedule (k_setup_bin's schedule_builder writes it)
+    uint32_t* tile_order = nullptr;  // k_tile's block -> tile schedule (k_setup_bin's last workgroup writes it)
     uint32_t* job_slot = nullptr;    // tile jobs (DrawParams::job_entries): key slot per split tile
     uint64_t job_slot_cap = 0;
     unsigned long long* job_keys = nullptr;  // [slots][kTilePixels] per-job key buffers
@@ -261,9 +261,13 @@ struct zr_device_t {
     // fills CUs draw i's tile pass frees.  Measured with round 1's two-launch
     // split setup (1 GPU): C1 (100k tris) 1180 -> 1274 Mtri/s, C2 7925 -> 8007,
     // C3 equal, C4 (10M) 25.1 -> 23.8 G (the co-running passes contend), so by
-    // default only draws of <= 2^18 primitives overlap, and tile-row shards (whose
+    // default only draws of <= 2^18 primitives overlapped, and tile-row shards (whose
     // tile pass leaves most CUs idle: C2 G=2/4/8 +2.8/+2.3/+0.7 %, C3 G=8 +7 %).
-    // ZR_SETUP_OVERLAP=0 / 1 forces it off / on.
+    // Re-measured with round 6's kernels (one setup workgroup per CU, slab
+    // binning, spread allocators; docs/EXPERIMENTS.md round 6): C2 107.7 -> 95.5 us per frame, C3
+    // 206.8 -> 196.9, c2x 155.2 -> 133.7, c3x 243.1 -> 216.5, but C4 316.9 -> 405.8
+    // (its HBM-bound setup is the frame).  So draws of fewer primitives than
+    // pixels overlap too (use_overlap_setup); ZR_SETUP_OVERLAP=0 / 1 forces it off / on.
     int setup_overlap = -1;
     int rec_table = -1;        // ZR_REC_TABLE=0/1 forces k_tile's record table (A/B); -1: use_record_table
     int tile_sched = -1;       // ZR_TILE_SCHED=0/1 forces the heaviest-first tile schedule (A/B); -1: use_tile_schedule
@@ -1080,7 +1084,7 @@ zr_result exec_draw(zr_device* d, ExecState& s, const Cmd& c, bool indexed) {
     }
     // k_setup_bin on the setup stream with two scratch sets (zr_device_t::setup_overlap);
     // not while debugging or with graph replay, whose captures bake in set 0
-    const bool overlap_setup = (d->setup_overlap > 0 || (d->setup_overlap < 0 && (prims <= (1u << 18) || P.shard_count > 1))) &&
+    const bool overlap_setup = (d->setup_overlap > 0 || (d->setup_overlap < 0 && use_overlap_setup(prims, P.fb_w, P.fb_h, P.shard_count))) &&
                        !d->use_graphs && !d->debug;
     // k_setup_bin phase 4 staged in LDS (pairs grouped by tile, stored run by run):
     // room for twice the workgroup's primitives, in the CU's LDS that setup owns
@@ -1128,9 +1132,9 @@ zr_result exec_draw(zr_device* d, ExecState& s, const Cmd& c, bool indexed) {
     ScratchSet& S = d->sets[overlap ? d->cur_set : 0];
     if (overlap) d->cur_set = (d->cur_set + 1u) % kScratchSets;
     if ((rc = ensure_scratch(d, S, P))) return rc;
-    // (a phase-1-only timing run takes no tickets, so it has no schedule -- its
-    // schedule_builder would wait forever -- and k_tile keeps xcd_tile order
-    // instead of reading an unwritten one)
+    // (a phase-1-only timing run never reaches the last workgroup's ticket, so it
+    // writes no schedule: k_tile then keeps xcd_tile order instead of reading an
+    // unwritten one)
     P.tile_sched = sched && !(d->debug & kDebugPhase1Only) ? 1u : 0u;
     if ((sched || P.job_entries) && !(d->debug & kDebugPhase1Only)) {
         if ((rc = grow(d, S.tile_order, S.tile_order_cap, (uint64_t)P.ntiles + P.job_pad, 4))) return rc;
