@@ -678,6 +678,12 @@ def main():
                      "frac": round(achieved / HBM_PEAK_GBPS, 4), "traffic": traffic,
                      "peak_source": "MI355X_MICROARCH.md measured float4 copy (SURVEY.md §8d)",
                      "peak_spec": HBM_SPEC_GBPS, "frac_spec": round(achieved / HBM_SPEC_GBPS, 4),
+                     # (the fragment pass's own figures, whichever kernel is the
+                     # dominant one: with setup overlapped, C2's setup spans longer)
+                     "tile_fields_note": "tile_*, *_per_pair, *_survey and design: k_tile over its own duration",
+                     "tile_achieved": kernels.get("tile", {}).get("gbps"),
+                     "tile_frac": (round(kernels["tile"]["gbps"] / HBM_PEAK_GBPS, 4)
+                                   if kernels.get("tile", {}).get("gbps") else None),
                      "alg_bytes_per_pair": BIN_ENTRY_BYTES + RECORD_BYTES,
                      "survey_bytes_per_pair": SURVEY_PAIR_BYTES,
                      "achieved_survey": achieved_survey,
